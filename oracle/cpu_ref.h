@@ -1,0 +1,89 @@
+/*
+ * cpu_ref.h -- CPU restatement (ORACLE) of the reference JPEG block-transform hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (jpeg-encoder-and-decoder_amd/) may
+ * include, link or call this.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg use it, and only as the checker / the timed CPU baseline.
+ *
+ * Restates, in plain C99 with IEEE double arithmetic in the reference's exact operation
+ * order (no FMA contraction), the semantics of matthewT53/JPEG-Encoder-and-Decoder:
+ *   preprocess.c:101-174  convert_blocks  (RGB -> YCbCr doubles, block tiling)
+ *   preprocess.c:176-196  level_shift     (-128)
+ *   preprocess.c:199-211  blockToCoords   (x0 = -8 on the last block column: quirk kept)
+ *   downsample.c:9-32     chroma_subsample (print-only no-op: nothing to do)
+ *   dct.c:36-59           dct_block       (naive 4-deep loop, x outer / y inner)
+ *   quantise.c:30-86      quantise / scale_table (table applied transposed, no clamp)
+ *   zig_zag.c:6-58        zig_zag_block
+ *   dpcm.c:6-21           dpcm            (in-place recurrence)
+ *   bitmap.c:102-152      bmp_GetColourData (rows read from EOF backwards)
+ *
+ * Parity pinning: tests/test_oracle.py checks this restatement against the reference's own
+ * known-answer test (jpg_driver.c:54-150), against the reference compiled from its sources
+ * by oracle/Makefile (oracle/_ref, this container only) and against the committed golden
+ * fixtures under tests/golden/.
+ */
+#ifndef JPGX_CPU_REF_H
+#define JPGX_CPU_REF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* DCT evaluation mode.  Both give identical results. */
+#define CPUREF_MODE_TABLE   0   /* cos() values tabulated once (same doubles)            */
+#define CPUREF_MODE_REFCOST 1   /* two cos() calls per term, the reference's own cost     */
+
+/* Base tables of quantise.c:8-25 (row index = first subscript). */
+extern const int cpuref_q_lum[8][8];
+extern const int cpuref_q_chr[8][8];
+/* scan order of zig_zag.c:6-15 */
+extern const int cpuref_scan_order[8][8];
+
+/* quantise.c:74-86: Ts = floor((s*T + 50)/100) in int arithmetic, no clamp. */
+void cpuref_scale_table(const int base[8][8], int quality, int out[8][8]);
+
+/* glibc chunk-size bytes read by the x0 = -8 underflow. */
+void cpuref_glibc_underflow(long long n_pixels, long long file_size, uint8_t out[8]);
+
+/* Exact-order forward DCT of one block, in place: v[y*8+x] -> v[v*8+u]   (dct.c:36-59). */
+void cpuref_dct_block(double v[64], int mode);
+/* quantise_lum/_chr with an explicit (already scaled) table            (quantise.c:52-72). */
+void cpuref_quantise_block(double v[64], const int table[8][8]);
+/* zig_zag_block                                                          (zig_zag.c:48-58). */
+void cpuref_zigzag_block(const double v[64], int zz[64]);
+
+/*
+ * Whole hot path for block-rows [row_begin, row_end) of an image.
+ *   rgb      : interleaved, top-down, byte k of each pixel = reference plane k ("r","g","b")
+ *   pitch    : bytes between pixel rows
+ *   underflow: the 8 bytes the quirk block of block-row 0 reads before the planes
+ *   out      : int16 [3][nb_out][64], nb_out = (row_end-row_begin)*(W/8); channel-major,
+ *              block-raster, zig-zag order (zig_zag.c:48-58).
+ * Returns 0, or a negative error (-1 bad geometry, -2 bad quality, -3 bad sample ratio).
+ */
+int cpuref_blocks_rows(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
+                       int sample_ratio, const uint8_t underflow[8], int mode, int nthreads,
+                       int row_begin, int row_end, int16_t *out);
+int cpuref_blocks(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
+                  int sample_ratio, const uint8_t underflow[8], int mode, int nthreads,
+                  int16_t *out);
+
+/* dpcm.c:6-21 on one channel's [nb][64] int array (in place, alternating recurrence). */
+void cpuref_dpcm_i32(int32_t *zz, long nb);
+
+/* bitmap.c:41-152 restated on an in-memory file image.  Returns 0 and fills W,H; with rgb
+ * non-NULL also writes the interleaved top-down pixels exactly as the reference loader
+ * would hand them to preprocess (rows taken from the END of the file backwards). */
+int cpuref_bmp_decode(const uint8_t *file, size_t fs, int *W, int *H, uint8_t *rgb);
+
+/* Synthetic frames of SURVEY.md 8c: counter-based splitmix64 (G) and the tie frame (T). */
+void cpuref_gen_splitmix(uint64_t seed, int W, int H, uint8_t *rgb);
+void cpuref_gen_tie(int W, int H, uint8_t *rgb);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

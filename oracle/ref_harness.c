@@ -1,0 +1,55 @@
+/*
+ * ref_harness.c -- TEST INFRASTRUCTURE ONLY (this container; never shipped to the GPU box).
+ *
+ * Drives the REAL reference stage functions, compiled in place from /root/reference/src by
+ * oracle/Makefile into oracle/_ref/, and dumps their output:
+ *     ref_dump <in.bmp> <out.bin> <quality> <sample_ratio> [dpcm]
+ * writes int32 zig_zag_Y | zig_zag_Cb | zig_zag_Cr (each [nb][64]) after
+ * preprocess_jpeg -> chroma_subsample -> dct -> quantise -> zig_zag (jpg_encode.c:32-44),
+ * optionally followed by dpcm (jpg_encode.c:47).  huffman_encode is not called: it never
+ * terminates.  The stages print one line per block to stdout; redirect it.
+ *
+ * Allocation discipline: nothing large is malloc'd before preprocess_jpeg so that the heap
+ * history (which decides the bytes read by the x0 = -8 underflow, preprocess.c:159-160)
+ * matches a plain encode_bmp_to_jpeg() call.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "headers/jpg_encode.h"
+#include "headers/preprocess.h"
+#include "headers/downsample.h"
+#include "headers/dct.h"
+#include "headers/quantise.h"
+#include "headers/zig_zag.h"
+#include "headers/dpcm.h"
+
+int main(int argc, char **argv)
+{
+    if (argc < 5) {
+        fprintf(stderr, "usage: %s in.bmp out.bin quality sample_ratio [dpcm]\n", argv[0]);
+        return 2;
+    }
+    JpgData j = calloc(1, sizeof(JpegData));
+    j->input_filename = argv[1];
+    j->output_filename = argv[2];
+    j->quality = atoi(argv[3]);
+    j->sample_ratio = atoi(argv[4]);
+
+    preprocess_jpeg(j);
+    chroma_subsample(j);
+    dct(j);
+    quantise(j);
+    zig_zag(j);
+    if (argc > 5) dpcm(j);
+
+    FILE *f = fopen(argv[2], "wb");
+    if (!f) return 1;
+    int **zz[3] = {j->zig_zag_Y, j->zig_zag_Cb, j->zig_zag_Cr};
+    int nbs[3] = {j->num_blocks_Y, j->num_blocks_Cb, j->num_blocks_Cr};
+    for (int c = 0; c < 3; c++)
+        for (int i = 0; i < nbs[c]; i++) fwrite(zz[c][i], sizeof(int), 64, f);
+    fclose(f);
+    fprintf(stderr, "W=%d H=%d nb=%d\n", j->width, j->height, j->num_blocks_Y);
+    return 0;
+}
