@@ -1,0 +1,171 @@
+"""Benchmark: RGB -> quantised zig-zag int16 coefficients (the reference's per-block hot path,
+preprocess.c -> dct.c -> quantise.c -> zig_zag.c) on MI355X through libjpgx.so.
+
+Workload (BASELINE.json metric "Mpixels/sec RGB->quantised-coeff, 4K 4:4:4 q=90"):
+  every GPU processes, per step, its block-row stripe of a global batch of
+  frames_per_gpu * N synthetic 3840x2160 RGB frames (4:4:4, q=90) -- configs[3]'s
+  "batch of 64 x 4K frames, row-stripe sharded across 8 GPUs" at N=8, weak scaling.
+  Frames are generated on the device (splitmix64) before timing; a step is one
+  jpgx_blocks_gpu() call over all frames of the stripe (transform kernel + exact fixup).
+  8 frames per GPU = 597 MB moved per step, more than the 256 MiB Infinity Cache.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
+(one process per GPU, RCCL only for the barrier and the max-time reduction: the stripes need
+no data exchange).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "jpeg-encoder-and-decoder_amd"))
+
+METRIC = "Mpixels/sec RGB→quantised-coeff, 4K 4:4:4 q=90; % HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_PX = 9               # 3 B RGB in + 3 channels x 2 B int16 out
+SPLITMIX_C = 0x9E3779B97F4A7C15
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(width, height, quality, seconds, threads):
+    """The oracle (exact-order fp64 naive DCT with two cos() calls per term: the reference's
+    own algorithmic cost, src/dct.c:43-56) on the first block-rows of one frame."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    frame = oracle.gen_splitmix(1, width, height)
+    t = time.perf_counter()
+    oracle.blocks(frame, quality, mode=oracle.MODE_REFCOST, nthreads=threads, rows=(0, 1))
+    per_row = time.perf_counter() - t
+    rows = max(1, min(height // 8, int(seconds / max(per_row, 1e-6))))
+    t = time.perf_counter()
+    oracle.blocks(frame, quality, mode=oracle.MODE_REFCOST, nthreads=threads, rows=(0, rows))
+    dt = time.perf_counter() - t
+    px = rows * 8 * width
+    return {"value": round(px / dt / 1e6, 4), "unit": "Mpixels/s", "cores": threads,
+            "kind": "port",
+            "sample": f"block-rows 0..{rows} of one {width}x{height} frame ({px} px), q={quality}, "
+                      f"oracle/cpu_ref.c exact-order fp64 with cos() per term, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--frames-per-gpu", type=int, default=8)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--quality", type=int, default=90)
+    ap.add_argument("--sample-ratio", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import jpgx
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    N = world
+
+    W, H, q = args.width, args.height, args.quality
+    B = args.frames_per_gpu * N                      # global batch (weak scaling)
+    r0, r1 = jpgx.stripe(H // 8, N, rank)
+    halo = 1 if r0 > 0 else 0
+    rows_px = (r1 - r0) * 8 + halo
+    row_bytes = W * 3
+    fstride = rows_px * row_bytes
+    nb = (r1 - r0) * (W // 8)
+
+    # device-resident inputs: frame f's stripe (+ one halo pixel row) generated in place
+    d_in = torch.empty(B * fstride, dtype=torch.uint8, device=dev)
+    for f in range(B):
+        k0 = (8 * r0 - halo) * row_bytes
+        seed = (1000 + f + k0 * SPLITMIX_C) % (1 << 64)
+        jpgx.gen_splitmix_gpu(d_in[f * fstride:(f + 1) * fstride], seed)
+    d_out = torch.empty((B, 3, nb, 64), dtype=torch.int16, device=dev)
+    fr = jpgx.frames(W, H, nframes=B, rows=(r0, r1), in_pitch=row_bytes, in_frame_stride=fstride,
+                     out_frame_stride=3 * nb * 64)
+    d_ws = torch.empty(jpgx.workspace_size(fr), dtype=torch.uint8, device=dev)
+    params = jpgx.default_params(W, H, q, args.sample_ratio)
+    rgb_ptr = d_in.data_ptr() + halo * row_bytes
+    torch.cuda.synchronize()
+
+    def step(ev_mid=None):
+        jpgx.blocks_gpu(fr, params, rgb_ptr, d_out, d_ws, event_between=ev_mid)
+
+    for _ in range(args.warmup):
+        step()
+    # per-step events: [start, between transform and fixup, end] on the launch stream
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    for e in evs:
+        e[1].record()                                # materialise the raw event handle
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e in evs:
+        e[0].record()
+        step(e[1])
+        e[2].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    xform_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)
+    fix_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / len(evs)
+    px_rank_step = B * (r1 - r0) * 8 * W
+    px_total = B * W * H * args.steps                 # all ranks
+    value = px_total / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+    achieved = BYTES_PER_PX * px_rank_step / (xform_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        cpu = None
+        if N == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(W, H, q, args.cpu_seconds, 1)
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "Mpixels/s", "n_gpus": N,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (splitmix64 RGB frames generated in HBM)",
+            "config": {"workload": f"{args.frames_per_gpu} x {W}x{H} RGB frames per GPU, "
+                                   f"4:4:4, q={q}, block-row stripes",
+                       "global_batch_frames": B, "width": W, "height": H, "quality": q,
+                       "sample_ratio": args.sample_ratio, "parallelism": f"stripes{N}",
+                       "exact_fixup_ms_per_step": round(fix_ms, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None,
+                         "kernel": "k_xform", "kernel_ms": round(xform_ms, 4),
+                         "bytes_per_launch": BYTES_PER_PX * px_rank_step},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

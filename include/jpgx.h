@@ -1,0 +1,151 @@
+/*
+ * jpgx.h -- C ABI of the MI355X-native JPEG block-transform hot path (libjpgx.so).
+ *
+ * Replaces, for device-resident (or host) RGB frames, the per-8x8-block stage sequence of
+ * matthewT53/JPEG-Encoder-and-Decoder that encode_bmp_to_jpeg() runs between loading the
+ * bitmap and the entropy stage (reference src/jpg_encode.c:32-44):
+ *
+ *     preprocess_jpeg   src/preprocess.c:25-70   RGB -> YCbCr, level shift, 8x8 tiling
+ *     chroma_subsample  src/downsample.c:9-32    (a print-only no-op in the reference)
+ *     dct               src/dct.c:19-59          forward DCT-II per block
+ *     quantise          src/quantise.c:30-86     quality-scaled tables, applied transposed
+ *     zig_zag           src/zig_zag.c:17-58      scan order; result in JpgData.zig_zag_*
+ *
+ * Output contract (bit-exact to the reference on the same input, quirks included):
+ *   int16 coefficients laid out [channel Y,Cb,Cr][block n, raster order][64 zig-zag], i.e. the
+ *   reference's JpgData.zig_zag_Y[n][k], zig_zag_Cb[n][k], zig_zag_Cr[n][k]
+ *   (src/headers/jpg_encode.h:60-62) narrowed to int16 (|coef| <= 2728 always fits).
+ *
+ * Input contract: interleaved, top-down pixels; byte k of each pixel is what the reference
+ * loader calls plane k ("red", "green", "blue": src/bitmap.c:129-137).
+ *
+ * Conventions (unlike the reference, whose stages return void and mutate globals):
+ *   - every entry point returns 0 or a negative JPGX_E* code;
+ *   - callers own every buffer; the library keeps no global mutable state (reentrant);
+ *   - quantisation tables are rebuilt from the pristine base tables on every call
+ *     (the reference rescales its globals in place, src/quantise.c:34-35).
+ */
+#ifndef JPGX_H
+#define JPGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JPGX_OK 0
+#define JPGX_EGEOMETRY (-1)  /* width/height not a multiple of 8 (16 for 4:2:2 / 4:2:0)   */
+#define JPGX_EQUALITY (-2)   /* quality outside [1, 97] (q >= 98 divides by zero, q <= 0
+                                divides by zero: src/quantise.c:81-82)                     */
+#define JPGX_ESAMPLE (-3)    /* sample_ratio not 0, 1 or 2                                 */
+#define JPGX_EARG (-4)       /* null pointer, bad stripe, misaligned buffer or stride      */
+#define JPGX_EHIP (-5)       /* HIP runtime error                                          */
+#define JPGX_EWORKSPACE (-6) /* workspace smaller than jpgx_workspace_size()               */
+#define JPGX_ENODEV (-7)     /* no usable GPU                                              */
+
+/* Chroma sampling constants, src/headers/jpg_encode.h:13-15.  The reference does not
+ * actually subsample (src/downsample.c:24-32): 1 and 2 only tighten the geometry rule
+ * (src/preprocess.c:87-95) and produce 4:4:4 output, which is what parity requires. */
+#define JPGX_NO_CHROMA_SUBSAMPLING 0
+#define JPGX_HORIZONTAL_SUBSAMPLING 1
+#define JPGX_HORIZONTAL_VERTICAL_SUBSAMPLING 2
+
+/* flags */
+#define JPGX_FLAG_FORCE_EXACT 1u /* send every coefficient through the exact fp64 path     */
+
+typedef struct jpgx_params {
+    int quality;              /* 1..97                                                    */
+    int sample_ratio;         /* JPGX_*_SUBSAMPLING                                       */
+    unsigned flags;           /* JPGX_FLAG_*                                              */
+    uint8_t underflow[3][8];  /* [plane][x]: the 8 bytes the reference reads in front of
+                                 each pixel plane r_new/g_new/b_new (src/preprocess.c:
+                                 127-129) for the last block of block-row 0 (offset
+                                 (y+y0)*W + x0 + x < 0 at :159, blockToCoords x0 = -8 at
+                                 :199-211).  They are glibc's chunk-size words;
+                                 jpgx_default_params fills the value a fresh
+                                 encode_bmp_to_jpeg() process reads (all three equal). */
+} jpgx_params;
+
+/* A batch of frames, or one block-row stripe [row_begin, row_end) of each frame. */
+typedef struct jpgx_frames {
+    int width, height;        /* full-frame pixel geometry                                */
+    int row_begin, row_end;   /* block rows processed; 0 and height/8 for whole frames    */
+    int nframes;              /* frames in the batch (>= 1)                               */
+    size_t in_pitch;          /* bytes between pixel rows (multiple of 8)                 */
+    size_t in_frame_stride;   /* bytes between frames (multiple of 8)                     */
+    size_t out_frame_stride;  /* int16 elements between frames' outputs                   */
+} jpgx_frames;
+
+/* Validation shared by every entry point. */
+int jpgx_validate(int width, int height, const jpgx_params *p);
+
+/* Defaults: the given quality/sample_ratio, no flags, glibc underflow bytes for a 24-bit
+ * 54-byte-header BMP of this size (jpgx_glibc_underflow with file = 54 + 3*w*h). */
+void jpgx_default_params(jpgx_params *p, int width, int height, int quality, int sample_ratio);
+
+/* Chunk-size bytes glibc leaves in front of the reference's r_new/g_new/b_new planes
+ * (src/preprocess.c:127-129) after its BMP loader freed a file-sized buffer
+ * (src/bitmap.c:113,151), when the planes come from the top chunk or from mmap (every
+ * image of 64x48 pixels or more in the fixtures; tiny images can reuse a freed chunk, then
+ * pass the real bytes per plane).  n_pixels = w*h, bmp_file_size = size of the BMP file. */
+void jpgx_glibc_underflow(long long n_pixels, long long bmp_file_size, uint8_t out[8]);
+
+/* quantise.c:74-86 on a pristine base table: 0 = luminance, 1 = chrominance. */
+int jpgx_scale_table(int which, int quality, int out[8][8]);
+
+/* The guard band in use for `quality` (per channel, natural index v*8+u): a coefficient
+ * whose fp32 quotient lies within lim of a rounding boundary is recomputed exactly.
+ * Also returns the fp32 per-coefficient scale.  For tests and documentation. */
+int jpgx_guard_band(int quality, float scale[3][64], float lim[3][64]);
+
+/* ---- device path (pointers are device pointers; `stream` is a hipStream_t or NULL) ---- */
+
+/* Bytes of device workspace one jpgx_blocks_gpu call on `fr` needs (flag counts + slots). */
+size_t jpgx_workspace_size(const jpgx_frames *fr);
+
+/* The fused hot path: RGB -> quantised zig-zag int16 for every block of fr's stripe of every
+ * frame.  d_rgb points at pixel (0, 8*row_begin) of frame 0; when row_begin > 0 the pixel
+ * row above it must be readable too (the x0 = -8 quirk reads the last 8 pixels of the
+ * previous pixel row).  Frame f's output is [3][nb][64] at d_out + f*out_frame_stride,
+ * nb = (row_end-row_begin)*width/8.  Asynchronous on `stream`. */
+int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
+                    int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream);
+
+/* Same, and records hipEvent_t `event_between` (if non-NULL) on `stream` after the fast
+ * transform kernel and before the exact-fixup kernel (for timing each one). */
+int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
+                       int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream,
+                       void *event_between);
+
+/* Synthetic frames, generated directly in device memory (SURVEY.md 8c generator G: byte k
+ * of the buffer = splitmix64(seed + (k+1)*0x9E3779B97F4A7C15) >> 56). */
+int jpgx_gen_splitmix_gpu(uint8_t *d_dst, size_t nbytes, uint64_t seed, void *stream);
+/* Tie frame T: flat gray 8x8 blocks, v = 97 + 2*(block_index % 40), R=G=B. */
+int jpgx_gen_tie_gpu(uint8_t *d_dst, int width, int height, void *stream);
+
+/* ---- host-buffer conveniences (synchronous) ------------------------------------------ */
+
+/* Whole image in host memory -> host int16 [3][nb][64] on GPU `device`. */
+int jpgx_blocks(const uint8_t *rgb, int width, int height, size_t pitch, const jpgx_params *p,
+                int16_t *out, int device);
+
+/* Same, sharded into ngpus block-row stripes (GPU 0..ngpus-1), one host thread and one
+ * stream per GPU, no inter-GPU communication: the stripes' outputs are disjoint ranges. */
+int jpgx_blocks_multi(const uint8_t *rgb, int width, int height, size_t pitch,
+                      const jpgx_params *p, int16_t *out, int ngpus);
+
+/* Block-row stripe bounds of shard k of n (balanced, contiguous). */
+void jpgx_stripe(int block_rows, int nshards, int k, int *row_begin, int *row_end);
+
+/* Number of visible GPUs (0 if none). */
+int jpgx_device_count(void);
+
+/* Library version string. */
+const char *jpgx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,64 @@
+/*
+ * jpgx_internal.h -- launch-argument layouts shared by the host plan (jpgx_plan.cpp) and
+ * the gfx950 kernels (jpgx_kernels.hip).  Passed by value as kernel arguments so the
+ * per-coefficient tables are read with scalar loads (wave-uniform).
+ */
+#ifndef JPGX_INTERNAL_H
+#define JPGX_INTERNAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/jpgx.h"
+
+#define JX_SLOTS 7          /* flagged-coefficient slots per block-channel before overflow */
+#define JX_WG 256           /* threads per workgroup for the transform (4 waves)           */
+
+struct jx_geom {
+    const uint8_t *rgb;     /* pixel (0, 8*row_begin) of frame 0                          */
+    int16_t *out;           /* frame 0 output [3][nb][64]                                 */
+    uint8_t *counts;        /* [nframes][3][nb]   flagged coefficients per block-channel  */
+    uint8_t *slots;         /* [nframes][3][nb][JX_SLOTS] zig-zag index of each flag      */
+    long long in_pitch;     /* bytes                                                      */
+    long long in_fstride;   /* bytes                                                      */
+    long long out_fstride;  /* int16 elements                                             */
+    int bpr;                /* blocks per block-row (width/8)                             */
+    int nb;                 /* blocks per frame in this stripe                            */
+    int nframes;
+    int row0;               /* frame block-row of stripe row 0 (underflow only at row 0)  */
+    uint32_t under[6];      /* the underflow pixel row, interleaved (u0 u0 u0 u1 u1 u1..)  */
+};
+
+/* Per-quality tables, device resident (one copy per quality 1..97, built once per device).
+ * Column-major ([ch][u][v]) so one column's 8 entries are one scalar load. */
+struct jx_qtab {
+    float w[3][8][8];       /* [ch][u][v]: fp32 scale of coefficient (u,v), 1/Q folded    */
+    float lim[3][8][8];     /* [ch][u][v]: |t - rint(t)| >= lim -> exact path             */
+    int16_t q[2][64];       /* scaled tables, q[t][u*8+v] = Qs[u][v] as the reference
+                               indexes them (src/quantise.c:58)                           */
+};
+
+#define JX_MAXQ 97
+
+struct jx_xform_args {
+    jx_geom g;
+    int quality;            /* index into the device table                                */
+    int force_exact;        /* JPGX_FLAG_FORCE_EXACT: flag every coefficient              */
+};
+
+struct jx_fix_args {
+    jx_geom g;
+    int quality;
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* host plan (jpgx_plan.cpp) */
+int jx_plan_tables(int quality, float w[3][64], float lim[3][64], int16_t q[2][64]);
+void jx_under_dwords(const uint8_t under[3][8], uint32_t out[6]);
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,542 @@
+/*
+ * jpgx_kernels.hip -- gfx950 kernels of the block-transform hot path + the device C-ABI.
+ *
+ * k_xform  (fast path, one lane = one 8x8 block, all three channels)
+ *   HBM -> VGPR: each lane loads its block's 8 pixel rows (8 x 24 B; a wave covers 64
+ *   horizontally adjacent blocks = 1.5 KiB contiguous per pixel row).  Per channel:
+ *   byte -> f32, colour + level shift (3 FMAs/px), row DCT then column DCT entirely inside
+ *   the lane's registers (even/odd 8-point DCT, 34 ops per 8 points -- no cross-lane
+ *   traffic at all), quantise by one fused multiply-add with the per-coefficient fp32 scale
+ *   that also rounds to an integer (magic 1.5*2^23), zig-zag as a compile-time register
+ *   permutation, int16 packing with v_perm, 8 x 16-B stores per channel.
+ *   A coefficient whose fp32 quotient is within the rigorous guard band of a .5 boundary
+ *   (jpgx_plan.cpp) is recorded in the workspace (count + zig-zag slot) for k_fixup.
+ *
+ * k_fixup  (exact path, one lane = one block-channel, exits at once when nothing is flagged)
+ *   Recomputes each flagged coefficient bit-identically to the reference: double colour
+ *   conversion in its operand order (src/preprocess.c:160-162), -128 (:186-188), the
+ *   64-term sum in x-outer / y-inner order with the product (X*c_u[x])*c_v[y] and the
+ *   glibc cosine doubles (src/dct.c:43-56), ((0.25*a_u)*a_v)*s (:54), true double division
+ *   by the transposed table entry and round() half away from zero (src/quantise.c:58).
+ *   More than JX_SLOTS flags in one block-channel -> all 64 coefficients recomputed.
+ *
+ * The whole file is compiled with FP contraction off; the fast path uses explicit fmaf.
+ */
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "jpgx_internal.h"
+#include "xform_math.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr float kMagic = 12582912.0f; /* 1.5 * 2^23: x + kMagic rounds x to an integer   */
+
+/* zig_zag.c:6-15: scan position of natural (row v, column u) */
+__host__ __device__ constexpr int zz_of(int v, int u)
+{
+    constexpr int t[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+                           3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+                           10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+                           21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+    return t[v * 8 + u];
+}
+
+/* inverse scan: zig-zag index -> (v << 3) | u */
+__constant__ uint8_t kUnZZ[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+/* cos(((2x+1)*u*M_PI)/16) exactly as glibc returns it for the reference (src/dct.c:49-50;
+ * SURVEY.md Appendix B; tests/test_host.py re-derives it from the host libm). */
+__constant__ double kCos[8][8] = {
+    {0x1p+0, 0x1p+0, 0x1p+0, 0x1p+0, 0x1p+0, 0x1p+0, 0x1p+0, 0x1p+0},
+    {0x1.f6297cff75cbp-1, 0x1.a9b66290ea1a3p-1, 0x1.1c73b39ae68c9p-1, 0x1.8f8b83c69a60dp-3,
+     -0x1.8f8b83c69a608p-3, -0x1.1c73b39ae68c6p-1, -0x1.a9b66290ea1a4p-1, -0x1.f6297cff75cbp-1},
+    {0x1.d906bcf328d46p-1, 0x1.87de2a6aea964p-2, -0x1.87de2a6aea962p-2, -0x1.d906bcf328d46p-1,
+     -0x1.d906bcf328d47p-1, -0x1.87de2a6aea96dp-2, 0x1.87de2a6aea967p-2, 0x1.d906bcf328d44p-1},
+    {0x1.a9b66290ea1a3p-1, -0x1.8f8b83c69a608p-3, -0x1.f6297cff75cbp-1, -0x1.1c73b39ae68c8p-1,
+     0x1.1c73b39ae68c5p-1, 0x1.f6297cff75cbp-1, 0x1.8f8b83c69a61dp-3, -0x1.a9b66290ea1a2p-1},
+    {0x1.6a09e667f3bcdp-1, -0x1.6a09e667f3bccp-1, -0x1.6a09e667f3bcep-1, 0x1.6a09e667f3bcbp-1,
+     0x1.6a09e667f3bcep-1, -0x1.6a09e667f3bc5p-1, -0x1.6a09e667f3bc9p-1, 0x1.6a09e667f3bc4p-1},
+    {0x1.1c73b39ae68c9p-1, -0x1.f6297cff75cbp-1, 0x1.8f8b83c69a60cp-3, 0x1.a9b66290ea1a5p-1,
+     -0x1.a9b66290ea1a2p-1, -0x1.8f8b83c69a602p-3, 0x1.f6297cff75cb2p-1, -0x1.1c73b39ae68c2p-1},
+    {0x1.87de2a6aea964p-2, -0x1.d906bcf328d47p-1, 0x1.d906bcf328d44p-1, -0x1.87de2a6aea965p-2,
+     -0x1.87de2a6aea971p-2, 0x1.d906bcf328d46p-1, -0x1.d906bcf328d43p-1, 0x1.87de2a6aea95fp-2},
+    {0x1.8f8b83c69a60dp-3, -0x1.1c73b39ae68c8p-1, 0x1.a9b66290ea1a5p-1, -0x1.f6297cff75cb2p-1,
+     0x1.f6297cff75cbp-1, -0x1.a9b66290ea1a1p-1, 0x1.1c73b39ae68c2p-1, -0x1.8f8b83c69a616p-3}};
+
+/* Per-quality tables (index 0 unused), constant address space so that wave-uniform reads
+ * become scalar loads; filled once per device by tables_for_current_device(). */
+__constant__ jx_qtab g_qtab[JX_MAXQ + 1];
+
+/* dct.c:13 ALPHA(0) = 1/sqrt(2) as the reference's double */
+constexpr double kAlpha0 = 0x1.6a09e667f3bccp-1;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&row)[6], int k)
+{
+    return (row[k >> 2] >> (8 * (k & 3))) & 0xffu;
+}
+
+/*
+ * The 8 pixel rows block `bi` of frame `f` reads, with the reference's addressing:
+ * blockToCoords (src/preprocess.c:199-211) gives x0 = -8 for the last block of a block-row,
+ * which with offset = (y+y0)*W + x0 + x (:159) means pixel row 8r+y-1, columns W-8..W-1;
+ * for frame block-row 0, y = 0 those are the 8 bytes before the planes (g.under).
+ */
+__device__ __forceinline__ void load_block(const jx_geom &g, unsigned f, unsigned bi,
+                                           uint32_t (&raw)[8][6])
+{
+    const unsigned r = bi / (unsigned)g.bpr, c = bi - r * (unsigned)g.bpr;
+    const bool last = c == (unsigned)g.bpr - 1;
+    const bool under = last && (g.row0 + (int)r == 0);
+    const long long row = 8ll * r - (last ? 1 : 0);
+    const uint8_t *base = g.rgb + (long long)f * g.in_fstride + row * g.in_pitch + 24ll * c;
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+        const uint8_t *p = base + (long long)(y == 0 && under ? 1 : y) * g.in_pitch;
+        p = (const uint8_t *)__builtin_assume_aligned(p, 8);
+        u32x4 a;
+        u32x2 b;
+        __builtin_memcpy(&a, p, 16);
+        __builtin_memcpy(&b, p + 16, 8);
+        raw[y][0] = a.x; raw[y][1] = a.y; raw[y][2] = a.z; raw[y][3] = a.w;
+        raw[y][4] = b.x; raw[y][5] = b.y;
+    }
+    if (under) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) raw[0][k] = g.under[k];
+    }
+}
+
+template <int CH>
+__device__ __forceinline__ void xform_channel(uint32_t (&raw)[8][6], const jx_xform_args &a,
+                                              bool active, int16_t *out_blk, unsigned fidx)
+{
+    /* Opaque to the optimiser: forces each channel to re-convert its bytes instead of
+     * keeping 192 converted floats alive across the three channel passes (CSE). */
+#pragma unroll
+    for (int y = 0; y < 8; y++)
+#pragma unroll
+        for (int k = 0; k < 6; k++) asm volatile("" : "+v"(raw[y][k]));
+    float T[8][8];
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+        __builtin_amdgcn_sched_barrier(0);
+        float px[8];
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+            const float r = (float)byte_of(raw[y], 3 * x);
+            const float g = (float)byte_of(raw[y], 3 * x + 1);
+            const float b = (float)byte_of(raw[y], 3 * x + 2);
+            px[x] = jx_pixel<FOps, CH>(r, g, b);
+        }
+        jx_fdct8<FOps>(px, T[y]);
+    }
+    uint32_t bits[64];
+    unsigned cnt = 0;
+    const jx_qtab &tab = g_qtab[a.quality];
+    const bool force = a.force_exact != 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        float col[8], F[8];
+#pragma unroll
+        for (int y = 0; y < 8; y++) col[y] = T[y][u];
+        jx_fdct8<FOps>(col, F);
+        float d[8];
+        uint64_t any = 0;   /* wave mask: lanes with a flagged coefficient in this column */
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            const float w = tab.w[CH][u][v];
+            const float tm = __builtin_fmaf(F[v], w, kMagic);   /* rint(F*w) + magic  */
+            const float rr = tm - kMagic;                         /* exact             */
+            d[v] = __builtin_fmaf(F[v], w, -rr);                  /* F*w - rint(F*w)   */
+            bits[zz_of(v, u)] = __float_as_uint(tm);              /* low 16 bits = int16 */
+            any |= __ballot(__builtin_fabsf(d[v]) >= tab.lim[CH][u][v]);
+        }
+        /* rare (wave-uniform branch): some lane has a coefficient inside the guard band */
+        if (__builtin_expect(force || any != 0, 0)) {
+#pragma unroll
+            for (int v = 0; v < 8; v++) {
+                if (force || __builtin_fabsf(d[v]) >= tab.lim[CH][u][v]) {
+                    if (active && cnt < JX_SLOTS)
+                        a.g.slots[fidx * JX_SLOTS + cnt] = (uint8_t)zz_of(v, u);
+                    cnt++;
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (active) {
+        u32x4 *o = (u32x4 *)out_blk;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            u32x4 s;
+            s.x = __builtin_amdgcn_perm(bits[8 * j + 1], bits[8 * j + 0], 0x05040100u);
+            s.y = __builtin_amdgcn_perm(bits[8 * j + 3], bits[8 * j + 2], 0x05040100u);
+            s.z = __builtin_amdgcn_perm(bits[8 * j + 5], bits[8 * j + 4], 0x05040100u);
+            s.w = __builtin_amdgcn_perm(bits[8 * j + 7], bits[8 * j + 6], 0x05040100u);
+            o[j] = s;
+        }
+        a.g.counts[fidx] = (uint8_t)cnt;
+    }
+}
+
+__global__ __launch_bounds__(JX_WG) void k_xform(const jx_xform_args a)
+{
+    const jx_geom &g = a.g;
+    const unsigned total = (unsigned)g.nb * (unsigned)g.nframes;
+    unsigned b = blockIdx.x * JX_WG + threadIdx.x;
+    const bool active = b < total;
+    if (!active) b = total - 1;
+    const unsigned f = b / (unsigned)g.nb, bi = b - f * (unsigned)g.nb;
+    uint32_t raw[8][6];
+    load_block(g, f, bi, raw);
+    int16_t *ob = g.out + (long long)f * g.out_fstride + (long long)bi * 64;
+    const long long cs = (long long)g.nb * 64;
+    const unsigned fi = f * 3u * (unsigned)g.nb + bi;
+    xform_channel<0>(raw, a, active, ob, fi);
+    __builtin_amdgcn_sched_barrier(0);
+    xform_channel<1>(raw, a, active, ob + cs, fi + (unsigned)g.nb);
+    __builtin_amdgcn_sched_barrier(0);
+    xform_channel<2>(raw, a, active, ob + 2 * cs, fi + 2u * (unsigned)g.nb);
+}
+
+/* Exact reference value of one channel pixel, level shift included (preprocess.c:160-162,
+ * 186-188); r,g,b promoted int -> double as in the reference. */
+__device__ __forceinline__ double exact_pixel(int ch, int r, int g, int b)
+{
+    if (ch == 0) {
+        const double yv = 0.299 * r + 0.587 * g + 0.114 * b;
+        return yv - 128;
+    }
+    if (ch == 1) {
+        const double cb = 128 - (0.168736 * r - 0.331264 * g + 0.5 * b);
+        return cb - 128;
+    }
+    const double cr = 128 + (0.5 * r - 0.418688 * g - 0.081312 * b);
+    return cr - 128;
+}
+
+__device__ int16_t exact_coef(const uint32_t (&raw)[8][6], int ch, int u, int v, int q)
+{
+    double cu[8], cv[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        cu[k] = kCos[u][k];
+        cv[k] = kCos[v][k];
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int x = 0; x < 8; x++)
+#pragma unroll
+        for (int y = 0; y < 8; y++) {
+            const double X = exact_pixel(ch, (int)byte_of(raw[y], 3 * x),
+                                         (int)byte_of(raw[y], 3 * x + 1),
+                                         (int)byte_of(raw[y], 3 * x + 2));
+            s += X * cu[x] * cv[y];
+        }
+    const double F = 0.25 * (u == 0 ? kAlpha0 : 1.0) * (v == 0 ? kAlpha0 : 1.0) * s;
+    return (int16_t)(int)round(F / (double)q);
+}
+
+__global__ __launch_bounds__(256) void k_fixup(const jx_fix_args a)
+{
+    const jx_geom &g = a.g;
+    const unsigned nb = (unsigned)g.nb;
+    const unsigned total = 3u * nb * (unsigned)g.nframes;
+    const unsigned i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= total) return;
+    const unsigned cnt = g.counts[i];
+    if (cnt == 0) return;
+    const unsigned f = i / (3u * nb), rem = i - f * 3u * nb;
+    const int ch = (int)(rem / nb);
+    const unsigned bi = rem - (unsigned)ch * nb;
+    uint32_t raw[8][6];
+    load_block(g, f, bi, raw);
+    int16_t *ob = g.out + (long long)f * g.out_fstride + ((long long)ch * nb + bi) * 64;
+    const int16_t *q = g_qtab[a.quality].q[ch == 0 ? 0 : 1];
+    const unsigned n = cnt > JX_SLOTS ? 64u : cnt;
+    for (unsigned k = 0; k < n; k++) {
+        const int z = cnt > JX_SLOTS ? (int)k : (int)g.slots[(size_t)i * JX_SLOTS + k];
+        const int uv = kUnZZ[z];
+        const int u = uv & 7, v = uv >> 3;
+        ob[z] = exact_coef(raw, ch, u, v, q[u * 8 + v]);
+    }
+}
+
+__device__ __forceinline__ uint8_t splitmix_byte(uint64_t seed, uint64_t k)
+{
+    uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (uint8_t)(z >> 56);
+}
+
+__global__ void k_gen_splitmix(uint8_t *dst, size_t n, uint64_t seed)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x * 16;
+    for (size_t k0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; k0 < n; k0 += stride) {
+        if (k0 + 16 <= n && (((uintptr_t)(dst + k0)) & 15) == 0) {
+            uint32_t w[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                w[j] = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    w[j] |= (uint32_t)splitmix_byte(seed, k0 + 4 * j + i) << (8 * i);
+            }
+            *(u32x4 *)(dst + k0) = u32x4{w[0], w[1], w[2], w[3]};
+        } else {
+            for (size_t k = k0; k < k0 + 16 && k < n; k++) dst[k] = splitmix_byte(seed, k);
+        }
+    }
+}
+
+__global__ void k_gen_tie(uint8_t *dst, int W, int H)
+{
+    const size_t npx = (size_t)W * H;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += stride) {
+        const size_t y = i / W, x = i - y * W;
+        const size_t bi = (y / 8) * (W / 8) + x / 8;
+        const uint8_t v = (uint8_t)(97 + 2 * (bi % 40));
+        dst[3 * i] = v;
+        dst[3 * i + 1] = v;
+        dst[3 * i + 2] = v;
+    }
+}
+
+int hip_rc(hipError_t e) { return e == hipSuccess ? JPGX_OK : JPGX_EHIP; }
+
+constexpr int kMaxDev = 64;
+std::once_flag g_tab_once[kMaxDev];
+int g_tab_rc[kMaxDev];
+
+int tables_for_current_device()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return JPGX_ENODEV;
+    std::call_once(g_tab_once[dev], [dev]() {
+        std::vector<jx_qtab> host(JX_MAXQ + 1);
+        memset(host.data(), 0, host.size() * sizeof(jx_qtab));
+        for (int q = 1; q <= JX_MAXQ; q++) {
+            float w[3][64], lim[3][64];
+            jx_plan_tables(q, w, lim, host[q].q);
+            for (int ch = 0; ch < 3; ch++)
+                for (int u = 0; u < 8; u++)
+                    for (int v = 0; v < 8; v++) {
+                        host[q].w[ch][u][v] = w[ch][v * 8 + u];
+                        host[q].lim[ch][u][v] = lim[ch][v * 8 + u];
+                    }
+        }
+        g_tab_rc[dev] = hip_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_qtab), host.data(),
+                                                 host.size() * sizeof(jx_qtab)));
+    });
+    return g_tab_rc[dev];
+}
+
+size_t ws_counts(size_t total) { return (3 * total + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" {
+
+size_t jpgx_workspace_size(const jpgx_frames *fr)
+{
+    if (!fr || fr->width <= 0 || fr->row_end <= fr->row_begin || fr->nframes <= 0) return 0;
+    const size_t total = (size_t)(fr->row_end - fr->row_begin) * (fr->width / 8) * fr->nframes;
+    return ws_counts(total) + 3 * total * JX_SLOTS;
+}
+
+int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
+                    int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream)
+{
+    return jpgx_blocks_gpu_ev(fr, p, d_rgb, d_out, d_workspace, workspace_bytes, stream, nullptr);
+}
+
+int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
+                       int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream,
+                       void *event_between)
+{
+    if (!fr || !p) return JPGX_EARG;
+    int rc = jpgx_validate(fr->width, fr->height, p);
+    if (rc) return rc;
+    if (fr->row_begin < 0 || fr->row_end > fr->height / 8 || fr->row_begin > fr->row_end ||
+        fr->nframes < 1)
+        return JPGX_EARG;
+    if (fr->row_begin == fr->row_end) return JPGX_OK;
+    if (!d_rgb || !d_out || !d_workspace) return JPGX_EARG;
+    if (fr->in_pitch < (size_t)fr->width * 3 || fr->in_pitch % 8 || fr->in_frame_stride % 8 ||
+        ((uintptr_t)d_rgb & 7) || ((uintptr_t)d_out & 15) || fr->out_frame_stride % 8)
+        return JPGX_EARG;
+    const int bpr = fr->width / 8;
+    const size_t nb = (size_t)(fr->row_end - fr->row_begin) * bpr;
+    const size_t total = nb * fr->nframes;
+    if (3 * total >= (1ull << 31)) return JPGX_EARG;
+    if (fr->nframes > 1 && fr->out_frame_stride < 3 * nb * 64) return JPGX_EARG;
+    if (workspace_bytes < jpgx_workspace_size(fr)) return JPGX_EWORKSPACE;
+
+    jx_xform_args xa;
+    jx_fix_args fa;
+    memset(&xa, 0, sizeof xa);
+    jx_geom &g = xa.g;
+    g.rgb = d_rgb;
+    g.out = d_out;
+    g.counts = (uint8_t *)d_workspace;
+    g.slots = (uint8_t *)d_workspace + ws_counts(total);
+    g.in_pitch = (long long)fr->in_pitch;
+    g.in_fstride = (long long)fr->in_frame_stride;
+    g.out_fstride = (long long)fr->out_frame_stride;
+    g.bpr = bpr;
+    g.nb = (int)nb;
+    g.nframes = fr->nframes;
+    g.row0 = fr->row_begin;
+    jx_under_dwords(p->underflow, g.under);
+    rc = tables_for_current_device();
+    if (rc) return rc;
+    xa.quality = p->quality;
+    xa.force_exact = (p->flags & JPGX_FLAG_FORCE_EXACT) ? 1 : 0;
+    fa.g = g;
+    fa.quality = p->quality;
+
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_xform, dim3((unsigned)((total + JX_WG - 1) / JX_WG)), dim3(JX_WG), 0, s, xa);
+    rc = hip_rc(hipGetLastError());
+    if (rc) return rc;
+    if (event_between) {
+        rc = hip_rc(hipEventRecord((hipEvent_t)event_between, s));
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_fixup, dim3((unsigned)((3 * total + 255) / 256)), dim3(256), 0, s, fa);
+    return hip_rc(hipGetLastError());
+}
+
+int jpgx_gen_splitmix_gpu(uint8_t *d_dst, size_t nbytes, uint64_t seed, void *stream)
+{
+    if (!d_dst) return JPGX_EARG;
+    if (!nbytes) return JPGX_OK;
+    const size_t threads = (nbytes + 15) / 16;
+    const unsigned grid = (unsigned)std::min<size_t>((threads + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_gen_splitmix, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_dst,
+                       nbytes, seed);
+    return hip_rc(hipGetLastError());
+}
+
+int jpgx_gen_tie_gpu(uint8_t *d_dst, int width, int height, void *stream)
+{
+    if (!d_dst || width <= 0 || height <= 0 || width % 8 || height % 8) return JPGX_EARG;
+    const size_t npx = (size_t)width * height;
+    const unsigned grid = (unsigned)std::min<size_t>((npx + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_gen_tie, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_dst, width,
+                       height);
+    return hip_rc(hipGetLastError());
+}
+
+int jpgx_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+/* One GPU, one stripe: H2D of the stripe (+ the pixel row above it), run, D2H of the
+ * stripe's three channel ranges into the whole-image [3][nb][64] host output. */
+static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
+                      const jpgx_params *p, int16_t *out, int device, int r0, int r1)
+{
+    if (r0 == r1) return JPGX_OK;
+    if (hipSetDevice(device) != hipSuccess) return JPGX_ENODEV;
+    const int bpr = width / 8;
+    const size_t row_bytes = (size_t)width * 3;
+    const size_t dpitch = (row_bytes + 7) & ~(size_t)7;
+    const int halo = r0 > 0 ? 1 : 0;
+    const size_t rows = (size_t)(r1 - r0) * 8 + halo;
+    const size_t nb_s = (size_t)(r1 - r0) * bpr, nb = (size_t)(height / 8) * bpr;
+    jpgx_frames fr;
+    memset(&fr, 0, sizeof fr);
+    fr.width = width;
+    fr.height = height;
+    fr.row_begin = r0;
+    fr.row_end = r1;
+    fr.nframes = 1;
+    fr.in_pitch = dpitch;
+    fr.out_frame_stride = 3 * nb_s * 64;
+    const size_t ws = jpgx_workspace_size(&fr);
+    uint8_t *d_in = nullptr;
+    int16_t *d_out = nullptr;
+    void *d_ws = nullptr;
+    hipStream_t s = nullptr;
+    int rc = JPGX_OK;
+    if (hipMalloc(&d_in, rows * dpitch) != hipSuccess ||
+        hipMalloc(&d_out, 3 * nb_s * 64 * sizeof(int16_t)) != hipSuccess ||
+        hipMalloc(&d_ws, ws) != hipSuccess || hipStreamCreate(&s) != hipSuccess) {
+        rc = JPGX_EHIP;
+    }
+    if (!rc) {
+        const uint8_t *src = rgb + ((size_t)r0 * 8 - halo) * pitch;
+        rc = hip_rc(hipMemcpy2DAsync(d_in, dpitch, src, pitch, row_bytes, rows,
+                                     hipMemcpyHostToDevice, s));
+    }
+    if (!rc) rc = jpgx_blocks_gpu(&fr, p, d_in + halo * dpitch, d_out, d_ws, ws, s);
+    for (int ch = 0; ch < 3 && !rc; ch++)
+        rc = hip_rc(hipMemcpyAsync(out + ((size_t)ch * nb + (size_t)r0 * bpr) * 64,
+                                   d_out + (size_t)ch * nb_s * 64, nb_s * 64 * sizeof(int16_t),
+                                   hipMemcpyDeviceToHost, s));
+    if (!rc) rc = hip_rc(hipStreamSynchronize(s));
+    if (s) (void)hipStreamDestroy(s);
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    (void)hipFree(d_ws);
+    return rc;
+}
+
+int jpgx_blocks(const uint8_t *rgb, int width, int height, size_t pitch, const jpgx_params *p,
+                int16_t *out, int device)
+{
+    if (!rgb || !out || !p) return JPGX_EARG;
+    int rc = jpgx_validate(width, height, p);
+    if (rc) return rc;
+    if (pitch < (size_t)width * 3) return JPGX_EARG;
+    if (device < 0 || device >= jpgx_device_count()) return JPGX_ENODEV;
+    return run_stripe(rgb, width, height, pitch, p, out, device, 0, height / 8);
+}
+
+int jpgx_blocks_multi(const uint8_t *rgb, int width, int height, size_t pitch,
+                      const jpgx_params *p, int16_t *out, int ngpus)
+{
+    if (!rgb || !out || !p || ngpus < 1) return JPGX_EARG;
+    int rc = jpgx_validate(width, height, p);
+    if (rc) return rc;
+    if (pitch < (size_t)width * 3) return JPGX_EARG;
+    if (ngpus > jpgx_device_count()) return JPGX_ENODEV;
+    std::vector<int> rcs(ngpus, JPGX_OK);
+    std::vector<std::thread> th;
+    for (int k = 0; k < ngpus; k++) {
+        th.emplace_back([&, k]() {
+            int r0, r1;
+            jpgx_stripe(height / 8, ngpus, k, &r0, &r1);
+            rcs[k] = run_stripe(rgb, width, height, pitch, p, out, k, r0, r1);
+        });
+    }
+    for (auto &t : th) t.join();
+    for (int k = 0; k < ngpus; k++)
+        if (rcs[k]) return rcs[k];
+    return JPGX_OK;
+}
+
+}  /* extern "C" */

@@ -1,0 +1,216 @@
+/*
+ * jpgx_plan.cpp -- host side of the C-ABI shim: argument validation, quantisation tables,
+ * the underflow bytes, and the rigorous fp32 guard band.  No device code here.
+ *
+ * Guard band.  The kernel computes each quotient t = F(u,v)/Q[u][v] in fp32 (xform_math.h,
+ * FOps).  BoundOps below pushes an interval [lo,hi] of the exact value and a bound E on the
+ * fp32 error through the very same template code, starting from pixel bytes in [0,255]:
+ *     add/sub:  E = Ea + Eb + 2^-24 (|c| + Ea + Eb)
+ *     a*k:      E = Ea|k_f| + |a| |k_f - k| + 2^-24 (...)
+ *     fma:      E = Ea|k_f| + |a| |k_f - k| + Eb + 2^-24 (...)
+ * and adds the error of the fp32 scale.  If the fp32 quotient sits farther than E_t from a
+ * half-integer, the reference's double quotient rounds (src/quantise.c:58, C round()) to the
+ * same integer; otherwise the kernel flags the coefficient for the exact-order fp64 path.
+ */
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "jpgx_internal.h"
+#include "xform_math.h"
+
+/* pristine base tables, src/quantise.c:8-25 (row index = first subscript) */
+static const int kLum[8][8] = {
+    {16, 11, 10, 16, 24, 40, 51, 61},   {12, 12, 14, 19, 26, 58, 60, 55},
+    {14, 13, 16, 24, 40, 57, 69, 56},   {14, 17, 22, 29, 51, 87, 80, 62},
+    {18, 22, 37, 56, 68, 109, 103, 77}, {24, 35, 55, 64, 81, 104, 113, 92},
+    {49, 64, 78, 87, 103, 121, 120, 101}, {72, 92, 95, 98, 112, 100, 103, 99}};
+static const int kChr[8][8] = {
+    {17, 18, 24, 47, 99, 99, 99, 99}, {18, 21, 26, 66, 99, 99, 99, 99},
+    {24, 26, 56, 99, 99, 99, 99, 99}, {47, 66, 99, 99, 99, 99, 99, 99},
+    {99, 99, 99, 99, 99, 99, 99, 99}, {99, 99, 99, 99, 99, 99, 99, 99},
+    {99, 99, 99, 99, 99, 99, 99, 99}, {99, 99, 99, 99, 99, 99, 99, 99}};
+
+namespace {
+
+struct Bnd {
+    double lo, hi, E;
+};
+
+struct BoundOps {
+    typedef Bnd T;
+    static double mag(const Bnd &a) { return std::max(fabs(a.lo), fabs(a.hi)); }
+    static Bnd round_(double lo, double hi, double err)
+    {
+        const double u = 0x1p-24;
+        Bnd c{lo, hi, 0};
+        c.E = err + u * (mag(c) + err);
+        return c;
+    }
+    static void span(double a, double b, double &lo, double &hi)
+    {
+        lo = std::min(a, b);
+        hi = std::max(a, b);
+    }
+    static Bnd add(Bnd a, Bnd b) { return round_(a.lo + b.lo, a.hi + b.hi, a.E + b.E); }
+    static Bnd sub(Bnd a, Bnd b) { return round_(a.lo - b.hi, a.hi - b.lo, a.E + b.E); }
+    static Bnd mulc(Bnd a, jx_const k)
+    {
+        double lo, hi;
+        span(a.lo * k.x, a.hi * k.x, lo, hi);
+        return round_(lo, hi, a.E * fabs((double)k.f) + mag(a) * fabs((double)k.f - k.x));
+    }
+    static Bnd fmac(Bnd a, jx_const k, Bnd b)
+    {
+        double lo, hi;
+        span(a.lo * k.x, a.hi * k.x, lo, hi);
+        return round_(lo + b.lo, hi + b.hi,
+                      a.E * fabs((double)k.f) + mag(a) * fabs((double)k.f - k.x) + b.E);
+    }
+    static Bnd lit(jx_const k) { return Bnd{k.x, k.x, fabs((double)k.f - k.x)}; }
+};
+
+template <int CH>
+void coef_bounds(Bnd F[8][8])
+{
+    const Bnd byte{0.0, 255.0, 0.0};
+    Bnd px[8], row[8];
+    const Bnd p = jx_pixel<BoundOps, CH>(byte, byte, byte);
+    for (int x = 0; x < 8; x++) px[x] = p;
+    jx_fdct8<BoundOps>(px, row);   /* every pixel row has the same bound */
+    for (int u = 0; u < 8; u++) {
+        Bnd col[8], out[8];
+        for (int y = 0; y < 8; y++) col[y] = row[u];
+        jx_fdct8<BoundOps>(col, out);
+        for (int v = 0; v < 8; v++) F[v][u] = out[v];
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int jpgx_validate(int width, int height, const jpgx_params *p)
+{
+    if (!p) return JPGX_EARG;
+    if (p->sample_ratio < 0 || p->sample_ratio > 2) return JPGX_ESAMPLE;
+    if (p->quality < 1 || p->quality > 97) return JPGX_EQUALITY;
+    /* src/preprocess.c:82-98 pads by w%8 / w%16 / h%16 (not up to a multiple), after which
+     * its copy loop is wrong: only exact multiples have defined reference behaviour. */
+    const int wm = p->sample_ratio == 0 ? 8 : 16, hm = p->sample_ratio == 2 ? 16 : 8;
+    if (width <= 0 || height <= 0 || width % wm || height % hm) return JPGX_EGEOMETRY;
+    return JPGX_OK;
+}
+
+static unsigned long long req2size(unsigned long long n)
+{
+    unsigned long long s = (n + 8 + 15) & ~15ULL;
+    return s < 32 ? 32 : s;
+}
+
+void jpgx_glibc_underflow(long long n_pixels, long long bmp_file_size, uint8_t out[8])
+{
+    /* glibc malloc (64-bit): the chunk-size word sits 8 bytes before the user pointer.
+     * r_new is an sbrk chunk (size | PREV_INUSE) unless it is at or above the mmap
+     * threshold (size rounded to pages | IS_MMAPPED).  The threshold starts at 128 KiB and
+     * rises to the size of the mmapped file buffer freed at src/bitmap.c:151 when that
+     * chunk is at most 32 MiB (DEFAULT_MMAP_THRESHOLD_MAX). */
+    const unsigned long long page = 4096, thr0 = 128 * 1024, thr_max = 32ULL << 20;
+    unsigned long long thr = thr0;
+    const unsigned long long fchunk = req2size((unsigned long long)bmp_file_size);
+    if (fchunk >= thr0) {
+        const unsigned long long mm = (fchunk + 8 + page - 1) & ~(page - 1);
+        if (mm > thr && mm <= thr_max) thr = mm;
+    }
+    const unsigned long long nb = req2size((unsigned long long)n_pixels);
+    const unsigned long long size =
+        nb >= thr ? (((nb + 8 + page - 1) & ~(page - 1)) | 2ULL) : (nb | 1ULL);
+    for (int k = 0; k < 8; k++) out[k] = (uint8_t)(size >> (8 * k));
+}
+
+void jpgx_default_params(jpgx_params *p, int width, int height, int quality, int sample_ratio)
+{
+    memset(p, 0, sizeof *p);
+    p->quality = quality;
+    p->sample_ratio = sample_ratio;
+    const long long n = (long long)width * height;
+    jpgx_glibc_underflow(n, 54 + 3 * n, p->underflow[0]);
+    memcpy(p->underflow[1], p->underflow[0], 8);
+    memcpy(p->underflow[2], p->underflow[0], 8);
+}
+
+int jpgx_scale_table(int which, int quality, int out[8][8])
+{
+    if (quality < 1 || quality > 97) return JPGX_EQUALITY;
+    const int(*base)[8] = which == 0 ? kLum : kChr;
+    const int s = quality < 50 ? 5000 / quality : 200 - 2 * quality;  /* quantise.c:81 */
+    for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 8; j++) out[i][j] = (s * base[i][j] + 50) / 100;  /* :82 */
+    return JPGX_OK;
+}
+
+void jx_under_dwords(const uint8_t under[3][8], uint32_t out[6])
+{
+    /* the missing pixel row, interleaved like the input: pixel x = (r_x, g_x, b_x) */
+    uint8_t row[24];
+    for (int x = 0; x < 8; x++)
+        for (int k = 0; k < 3; k++) row[3 * x + k] = under[k][x];
+    memcpy(out, row, sizeof row);
+}
+
+int jx_plan_tables(int quality, float w[3][64], float lim[3][64], int16_t q[2][64])
+{
+    int qs[2][8][8];
+    int rc = jpgx_scale_table(0, quality, qs[0]);
+    if (rc) return rc;
+    jpgx_scale_table(1, quality, qs[1]);
+    for (int t = 0; t < 2; t++)
+        for (int u = 0; u < 8; u++)
+            for (int v = 0; v < 8; v++) q[t][u * 8 + v] = (int16_t)qs[t][u][v];
+
+    Bnd F[3][8][8];
+    coef_bounds<0>(F[0]);
+    coef_bounds<1>(F[1]);
+    coef_bounds<2>(F[2]);
+    const long double a0 = 1.0L / sqrtl(2.0L);
+    for (int ch = 0; ch < 3; ch++) {
+        const int t = ch == 0 ? 0 : 1;
+        for (int v = 0; v < 8; v++)
+            for (int u = 0; u < 8; u++) {
+                /* exact scale: 1/4 a(u) a(v) k(u) k(v) / Q[u][v] (dct.c:54, quantise.c:58) */
+                const long double au = u == 0 ? a0 : 1.0L, av = v == 0 ? a0 : 1.0L;
+                const long double ku = u == 4 ? a0 : 1.0L, kv = v == 4 ? a0 : 1.0L;
+                const long double ws = 0.25L * au * av * ku * kv / (long double)qs[t][u][v];
+                const float wf = (float)ws;
+                const Bnd &b = F[ch][v][u];
+                const double mF = BoundOps::mag(b) + b.E;
+                /* error of t_fp vs the reference's real-arithmetic quotient, plus the final
+                 * fma rounding of d (< 2^-25), plus slack for the reference's own double
+                 * rounding (< 1e-10) and for this bound's own double arithmetic */
+                double et = b.E * (double)wf + mF * (double)fabsl((long double)wf - ws) + 0x1p-25;
+                et = et * 1.01 + 1e-7;
+                w[ch][v * 8 + u] = wf;
+                lim[ch][v * 8 + u] = (float)(0.5 - et);
+            }
+    }
+    return JPGX_OK;
+}
+
+int jpgx_guard_band(int quality, float scale[3][64], float lim[3][64])
+{
+    int16_t q[2][64];
+    return jx_plan_tables(quality, scale, lim, q);
+}
+
+void jpgx_stripe(int block_rows, int nshards, int k, int *row_begin, int *row_end)
+{
+    /* contiguous, sizes differ by at most one block row: the first block_rows % n get +1 */
+    const int base = block_rows / nshards, extra = block_rows % nshards;
+    *row_begin = k * base + std::min(k, extra);
+    *row_end = *row_begin + base + (k < extra ? 1 : 0);
+}
+
+const char *jpgx_version(void) { return "jpgx 0.1 (gfx950)"; }
+
+}  /* extern "C" */

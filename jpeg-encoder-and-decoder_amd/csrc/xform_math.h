@@ -1,0 +1,92 @@
+/*
+ * xform_math.h -- the fast-path arithmetic of the block transform, written ONCE as templates
+ * over an "ops" policy so that the same source text is
+ *   (a) instantiated with FOps (fp32, explicit FMAs) inside the gfx950 kernel, and
+ *   (b) instantiated with BoundOps on the host, which propagates a rigorous interval + error
+ *       bound through exactly the same operation sequence.  (b) yields, per quality and per
+ *       coefficient, the guard band that decides when the fp32 quotient is too close to a
+ *       rounding boundary and must be recomputed by the exact-order fp64 path.
+ *
+ * Reference semantics being approximated (exact values in real arithmetic):
+ *   pixel:  preprocess.c:160-162 then level_shift preprocess.c:186-188
+ *   DCT:    dct.c:43-56   F(u,v) = 1/4 a(u) a(v) sum_x sum_y X[y][x] cos((2x+1)u pi/16) cos((2y+1)v pi/16)
+ * The 1-D transform below is the unnormalised 8-point DCT-II computed by an even/odd
+ * decomposition; out[4] omits its cos(pi/4) factor and nothing is normalised: both factors
+ * and the quantiser divisor are folded into one per-coefficient scale w(u,v) on the host.
+ */
+#ifndef JPGX_XFORM_MATH_H
+#define JPGX_XFORM_MATH_H
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define JX_HD __host__ __device__ __forceinline__
+#else
+#define JX_HD inline
+#endif
+
+/* A constant as the kernel uses it (f) and its exact real value (x, to double precision). */
+struct jx_const {
+    float f;
+    double x;
+};
+
+#define JX_K(v) jx_const{(float)(v), (double)(v)}
+
+/* cos(k*pi/16), 40 digits */
+#define JX_C1 0.9807852804032304491261822361342390369739
+#define JX_C2 0.9238795325112867561281831893967882868224
+#define JX_C3 0.8314696123025452370787883776179057567386
+#define JX_C4 0.7071067811865475244008443621048490392848
+#define JX_C5 0.5555702330196022247428308139485328743749
+#define JX_C6 0.3826834323650897717284599840303988667613
+#define JX_C7 0.1950903220161282678482848684770222409277
+
+/* ---- fp32 policy (device) ------------------------------------------------------------- */
+struct FOps {
+    typedef float T;
+    static JX_HD T add(T a, T b) { return a + b; }
+    static JX_HD T sub(T a, T b) { return a - b; }
+    static JX_HD T mulc(T a, jx_const k) { return a * k.f; }
+    static JX_HD T fmac(T a, jx_const k, T b) { return __builtin_fmaf(a, k.f, b); }
+    static JX_HD T lit(jx_const k) { return k.f; }
+};
+
+/*
+ * Pixel value of channel CH from the three input bytes (reference planes 0,1,2 = "r,g,b"),
+ * level shift included:  Y-128,  Cb-128 = -(0.168736r - 0.331264g + 0.5b),
+ * Cr-128 = 0.5r - 0.418688g - 0.081312b.
+ */
+template <class O, int CH>
+JX_HD typename O::T jx_pixel(typename O::T r, typename O::T g, typename O::T b)
+{
+    if (CH == 0)
+        return O::fmac(r, JX_K(0.299), O::fmac(g, JX_K(0.587), O::fmac(b, JX_K(0.114), O::lit(JX_K(-128.0)))));
+    if (CH == 1)
+        return O::fmac(r, JX_K(-0.168736), O::fmac(g, JX_K(0.331264), O::mulc(b, JX_K(-0.5))));
+    return O::fmac(r, JX_K(0.5), O::fmac(g, JX_K(-0.418688), O::mulc(b, JX_K(-0.081312))));
+}
+
+/* Unnormalised 8-point DCT-II, even/odd split; out[4] lacks its cos(pi/4) factor. 34 ops. */
+template <class O>
+JX_HD void jx_fdct8(const typename O::T *in, typename O::T *out)
+{
+    typedef typename O::T T;
+    const T s0 = O::add(in[0], in[7]), d0 = O::sub(in[0], in[7]);
+    const T s1 = O::add(in[1], in[6]), d1 = O::sub(in[1], in[6]);
+    const T s2 = O::add(in[2], in[5]), d2 = O::sub(in[2], in[5]);
+    const T s3 = O::add(in[3], in[4]), d3 = O::sub(in[3], in[4]);
+    const T e0 = O::add(s0, s3), e1 = O::add(s1, s2);
+    const T e2 = O::sub(s0, s3), e3 = O::sub(s1, s2);
+    out[0] = O::add(e0, e1);
+    out[4] = O::sub(e0, e1);
+    out[2] = O::fmac(e2, JX_K(JX_C2), O::mulc(e3, JX_K(JX_C6)));
+    out[6] = O::fmac(e2, JX_K(JX_C6), O::mulc(e3, JX_K(-JX_C2)));
+    out[1] = O::fmac(d0, JX_K(JX_C1), O::fmac(d1, JX_K(JX_C3), O::fmac(d2, JX_K(JX_C5), O::mulc(d3, JX_K(JX_C7)))));
+    out[3] = O::fmac(d0, JX_K(JX_C3), O::fmac(d1, JX_K(-JX_C7), O::fmac(d2, JX_K(-JX_C1), O::mulc(d3, JX_K(-JX_C5)))));
+    out[5] = O::fmac(d0, JX_K(JX_C5), O::fmac(d1, JX_K(-JX_C1), O::fmac(d2, JX_K(JX_C7), O::mulc(d3, JX_K(JX_C3)))));
+    out[7] = O::fmac(d0, JX_K(JX_C7), O::fmac(d1, JX_K(-JX_C5), O::fmac(d2, JX_K(JX_C3), O::mulc(d3, JX_K(-JX_C1)))));
+}
+
+/* Factor the computed out[k] must be multiplied by to give sum_x in[x] cos((2x+1)k pi/16). */
+JX_HD double jx_dct_kfactor(int k) { return k == 4 ? JX_C4 : 1.0; }
+
+#endif

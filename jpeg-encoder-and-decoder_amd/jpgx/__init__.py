@@ -1,0 +1,236 @@
+"""jpgx -- Python view of libjpgx.so, the MI355X-native JPEG block-transform hot path.
+
+Everything here calls through the C ABI declared in include/jpgx.h; there is no Python or
+CPU implementation of the transform in this package.  If the shared library is missing the
+import fails loudly (ImportError) instead of falling back.
+
+Reference mapping (matthewT53/JPEG-Encoder-and-Decoder):
+    blocks_gpu / blocks   <- preprocess_jpeg + chroma_subsample + dct + quantise + zig_zag
+                             (src/jpg_encode.c:32-44), output = JpgData.zig_zag_{Y,Cb,Cr}
+    default_params        <- encode_bmp_to_jpeg(quality, sample_ratio) (src/jpg_encode.c:19)
+    scale_table           <- scale_table (src/quantise.c:74-86)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libjpgx.so")
+
+NO_CHROMA_SUBSAMPLING = 0
+HORIZONTAL_SUBSAMPLING = 1
+HORIZONTAL_VERTICAL_SUBSAMPLING = 2
+FLAG_FORCE_EXACT = 1
+
+OK, EGEOMETRY, EQUALITY, ESAMPLE, EARG, EHIP, EWORKSPACE, ENODEV = 0, -1, -2, -3, -4, -5, -6, -7
+_ERRNAMES = {-1: "EGEOMETRY", -2: "EQUALITY", -3: "ESAMPLE", -4: "EARG", -5: "EHIP",
+             -6: "EWORKSPACE", -7: "ENODEV"}
+
+# every symbol include/jpgx.h declares (tests check the library exports them all)
+EXPORTS = [
+    "jpgx_validate", "jpgx_default_params", "jpgx_glibc_underflow", "jpgx_scale_table",
+    "jpgx_guard_band", "jpgx_workspace_size", "jpgx_blocks_gpu", "jpgx_blocks_gpu_ev",
+    "jpgx_gen_splitmix_gpu",
+    "jpgx_gen_tie_gpu", "jpgx_blocks", "jpgx_blocks_multi", "jpgx_stripe",
+    "jpgx_device_count", "jpgx_version",
+]
+
+
+class JpgxError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        super().__init__(f"{what} failed: {_ERRNAMES.get(rc, rc)}")
+        self.rc = rc
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("quality", ctypes.c_int), ("sample_ratio", ctypes.c_int),
+                ("flags", ctypes.c_uint), ("underflow", (ctypes.c_uint8 * 8) * 3)]
+
+
+class Frames(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int),
+                ("row_begin", ctypes.c_int), ("row_end", ctypes.c_int),
+                ("nframes", ctypes.c_int), ("in_pitch", ctypes.c_size_t),
+                ("in_frame_stride", ctypes.c_size_t), ("out_frame_stride", ctypes.c_size_t)]
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libjpgx.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i, u8p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p
+    P, Fp = ctypes.POINTER(Params), ctypes.POINTER(Frames)
+    L.jpgx_validate.argtypes = [i, i, P]
+    L.jpgx_default_params.argtypes = [P, i, i, i, i]
+    L.jpgx_default_params.restype = None
+    L.jpgx_glibc_underflow.argtypes = [ctypes.c_longlong, ctypes.c_longlong, u8p]
+    L.jpgx_glibc_underflow.restype = None
+    L.jpgx_scale_table.argtypes = [i, i, vp]
+    L.jpgx_guard_band.argtypes = [i, vp, vp]
+    L.jpgx_workspace_size.argtypes = [Fp]
+    L.jpgx_workspace_size.restype = sz
+    L.jpgx_blocks_gpu.argtypes = [Fp, P, vp, vp, vp, sz, vp]
+    L.jpgx_blocks_gpu_ev.argtypes = [Fp, P, vp, vp, vp, sz, vp, vp]
+    L.jpgx_gen_splitmix_gpu.argtypes = [vp, sz, ctypes.c_uint64, vp]
+    L.jpgx_gen_tie_gpu.argtypes = [vp, i, i, vp]
+    L.jpgx_blocks.argtypes = [vp, i, i, sz, P, vp, i]
+    L.jpgx_blocks_multi.argtypes = [vp, i, i, sz, P, vp, i]
+    L.jpgx_stripe.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
+    L.jpgx_stripe.restype = None
+    L.jpgx_device_count.argtypes = []
+    L.jpgx_version.restype = ctypes.c_char_p
+    return L
+
+
+lib = _load()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise JpgxError(rc, what)
+
+
+def version() -> str:
+    return lib.jpgx_version().decode()
+
+
+def device_count() -> int:
+    return lib.jpgx_device_count()
+
+
+def glibc_underflow(n_pixels: int, bmp_file_size: int | None = None) -> bytes:
+    if bmp_file_size is None:
+        bmp_file_size = 54 + 3 * n_pixels
+    out = (ctypes.c_uint8 * 8)()
+    lib.jpgx_glibc_underflow(n_pixels, bmp_file_size, ctypes.cast(out, ctypes.c_void_p))
+    return bytes(out)
+
+
+def default_params(width: int, height: int, quality: int, sample_ratio: int = 0,
+                   underflow=None, flags: int = 0) -> Params:
+    """underflow: None (glibc default), 8 bytes (same for all planes) or [3][8] per plane."""
+    p = Params()
+    lib.jpgx_default_params(ctypes.byref(p), width, height, quality, sample_ratio)
+    if underflow is not None:
+        u = np.asarray(list(underflow) if isinstance(underflow, (bytes, bytearray))
+                       else underflow, np.uint8)
+        u = np.tile(u, (3, 1)) if u.shape == (8,) else u.reshape(3, 8)
+        for k in range(3):
+            for x in range(8):
+                p.underflow[k][x] = int(u[k, x])
+    p.flags = flags
+    return p
+
+
+def validate(width: int, height: int, params: Params) -> int:
+    return lib.jpgx_validate(width, height, ctypes.byref(params))
+
+
+def scale_table(which: int, quality: int) -> np.ndarray:
+    out = np.zeros((8, 8), np.int32)
+    _check(lib.jpgx_scale_table(which, quality, out.ctypes.data), "jpgx_scale_table")
+    return out
+
+
+def guard_band(quality: int) -> tuple[np.ndarray, np.ndarray]:
+    w = np.zeros((3, 64), np.float32)
+    lim = np.zeros((3, 64), np.float32)
+    _check(lib.jpgx_guard_band(quality, w.ctypes.data, lim.ctypes.data), "jpgx_guard_band")
+    return w, lim
+
+
+def stripe(block_rows: int, nshards: int, k: int) -> tuple[int, int]:
+    a, b = ctypes.c_int(), ctypes.c_int()
+    lib.jpgx_stripe(block_rows, nshards, k, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def frames(width: int, height: int, nframes: int = 1, rows: tuple[int, int] | None = None,
+           in_pitch: int | None = None, in_frame_stride: int | None = None,
+           out_frame_stride: int | None = None) -> Frames:
+    r0, r1 = rows if rows is not None else (0, height // 8)
+    fr = Frames()
+    fr.width, fr.height, fr.row_begin, fr.row_end, fr.nframes = width, height, r0, r1, nframes
+    fr.in_pitch = in_pitch if in_pitch is not None else width * 3
+    fr.in_frame_stride = in_frame_stride if in_frame_stride is not None else fr.in_pitch * height
+    nb = (r1 - r0) * (width // 8)
+    fr.out_frame_stride = out_frame_stride if out_frame_stride is not None else 3 * nb * 64
+    return fr
+
+
+def workspace_size(fr: Frames) -> int:
+    return lib.jpgx_workspace_size(ctypes.byref(fr))
+
+
+# ---- torch (device-memory) helpers -------------------------------------------------------
+def _stream_ptr(stream) -> int:
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def blocks_gpu(fr: Frames, params: Params, d_rgb, d_out, d_ws, stream=None,
+               event_between=None) -> None:
+    """Launch the hot path on device tensors (uint8 input, int16 output, uint8 workspace).
+    d_rgb must point at pixel (0, 8*row_begin) of frame 0 (pass a tensor view or an int).
+    event_between: a torch.cuda.Event recorded after the transform kernel, before the fixup
+    kernel (it must have been recorded once already so that its handle exists)."""
+    def ptr(t):
+        return t if isinstance(t, int) else t.data_ptr()
+    ws_bytes = d_ws.numel() if hasattr(d_ws, "numel") else workspace_size(fr)
+    ev = event_between.cuda_event if event_between is not None else None
+    _check(lib.jpgx_blocks_gpu_ev(ctypes.byref(fr), ctypes.byref(params), ptr(d_rgb),
+                                  ptr(d_out), ptr(d_ws), ws_bytes, _stream_ptr(stream), ev),
+           "jpgx_blocks_gpu")
+
+
+def gen_splitmix_gpu(d_dst, seed: int, nbytes: int | None = None, stream=None) -> None:
+    n = d_dst.numel() if nbytes is None else nbytes
+    _check(lib.jpgx_gen_splitmix_gpu(d_dst.data_ptr(), n, seed, _stream_ptr(stream)),
+           "jpgx_gen_splitmix_gpu")
+
+
+def gen_tie_gpu(d_dst, width: int, height: int, stream=None) -> None:
+    _check(lib.jpgx_gen_tie_gpu(d_dst.data_ptr(), width, height, _stream_ptr(stream)),
+           "jpgx_gen_tie_gpu")
+
+
+def encode_blocks(rgb, quality: int, sample_ratio: int = 0, underflow: bytes | None = None,
+                  flags: int = 0, device=None):
+    """Convenience: one image (H,W,3 uint8 torch tensor on a GPU, or numpy on the host) ->
+    int16 [3][nb][64].  Device tensors stay on the device; numpy goes through jpgx_blocks."""
+    if isinstance(rgb, np.ndarray):
+        rgb = np.ascontiguousarray(rgb, np.uint8)
+        H, W = rgb.shape[:2]
+        p = default_params(W, H, quality, sample_ratio, underflow, flags)
+        out = np.empty((3, (H // 8) * (W // 8), 64), np.int16)
+        dev = 0 if device is None else int(device)
+        _check(lib.jpgx_blocks(rgb.ctypes.data, W, H, W * 3, ctypes.byref(p), out.ctypes.data,
+                               dev), "jpgx_blocks")
+        return out
+    import torch
+    H, W = int(rgb.shape[0]), int(rgb.shape[1])
+    p = default_params(W, H, quality, sample_ratio, underflow, flags)
+    _check(validate(W, H, p), "jpgx_validate")
+    fr = frames(W, H)
+    out = torch.empty((3, (H // 8) * (W // 8), 64), dtype=torch.int16, device=rgb.device)
+    ws = torch.empty(workspace_size(fr), dtype=torch.uint8, device=rgb.device)
+    blocks_gpu(fr, p, rgb.contiguous(), out, ws)
+    return out
+
+
+def encode_blocks_multi(rgb: np.ndarray, quality: int, ngpus: int, sample_ratio: int = 0,
+                        underflow: bytes | None = None, flags: int = 0) -> np.ndarray:
+    """Host image -> host coefficients, block-row stripes over GPUs 0..ngpus-1."""
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    H, W = rgb.shape[:2]
+    p = default_params(W, H, quality, sample_ratio, underflow, flags)
+    out = np.empty((3, (H // 8) * (W // 8), 64), np.int16)
+    _check(lib.jpgx_blocks_multi(rgb.ctypes.data, W, H, W * 3, ctypes.byref(p), out.ctypes.data,
+                                 ngpus), "jpgx_blocks_multi")
+    return out

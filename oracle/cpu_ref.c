@@ -140,7 +140,7 @@ static int validate(int W, int H, int quality, int sample_ratio)
 
 /* Reference pixel fetch through blockToCoords (preprocess.c:155-163, 199-211). */
 static void fetch_block_rgb(const uint8_t *rgb, int W, size_t pitch, long bn,
-                            const uint8_t underflow[8], int px[64][3])
+                            const uint8_t underflow[3][8], int px[64][3])
 {
     unsigned int w = (unsigned int)W, tw = 8u * (unsigned int)bn;
     long y0 = (long)(tw / w) * 8;
@@ -150,7 +150,7 @@ static void fetch_block_rgb(const uint8_t *rgb, int W, size_t pitch, long bn,
         for (int x = 0; x < 8; x++) {
             long off = (y + y0) * (long)W + (x0 + x);
             for (int k = 0; k < 3; k++) {
-                if (off < 0) px[y * 8 + x][k] = underflow[off + 8];
+                if (off < 0) px[y * 8 + x][k] = underflow[k][off + 8];
                 else
                     px[y * 8 + x][k] = rgb[(size_t)(off / W) * pitch + (size_t)(off % W) * 3 + k];
             }
@@ -158,7 +158,7 @@ static void fetch_block_rgb(const uint8_t *rgb, int W, size_t pitch, long bn,
 }
 
 int cpuref_blocks_rows(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
-                       int sample_ratio, const uint8_t underflow[8], int mode, int nthreads,
+                       int sample_ratio, const uint8_t underflow[3][8], int mode, int nthreads,
                        int row_begin, int row_end, int16_t *out)
 {
     int err = validate(W, H, quality, sample_ratio);
@@ -202,7 +202,7 @@ int cpuref_blocks_rows(const uint8_t *rgb, int W, int H, size_t pitch, int quali
 }
 
 int cpuref_blocks(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
-                  int sample_ratio, const uint8_t underflow[8], int mode, int nthreads,
+                  int sample_ratio, const uint8_t underflow[3][8], int mode, int nthreads,
                   int16_t *out)
 {
     return cpuref_blocks_rows(rgb, W, H, pitch, quality, sample_ratio, underflow, mode,

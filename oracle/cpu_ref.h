@@ -59,16 +59,17 @@ void cpuref_zigzag_block(const double v[64], int zz[64]);
  * Whole hot path for block-rows [row_begin, row_end) of an image.
  *   rgb      : interleaved, top-down, byte k of each pixel = reference plane k ("r","g","b")
  *   pitch    : bytes between pixel rows
- *   underflow: the 8 bytes the quirk block of block-row 0 reads before the planes
+ *   underflow: [plane][8] bytes the quirk block of block-row 0 reads in front of each of
+ *              the planes r_new/g_new/b_new (preprocess.c:127-129; glibc chunk words)
  *   out      : int16 [3][nb_out][64], nb_out = (row_end-row_begin)*(W/8); channel-major,
  *              block-raster, zig-zag order (zig_zag.c:48-58).
  * Returns 0, or a negative error (-1 bad geometry, -2 bad quality, -3 bad sample ratio).
  */
 int cpuref_blocks_rows(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
-                       int sample_ratio, const uint8_t underflow[8], int mode, int nthreads,
+                       int sample_ratio, const uint8_t underflow[3][8], int mode, int nthreads,
                        int row_begin, int row_end, int16_t *out);
 int cpuref_blocks(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
-                  int sample_ratio, const uint8_t underflow[8], int mode, int nthreads,
+                  int sample_ratio, const uint8_t underflow[3][8], int mode, int nthreads,
                   int16_t *out);
 
 /* dpcm.c:6-21 on one channel's [nb][64] int array (in place, alternating recurrence). */

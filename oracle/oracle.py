@@ -90,7 +90,10 @@ def blocks(rgb: np.ndarray, quality: int, sample_ratio: int = 0, underflow=None,
         pitch = W * 3
     if underflow is None:
         underflow = glibc_underflow(W * H)
-    underflow = np.ascontiguousarray(np.asarray(underflow, np.uint8))
+    underflow = np.asarray(underflow, np.uint8)
+    if underflow.shape == (8,):          # same chunk word in front of all three planes
+        underflow = np.tile(underflow, (3, 1))
+    underflow = np.ascontiguousarray(underflow.reshape(3, 8))
     r0, r1 = rows if rows is not None else (0, H // 8)
     nb = max(r1 - r0, 0) * (W // 8)
     out = np.empty((3, nb, 64), np.int16)
@@ -177,13 +180,24 @@ def ref_available() -> bool:
 
 
 def ref_dump(bmp_path: str, quality: int, sample_ratio: int = 0, dpcm_: bool = False,
-             tmp_out: str | None = None) -> np.ndarray:
-    """Run the real reference (compiled by `make -C oracle ref`) on a BMP file."""
+             tmp_out: str | None = None, want_underflow: bool = False):
+    """Run the real reference (compiled by `make -C oracle ref`) on a BMP file.
+    With want_underflow also return the [3][8] bytes glibc left in front of r_new, g_new,
+    b_new (recorded by the harness's malloc wrapper, oracle/ref_harness.c)."""
     import tempfile
     exe = os.path.join(REF_DIR, "ref_dump")
+    with open(bmp_path, "rb") as f:
+        hdr = f.read(26)
+    n = int.from_bytes(hdr[18:22], "little") * int.from_bytes(hdr[22:26], "little")
+    env = dict(os.environ, REF_WATCH_PIXELS=str(n))
     with tempfile.TemporaryDirectory() as td:
         out = tmp_out or os.path.join(td, "out.bin")
         args = [exe, bmp_path, out, str(quality), str(sample_ratio)] + (["1"] if dpcm_ else [])
-        subprocess.run(args, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
-        a = np.fromfile(out, np.int32)
-    return a.reshape(3, -1, 64)
+        r = subprocess.run(args, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                           env=env, text=True)
+        a = np.fromfile(out, np.int32).reshape(3, -1, 64)
+    if not want_underflow:
+        return a
+    seen = [bytes.fromhex(l.split("=")[1]) for l in r.stderr.split() if l.startswith("pre[")]
+    uf = np.frombuffer(b"".join(seen[-3:]), np.uint8).reshape(3, 8).copy()
+    return a, uf

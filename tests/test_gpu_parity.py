@@ -1,0 +1,167 @@
+"""GPU parity: libjpgx.so (HIP, gfx950) against the oracle and the reference's golden vectors.
+Bit-exact int16 coefficients are required everywhere (integer output: no tolerance)."""
+import os
+
+import numpy as np
+import pytest
+
+import jpgx
+import oracle as O
+from conftest import GOLDEN, coef_sha
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, cuda):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+
+
+def _gpu(rgb, q, cuda, sr=0, underflow=None, flags=0):
+    out = jpgx.encode_blocks(_dev(rgb, cuda), q, sr, underflow=underflow, flags=flags)
+    return out.cpu().numpy()
+
+
+def _frame(ent):
+    if ent["kind"] == "G":
+        return O.gen_splitmix(ent["seed"], ent["W"], ent["H"])
+    return O.gen_tie(ent["W"], ent["H"])
+
+
+def test_golden_synthetic(golden, cuda):
+    for ent in golden["synthetic"]:
+        rgb = _frame(ent)
+        for q, h in ent["coef_sha256"].items():
+            out = _gpu(rgb, int(q), cuda, underflow=ent["underflow"])
+            if coef_sha(out) != h:
+                ref = O.blocks(rgb, int(q), underflow=ent["underflow"])
+                bad = np.argwhere(out != ref)
+                pytest.fail(f"{ent['kind']} {ent['W']}x{ent['H']} q{q}: {len(bad)} mismatches, "
+                            f"first {bad[:5].tolist()}")
+        if "coef_sha256_sr1" in ent:
+            q0 = int(next(iter(ent["coef_sha256"])))
+            out = _gpu(rgb, q0, cuda, sr=1, underflow=ent["underflow"])
+            assert coef_sha(out) == ent["coef_sha256_sr1"]
+
+
+@pytest.mark.parametrize("name", ["cam", "tiger"])
+def test_golden_images(golden, cuda, name):
+    data = open(os.path.join(GOLDEN, "images", f"{name}.bmp"), "rb").read()
+    rgb = O.bmp_decode(data)
+    ent = golden["images"][name]
+    for q, h in ent["coef_sha256"].items():
+        assert coef_sha(_gpu(rgb, int(q), cuda, underflow=ent["underflow"])) == h, (name, q)
+
+
+def test_force_exact_path(golden, cuda):
+    """Every coefficient through the exact fp64 path must still be bit-exact."""
+    for ent in golden["synthetic"]:
+        if ent["W"] * ent["H"] > 512 * 512:
+            continue
+        rgb = _frame(ent)
+        q = next(iter(ent["coef_sha256"]))
+        out = _gpu(rgb, int(q), cuda, underflow=ent["underflow"], flags=jpgx.FLAG_FORCE_EXACT)
+        assert coef_sha(out) == ent["coef_sha256"][q], (ent["W"], ent["H"], q)
+
+
+@pytest.mark.parametrize("q", list(range(1, 98, 4)) + [97])
+def test_quality_sweep(cuda, q):
+    rgb = O.gen_splitmix(1000 + q, 136, 64)
+    assert np.array_equal(_gpu(rgb, q, cuda), O.blocks(rgb, q))
+
+
+@pytest.mark.parametrize("W,H", [(8, 8), (8, 64), (64, 8), (16, 16), (24, 40), (520, 8)])
+def test_edge_geometries(cuda, W, H):
+    rgb = O.gen_splitmix(W * 1000 + H, W, H)
+    uf = np.arange(24, dtype=np.uint8).reshape(3, 8) * 7 + 3   # distinct per plane
+    for q in (30, 90):
+        assert np.array_equal(_gpu(rgb, q, cuda, underflow=uf), O.blocks(rgb, q, underflow=uf))
+
+
+def test_tie_frame_every_dc_is_a_tie(cuda):
+    """T frame at q50: every Y DC is an exact .5 tie (fp32 and fp64-separable fail here)."""
+    rgb = O.gen_tie(512, 512)
+    assert np.array_equal(_gpu(rgb, 50, cuda), O.blocks(rgb, 50))
+
+
+def test_batch_and_stripes(cuda):
+    """A batch of frames in one launch, and block-row stripes with the one-row halo, give the
+    same output as frame-by-frame whole images."""
+    import torch
+    W, H, F, q = 96, 64, 3, 85
+    frames = [O.gen_splitmix(70 + f, W, H) for f in range(F)]
+    host = np.stack(frames)
+    d_in = _dev(host, cuda)
+    p = jpgx.default_params(W, H, q)
+    nb = (H // 8) * (W // 8)
+    fr = jpgx.frames(W, H, nframes=F)
+    out = torch.zeros((F, 3, nb, 64), dtype=torch.int16, device=cuda)
+    ws = torch.empty(jpgx.workspace_size(fr), dtype=torch.uint8, device=cuda)
+    jpgx.blocks_gpu(fr, p, d_in, out, ws)
+    got = out.cpu().numpy()
+    for f in range(F):
+        assert np.array_equal(got[f], O.blocks(frames[f], q)), f
+    # stripes: rows [r0, r1) of every frame, input pointer at pixel row 8*r0
+    bpr = W // 8
+    for r0, r1 in [(0, 3), (3, 5), (5, 8)]:
+        frs = jpgx.frames(W, H, nframes=F, rows=(r0, r1))
+        nbs = (r1 - r0) * bpr
+        o = torch.zeros((F, 3, nbs, 64), dtype=torch.int16, device=cuda)
+        ws = torch.empty(jpgx.workspace_size(frs), dtype=torch.uint8, device=cuda)
+        base = d_in.data_ptr() + r0 * 8 * W * 3
+        jpgx.blocks_gpu(frs, p, base, o, ws)
+        o = o.cpu().numpy()
+        for f in range(F):
+            assert np.array_equal(o[f], O.blocks(frames[f], q, rows=(r0, r1))), (f, r0, r1)
+
+
+def test_host_buffer_entry_points(cuda):
+    rgb = O.gen_splitmix(9, 200, 120)
+    ref = O.blocks(rgb, 77)
+    assert np.array_equal(jpgx.encode_blocks(rgb, 77), ref)
+    n = jpgx.device_count()
+    assert np.array_equal(jpgx.encode_blocks_multi(rgb, 77, n), ref)
+    with pytest.raises(jpgx.JpgxError):
+        jpgx.encode_blocks_multi(rgb, 77, n + 1)
+
+
+def test_invalid_arguments_gpu(cuda):
+    import torch
+    rgb = torch.zeros((16, 16, 3), dtype=torch.uint8, device=cuda)
+    with pytest.raises(jpgx.JpgxError) as e:
+        jpgx.encode_blocks(rgb, 98)
+    assert e.value.rc == jpgx.EQUALITY
+    with pytest.raises(jpgx.JpgxError) as e:
+        jpgx.encode_blocks(torch.zeros((16, 12, 3), dtype=torch.uint8, device=cuda), 50)
+    assert e.value.rc == jpgx.EGEOMETRY
+    fr = jpgx.frames(16, 16)
+    out = torch.zeros((3, 4, 64), dtype=torch.int16, device=cuda)
+    small = torch.empty(8, dtype=torch.uint8, device=cuda)
+    with pytest.raises(jpgx.JpgxError) as e:
+        jpgx.blocks_gpu(fr, jpgx.default_params(16, 16, 50), rgb, out, small)
+    assert e.value.rc == jpgx.EWORKSPACE
+
+
+def test_gpu_generators_match_oracle(cuda):
+    import torch
+    for W, H, seed in [(64, 40, 3), (3840, 16, 77)]:
+        d = torch.empty((H, W, 3), dtype=torch.uint8, device=cuda)
+        jpgx.gen_splitmix_gpu(d, seed)
+        assert np.array_equal(d.cpu().numpy(), O.gen_splitmix(seed, W, H))
+    d = torch.empty((64, 48, 3), dtype=torch.uint8, device=cuda)
+    jpgx.gen_tie_gpu(d, 48, 64)
+    assert np.array_equal(d.cpu().numpy(), O.gen_tie(48, 64))
+
+
+def test_large_frames_hash(golden, cuda):
+    """1080p q90 and 4K q90/q75 generated on the GPU, hashed against the reference."""
+    import torch
+    for ent in golden["synthetic"]:
+        if ent["W"] * ent["H"] < 1920 * 1080:
+            continue
+        W, H = ent["W"], ent["H"]
+        d = torch.empty((H, W, 3), dtype=torch.uint8, device=cuda)
+        jpgx.gen_splitmix_gpu(d, ent["seed"])
+        for q, h in ent["coef_sha256"].items():
+            out = jpgx.encode_blocks(d, int(q), underflow=ent["underflow"]).cpu().numpy()
+            assert coef_sha(out) == h, (W, H, q)

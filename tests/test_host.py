@@ -1,0 +1,102 @@
+"""Host-side checks of the product library (no GPU compute): it loads, exports every symbol
+include/jpgx.h declares, validates arguments like the reference's valid domain, and its
+tables / underflow bytes / guard band agree with the oracle and with the analysis."""
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+import jpgx
+import oracle as O
+from conftest import PKG, REPO
+from test_oracle import CHR, LUM
+
+
+def test_exports_every_declared_symbol():
+    hdr = open(os.path.join(REPO, "include", "jpgx.h")).read()
+    declared = sorted(set(re.findall(r"\b(jpgx_[a-z_0-9]+)\s*\(", hdr)))
+    assert declared == sorted(jpgx.EXPORTS)
+    for name in declared:
+        assert hasattr(jpgx.lib, name), name
+
+
+def test_version_and_devices():
+    assert "gfx950" in jpgx.version()
+    assert jpgx.device_count() >= 0
+
+
+def test_validate_codes():
+    p = jpgx.default_params(64, 64, 50)
+    assert jpgx.validate(64, 64, p) == jpgx.OK
+    assert jpgx.validate(60, 64, p) == jpgx.EGEOMETRY
+    assert jpgx.validate(64, 60, p) == jpgx.EGEOMETRY
+    assert jpgx.validate(0, 64, p) == jpgx.EGEOMETRY
+    for q in (0, -1, 98, 99, 100):
+        assert jpgx.validate(64, 64, jpgx.default_params(64, 64, q)) == jpgx.EQUALITY
+    assert jpgx.validate(64, 64, jpgx.default_params(64, 64, 50, 3)) == jpgx.ESAMPLE
+    assert jpgx.validate(24, 16, jpgx.default_params(24, 16, 50, 1)) == jpgx.EGEOMETRY
+    assert jpgx.validate(32, 16, jpgx.default_params(32, 16, 50, 1)) == jpgx.OK
+    assert jpgx.validate(32, 24, jpgx.default_params(32, 24, 50, 2)) == jpgx.EGEOMETRY
+    assert jpgx.validate(32, 32, jpgx.default_params(32, 32, 50, 2)) == jpgx.OK
+
+
+def test_scale_tables_match_oracle():
+    for q in range(1, 98):
+        assert np.array_equal(jpgx.scale_table(0, q), O.scale_table(LUM, q)), q
+        assert np.array_equal(jpgx.scale_table(1, q), O.scale_table(CHR, q)), q
+    with pytest.raises(jpgx.JpgxError):
+        jpgx.scale_table(0, 98)
+
+
+@pytest.mark.parametrize("n,fs", [(64 * 64, 12426), (320 * 240, 230456), (512 * 512, None),
+                                  (1920 * 1080, None), (3840 * 2160, None), (4096 * 2736, None),
+                                  (4096 * 4096, None), (16384 * 16384, None), (8 * 8, None)])
+def test_underflow_matches_oracle(n, fs):
+    assert jpgx.glibc_underflow(n, fs) == bytes(O.glibc_underflow(n, fs))
+
+
+def test_underflow_survey_values():
+    # 4K -> 11 90 7e 00 ..; 16384^2 -> 02 10 00 10 ..
+    assert jpgx.glibc_underflow(3840 * 2160).hex() == "11907e0000000000"
+    assert jpgx.glibc_underflow(16384 * 16384).hex() == "0210001000000000"
+
+
+def test_stripes_partition():
+    for rows in (1, 7, 8, 135, 270, 2048):
+        for n in (1, 2, 3, 4, 8):
+            spans = [jpgx.stripe(rows, n, k) for k in range(n)]
+            assert spans[0][0] == 0 and spans[-1][1] == rows
+            for (a0, b0), (a1, b1) in zip(spans, spans[1:]):
+                assert b0 == a1
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_guard_band_sane():
+    for q in (1, 10, 50, 75, 90, 97):
+        w, lim = jpgx.guard_band(q)
+        assert np.all(lim > 0.49) and np.all(lim < 0.5)
+        assert np.all(w > 0)
+    # wider band at higher quality (smaller divisors)
+    assert (0.5 - jpgx.guard_band(90)[1]).max() > (0.5 - jpgx.guard_band(50)[1]).max()
+
+
+def test_kernel_cos_table_is_glibc():
+    """The exact path's cosine doubles are those the reference's libm call returns:
+    cos(((2x+1)*u*M_PI)/16) (src/dct.c:49-50)."""
+    src = open(os.path.join(PKG, "csrc", "jpgx_kernels.hip")).read()
+    body = src.split("kCos[8][8] = {")[1].split("}};")[0]
+    vals = [float.fromhex(t) for t in re.findall(r"-?0x[0-9a-f.]+p[+-]\d+", body)]
+    assert len(vals) == 64
+    for u in range(8):
+        for x in range(8):
+            assert vals[u * 8 + x] == math.cos(((2 * x + 1) * u * math.pi) / 16), (u, x)
+
+
+def test_workspace_size():
+    fr = jpgx.frames(3840, 2160, nframes=8)
+    nb = 480 * 270
+    assert jpgx.workspace_size(fr) >= 8 * 3 * nb * 8
+    assert jpgx.workspace_size(jpgx.frames(64, 64, rows=(3, 3))) == 0
