@@ -38,6 +38,10 @@
 
 namespace {
 
+#ifndef JX_PREFETCH
+#define JX_PREFETCH 1   /* load tile t+1 into registers while tile t is transformed */
+#endif
+
 constexpr float kMagic = 12582912.0f; /* 1.5 * 2^23: x + kMagic rounds x to an integer   */
 
 /* zig_zag.c:6-15: scan position of natural (row v, column u) */
@@ -48,6 +52,27 @@ __host__ __device__ constexpr int zz_of(int v, int u)
                            10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
                            21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
     return t[v * 8 + u];
+}
+
+/* column u of zig-zag index z */
+__host__ __device__ constexpr int zz_col(int z)
+{
+    for (int v = 0; v < 8; v++)
+        for (int u = 0; u < 8; u++)
+            if (zz_of(v, u) == z) return u;
+    return -1;
+}
+/* the column pass after which zig-zag entries z0 and z1 are both available */
+__host__ __device__ constexpr int zz_col_done(int z0, int z1)
+{
+    return zz_col(z0) > zz_col(z1) ? zz_col(z0) : zz_col(z1);
+}
+/* the column pass after which the 16-byte output chunk j (zig-zag 8j..8j+7) is complete */
+__host__ __device__ constexpr int zz_chunk_done(int j)
+{
+    int m = 0;
+    for (int z = 8 * j; z < 8 * j + 8; z++) m = zz_col(z) > m ? zz_col(z) : m;
+    return m;
 }
 
 /* inverse scan: zig-zag index -> (v << 3) | u */
@@ -123,8 +148,8 @@ __device__ __forceinline__ void load_block(const jx_geom &g, unsigned f, unsigne
 }
 
 template <int CH>
-__device__ __forceinline__ void xform_channel(uint32_t (&raw)[8][6], const jx_xform_args &a,
-                                              bool active, int16_t *out_blk, unsigned fidx)
+__device__ __forceinline__ unsigned xform_channel(uint32_t (&raw)[8][6], const jx_xform_args &a,
+                                                  bool active, int16_t *out_blk, unsigned fidx)
 {
     /* Opaque to the optimiser: forces each channel to re-convert its bytes instead of
      * keeping 192 converted floats alive across the three channel passes (CSE). */
@@ -146,10 +171,12 @@ __device__ __forceinline__ void xform_channel(uint32_t (&raw)[8][6], const jx_xf
         }
         jx_fdct8<FOps>(px, T[y]);
     }
-    uint32_t bits[64];
+    uint32_t bits[64];     /* tm bit patterns by zig-zag index; low 16 bits = the int16    */
+    uint32_t packed[32];   /* zig-zag pairs (2k, 2k+1) as one dword, formed when complete */
     unsigned cnt = 0;
     const jx_qtab &tab = g_qtab[a.quality];
     const bool force = a.force_exact != 0;
+    u32x4 *o = (u32x4 *)out_blk;
 #pragma unroll
     for (int u = 0; u < 8; u++) {
         float col[8], F[8];
@@ -178,41 +205,87 @@ __device__ __forceinline__ void xform_channel(uint32_t (&raw)[8][6], const jx_xf
                 }
             }
         }
+        /* pack zig-zag pairs completed by this column; store 16-B chunks completed by it
+         * (compile-time decisions: the loops are fully unrolled) */
+#pragma unroll
+        for (int k = 0; k < 32; k++)
+            if (zz_col_done(2 * k, 2 * k + 1) == u)
+                packed[k] = __builtin_amdgcn_perm(bits[2 * k + 1], bits[2 * k], 0x05040100u);
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (zz_chunk_done(j) == u && active)
+                o[j] = u32x4{packed[4 * j], packed[4 * j + 1], packed[4 * j + 2], packed[4 * j + 3]};
         __builtin_amdgcn_sched_barrier(0);
     }
-    if (active) {
-        u32x4 *o = (u32x4 *)out_blk;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            u32x4 s;
-            s.x = __builtin_amdgcn_perm(bits[8 * j + 1], bits[8 * j + 0], 0x05040100u);
-            s.y = __builtin_amdgcn_perm(bits[8 * j + 3], bits[8 * j + 2], 0x05040100u);
-            s.z = __builtin_amdgcn_perm(bits[8 * j + 5], bits[8 * j + 4], 0x05040100u);
-            s.w = __builtin_amdgcn_perm(bits[8 * j + 7], bits[8 * j + 6], 0x05040100u);
-            o[j] = s;
-        }
-        a.g.counts[fidx] = (uint8_t)cnt;
-    }
+    if (active) a.g.counts[fidx] = (uint8_t)cnt;
+    return cnt;
 }
 
-__global__ __launch_bounds__(JX_WG) void k_xform(const jx_xform_args a)
+/* block index of this lane in tile t (clamped into range for the tail tile) */
+__device__ __forceinline__ unsigned tile_block(unsigned t, unsigned lane, unsigned total)
+{
+    const unsigned b = t * 64u + lane;
+    return b < total ? b : total - 1;
+}
+
+/*
+ * Persistent: each wave walks tiles t, t + waves, ...; the next tile's 8 pixel rows are
+ * loaded into registers before the current tile is transformed, so HBM latency overlaps the
+ * ~3k VALU instructions of a tile instead of stalling every wave at its start.
+ */
+__global__ __launch_bounds__(JX_WG, 2) void k_xform(const jx_xform_args a)
 {
     const jx_geom &g = a.g;
-    const unsigned total = (unsigned)g.nb * (unsigned)g.nframes;
-    unsigned b = blockIdx.x * JX_WG + threadIdx.x;
-    const bool active = b < total;
-    if (!active) b = total - 1;
-    const unsigned f = b / (unsigned)g.nb, bi = b - f * (unsigned)g.nb;
+    const unsigned nb = (unsigned)g.nb;
+    const unsigned total = nb * (unsigned)g.nframes;
+    const unsigned ntiles = (total + 63u) / 64u;
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned nwaves = gridDim.x * (JX_WG / 64);
+    unsigned t = blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6);
+    if (t >= ntiles) return;                       /* whole wave */
+    const long long cs = (long long)nb * 64;
     uint32_t raw[8][6];
-    load_block(g, f, bi, raw);
-    int16_t *ob = g.out + (long long)f * g.out_fstride + (long long)bi * 64;
-    const long long cs = (long long)g.nb * 64;
-    const unsigned fi = f * 3u * (unsigned)g.nb + bi;
-    xform_channel<0>(raw, a, active, ob, fi);
-    __builtin_amdgcn_sched_barrier(0);
-    xform_channel<1>(raw, a, active, ob + cs, fi + (unsigned)g.nb);
-    __builtin_amdgcn_sched_barrier(0);
-    xform_channel<2>(raw, a, active, ob + 2 * cs, fi + 2u * (unsigned)g.nb);
+#if JX_PREFETCH
+    {
+        const unsigned b = tile_block(t, lane, total), f = b / nb;
+        load_block(g, f, b - f * nb, raw);
+    }
+#endif
+    for (; t < ntiles; t += nwaves) {
+        const unsigned b0 = t * 64u + lane;
+        const bool active = b0 < total;
+        const unsigned b = active ? b0 : total - 1;
+        const unsigned f = b / nb, bi = b - f * nb;
+        const unsigned tn = t + nwaves;
+#if JX_PREFETCH
+        uint32_t nxt[8][6];
+        if (tn < ntiles) {
+            const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
+            load_block(g, fn, bn - fn * nb, nxt);
+        }
+#else
+        load_block(g, f, bi, raw);
+#endif
+        int16_t *ob = g.out + (long long)f * g.out_fstride + (long long)bi * 64;
+        const unsigned fi = f * 3u * nb + bi;
+        unsigned c = xform_channel<0>(raw, a, active, ob, fi);
+        __builtin_amdgcn_sched_barrier(0);
+        c += xform_channel<1>(raw, a, active, ob + cs, fi + nb);
+        __builtin_amdgcn_sched_barrier(0);
+        c += xform_channel<2>(raw, a, active, ob + 2 * cs, fi + 2u * nb);
+        const uint64_t m = __ballot(active && c != 0);
+        if (lane == 0) g.tile_mask[t] = m;
+#if JX_PREFETCH
+        if (tn < ntiles) {
+#pragma unroll
+            for (int y = 0; y < 8; y++)
+#pragma unroll
+                for (int k = 0; k < 6; k++) raw[y][k] = nxt[y][k];
+        }
+#else
+        (void)tn;
+#endif
+    }
 }
 
 /* Exact reference value of one channel pixel, level shift included (preprocess.c:160-162,
@@ -231,50 +304,70 @@ __device__ __forceinline__ double exact_pixel(int ch, int r, int g, int b)
     return cr - 128;
 }
 
-__device__ int16_t exact_coef(const uint32_t (&raw)[8][6], int ch, int u, int v, int q)
+/* One coefficient in the reference's exact operation order.  px = the block's 8 pixel rows
+ * (24 interleaved bytes each) in this thread's LDS slice. */
+__device__ int16_t exact_coef(const uint8_t *px, int ch, int u, int v, int q)
 {
-    double cu[8], cv[8];
+    double cv[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-        cu[k] = kCos[u][k];
-        cv[k] = kCos[v][k];
-    }
+    for (int y = 0; y < 8; y++) cv[y] = kCos[v][y];
     double s = 0.0;
+#pragma unroll 1
+    for (int x = 0; x < 8; x++) {            /* dct.c:46 x outer */
+        const double cux = kCos[u][x];
 #pragma unroll
-    for (int x = 0; x < 8; x++)
-#pragma unroll
-        for (int y = 0; y < 8; y++) {
-            const double X = exact_pixel(ch, (int)byte_of(raw[y], 3 * x),
-                                         (int)byte_of(raw[y], 3 * x + 1),
-                                         (int)byte_of(raw[y], 3 * x + 2));
-            s += X * cu[x] * cv[y];
+        for (int y = 0; y < 8; y++) {        /* dct.c:47 y inner */
+            const uint8_t *p = px + y * 24 + 3 * x;
+            const double X = exact_pixel(ch, p[0], p[1], p[2]);
+            s += X * cux * cv[y];            /* (X * c_u[x]) * c_v[y], dct.c:48-50 */
         }
+    }
     const double F = 0.25 * (u == 0 ? kAlpha0 : 1.0) * (v == 0 ? kAlpha0 : 1.0) * s;
-    return (int16_t)(int)round(F / (double)q);
+    return (int16_t)(int)round(F / (double)q);      /* quantise.c:58 */
 }
 
-__global__ __launch_bounds__(256) void k_fixup(const jx_fix_args a)
+/*
+ * One thread per 64-block tile.  Nearly every tile has tile_mask == 0 and the thread leaves
+ * after one 8-byte load; a flagged block is staged into LDS once and each of its flagged
+ * coefficients (or all 64 of a block-channel whose slots overflowed) is recomputed exactly.
+ */
+__global__ __launch_bounds__(64) void k_fixup(const jx_fix_args a)
 {
+    __shared__ uint8_t s_px[64][192];
     const jx_geom &g = a.g;
     const unsigned nb = (unsigned)g.nb;
-    const unsigned total = 3u * nb * (unsigned)g.nframes;
-    const unsigned i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= total) return;
-    const unsigned cnt = g.counts[i];
-    if (cnt == 0) return;
-    const unsigned f = i / (3u * nb), rem = i - f * 3u * nb;
-    const int ch = (int)(rem / nb);
-    const unsigned bi = rem - (unsigned)ch * nb;
-    uint32_t raw[8][6];
-    load_block(g, f, bi, raw);
-    int16_t *ob = g.out + (long long)f * g.out_fstride + ((long long)ch * nb + bi) * 64;
-    const int16_t *q = g_qtab[a.quality].q[ch == 0 ? 0 : 1];
-    const unsigned n = cnt > JX_SLOTS ? 64u : cnt;
-    for (unsigned k = 0; k < n; k++) {
-        const int z = cnt > JX_SLOTS ? (int)k : (int)g.slots[(size_t)i * JX_SLOTS + k];
-        const int uv = kUnZZ[z];
-        const int u = uv & 7, v = uv >> 3;
-        ob[z] = exact_coef(raw, ch, u, v, q[u * 8 + v]);
+    const unsigned total = nb * (unsigned)g.nframes;
+    const unsigned ntiles = (total + 63u) / 64u;
+    const unsigned t = blockIdx.x * 64u + threadIdx.x;
+    if (t >= ntiles) return;
+    uint64_t mask = g.tile_mask[t];
+    uint8_t *px = s_px[threadIdx.x];
+    while (mask) {
+        const unsigned L = (unsigned)__builtin_ctzll(mask);
+        mask &= mask - 1;
+        const unsigned b = t * 64u + L;
+        if (b >= total) break;
+        const unsigned f = b / nb, bi = b - f * nb;
+        uint32_t raw[8][6];
+        load_block(g, f, bi, raw);
+#pragma unroll
+        for (int y = 0; y < 8; y++)
+#pragma unroll
+            for (int k = 0; k < 6; k++) *(uint32_t *)(px + y * 24 + 4 * k) = raw[y][k];
+        for (int ch = 0; ch < 3; ch++) {
+            const unsigned i = (f * 3u + (unsigned)ch) * nb + bi;
+            const unsigned cnt = g.counts[i];
+            if (!cnt) continue;
+            int16_t *ob = g.out + (long long)f * g.out_fstride + ((long long)ch * nb + bi) * 64;
+            const int16_t *q = g_qtab[a.quality].q[ch == 0 ? 0 : 1];
+            const unsigned n = cnt > JX_SLOTS ? 64u : cnt;
+            for (unsigned k = 0; k < n; k++) {
+                const int z = cnt > JX_SLOTS ? (int)k : (int)g.slots[(size_t)i * JX_SLOTS + k];
+                const int uv = kUnZZ[z];
+                const int u = uv & 7, v = uv >> 3;
+                ob[z] = exact_coef(px, ch, u, v, q[u * 8 + v]);
+            }
+        }
     }
 }
 
@@ -350,7 +443,30 @@ int tables_for_current_device()
     return g_tab_rc[dev];
 }
 
-size_t ws_counts(size_t total) { return (3 * total + 255) & ~(size_t)255; }
+/* workspace: [tile_mask u64 x ntiles][counts u8 x 3*total][slots u8 x 3*total*JX_SLOTS] */
+size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
+size_t ws_mask_bytes(size_t total) { return align256((total + 63) / 64 * 8); }
+size_t ws_count_bytes(size_t total) { return align256(3 * total); }
+
+/* resident waves of k_xform on the current device (persistent grid size) */
+int g_resident_waves[kMaxDev];
+std::once_flag g_res_once[kMaxDev];
+
+int resident_waves()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
+    std::call_once(g_res_once[dev], [dev]() {
+        int cus = 0, per_cu = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_xform, JX_WG, 0) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 2;
+        g_resident_waves[dev] = cus * per_cu * (JX_WG / 64);
+    });
+    return g_resident_waves[dev];
+}
 
 }  // namespace
 
@@ -360,7 +476,7 @@ size_t jpgx_workspace_size(const jpgx_frames *fr)
 {
     if (!fr || fr->width <= 0 || fr->row_end <= fr->row_begin || fr->nframes <= 0) return 0;
     const size_t total = (size_t)(fr->row_end - fr->row_begin) * (fr->width / 8) * fr->nframes;
-    return ws_counts(total) + 3 * total * JX_SLOTS;
+    return ws_mask_bytes(total) + ws_count_bytes(total) + 3 * total * JX_SLOTS;
 }
 
 int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
@@ -397,8 +513,9 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     jx_geom &g = xa.g;
     g.rgb = d_rgb;
     g.out = d_out;
-    g.counts = (uint8_t *)d_workspace;
-    g.slots = (uint8_t *)d_workspace + ws_counts(total);
+    g.tile_mask = (uint64_t *)d_workspace;
+    g.counts = (uint8_t *)d_workspace + ws_mask_bytes(total);
+    g.slots = g.counts + ws_count_bytes(total);
     g.in_pitch = (long long)fr->in_pitch;
     g.in_fstride = (long long)fr->in_frame_stride;
     g.out_fstride = (long long)fr->out_frame_stride;
@@ -415,14 +532,17 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     fa.quality = p->quality;
 
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_xform, dim3((unsigned)((total + JX_WG - 1) / JX_WG)), dim3(JX_WG), 0, s, xa);
+    const size_t ntiles = (total + 63) / 64;
+    const size_t waves = std::min<size_t>(ntiles, (size_t)std::max(resident_waves(), 4));
+    const unsigned grid = (unsigned)((waves + JX_WG / 64 - 1) / (JX_WG / 64));
+    hipLaunchKernelGGL(k_xform, dim3(grid), dim3(JX_WG), 0, s, xa);
     rc = hip_rc(hipGetLastError());
     if (rc) return rc;
     if (event_between) {
         rc = hip_rc(hipEventRecord((hipEvent_t)event_between, s));
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_fixup, dim3((unsigned)((3 * total + 255) / 256)), dim3(256), 0, s, fa);
+    hipLaunchKernelGGL(k_fixup, dim3((unsigned)((ntiles + 63) / 64)), dim3(64), 0, s, fa);
     return hip_rc(hipGetLastError());
 }
 

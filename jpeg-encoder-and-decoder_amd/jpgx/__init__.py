@@ -61,6 +61,12 @@ class Frames(ctypes.Structure):
 def _load() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libjpgx.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    # libjpgx.so and torch both need libamdhip64.so.7 (same soname): load torch first so the
+    # process has ONE HIP runtime and device pointers/streams are shared.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, sz, i, u8p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p
     P, Fp = ctypes.POINTER(Params), ctypes.POINTER(Frames)
