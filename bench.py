@@ -154,7 +154,7 @@ def main():
                                    f"4:4:4, q={q}, block-row stripes",
                        "global_batch_frames": B, "width": W, "height": H, "quality": q,
                        "sample_ratio": args.sample_ratio, "parallelism": f"stripes{N}",
-                       "exact_fixup_ms_per_step": round(fix_ms, 4)},
+                       "host_gap_ms_per_step": round(fix_ms, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None,

@@ -17,9 +17,6 @@
 struct jx_geom {
     const uint8_t *rgb;     /* pixel (0, 8*row_begin) of frame 0                          */
     int16_t *out;           /* frame 0 output [3][nb][64]                                 */
-    uint64_t *tile_mask;    /* [ntiles] lanes (blocks) of each 64-block tile with a flag  */
-    uint8_t *counts;        /* [nframes][3][nb]   flagged coefficients per block-channel  */
-    uint8_t *slots;         /* [nframes][3][nb][JX_SLOTS] zig-zag index of each flag      */
     long long in_pitch;     /* bytes                                                      */
     long long in_fstride;   /* bytes                                                      */
     long long out_fstride;  /* int16 elements                                             */
@@ -47,10 +44,6 @@ struct jx_xform_args {
     int force_exact;        /* JPGX_FLAG_FORCE_EXACT: flag every coefficient              */
 };
 
-struct jx_fix_args {
-    jx_geom g;
-    int quality;
-};
 
 #ifdef __cplusplus
 extern "C" {

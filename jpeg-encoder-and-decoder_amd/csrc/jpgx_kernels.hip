@@ -1,32 +1,33 @@
 /*
  * jpgx_kernels.hip -- gfx950 kernels of the block-transform hot path + the device C-ABI.
  *
- * k_xform  (fast path, one lane = one 8x8 block, all three channels)
+ * k_xform (one kernel does the whole hot path; one lane = one 8x8 block, all 3 channels)
  *   HBM -> VGPR: each lane loads its block's 8 pixel rows (8 x 24 B; a wave covers 64
- *   horizontally adjacent blocks = 1.5 KiB contiguous per pixel row).  Per channel:
- *   byte -> f32, colour + level shift (3 FMAs/px), row DCT then column DCT entirely inside
- *   the lane's registers (even/odd 8-point DCT, 34 ops per 8 points -- no cross-lane
- *   traffic at all), quantise by one fused multiply-add with the per-coefficient fp32 scale
- *   that also rounds to an integer (magic 1.5*2^23), zig-zag as a compile-time register
- *   permutation, int16 packing with v_perm, 8 x 16-B stores per channel.
- *   A coefficient whose fp32 quotient is within the rigorous guard band of a .5 boundary
- *   (jpgx_plan.cpp) is recorded in the workspace (count + zig-zag slot) for k_fixup.
+ *   horizontally adjacent blocks = 1.5 KiB contiguous per pixel row), one tile ahead.
+ *   Per channel, entirely in the lane's registers (no cross-lane traffic):
+ *     byte -> f32, colour + level shift (3 FMAs/px)        src/preprocess.c:160-162,186-188
+ *     row DCT then column DCT, even/odd 8-point DCT-II      src/dct.c:36-59
+ *     quantise: one FMA with the per-coefficient fp32 scale (1/Q and DCT normalisation
+ *       folded) that also rounds to an integer (+1.5*2^23)  src/quantise.c:52-72 (transposed)
+ *     zig-zag as a compile-time register permutation, int16 pairs packed with v_perm
+ *                                                           src/zig_zag.c:48-58
+ *   LDS -> HBM: the wave's 64 blocks x 128 B of a channel are staged in LDS and written as
+ *   8 KiB of contiguous 16-B-per-lane stores (coalesced).
+ *   Exactness: a coefficient whose fp32 quotient lies within the rigorous guard band of a
+ *   .5 boundary (jpgx_plan.cpp) is queued in the wave's LDS (block pixels + item) and later
+ *   recomputed, many lanes at once, in the reference's exact fp64 operation order:
+ *   double colour conversion in its operand order, -128, the 64-term sum x-outer / y-inner
+ *   with (X*c_u[x])*c_v[y] and the glibc cosine doubles, ((0.25*a_u)*a_v)*s, true double
+ *   division by the transposed table entry, round() half away from zero.
  *
- * k_fixup  (exact path, one lane = one block-channel, exits at once when nothing is flagged)
- *   Recomputes each flagged coefficient bit-identically to the reference: double colour
- *   conversion in its operand order (src/preprocess.c:160-162), -128 (:186-188), the
- *   64-term sum in x-outer / y-inner order with the product (X*c_u[x])*c_v[y] and the
- *   glibc cosine doubles (src/dct.c:43-56), ((0.25*a_u)*a_v)*s (:54), true double division
- *   by the transposed table entry and round() half away from zero (src/quantise.c:58).
- *   More than JX_SLOTS flags in one block-channel -> all 64 coefficients recomputed.
- *
- * The whole file is compiled with FP contraction off; the fast path uses explicit fmaf.
+ * Compiled with FP contraction off; the fast path uses explicit fmaf.
  */
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -41,8 +42,34 @@ namespace {
 #ifndef JX_PREFETCH
 #define JX_PREFETCH 1   /* load tile t+1 into registers while tile t is transformed */
 #endif
+#ifndef JX_ROW_SB       /* scheduling fence between the row DCTs of a channel          */
+#define JX_ROW_SB 1
+#endif
+#ifndef JX_COL_SB       /* scheduling fence between the column DCTs of a channel       */
+#define JX_COL_SB 1
+#endif
+#ifndef JX_EXACT_INLINE /* inline the rare exact-path helpers (vs real calls)           */
+#define JX_EXACT_INLINE 1
+#endif
+#if JX_ROW_SB
+#define JX_SB_ROW() __builtin_amdgcn_sched_barrier(0)
+#else
+#define JX_SB_ROW() ((void)0)
+#endif
+#if JX_COL_SB
+#define JX_SB_COL() __builtin_amdgcn_sched_barrier(0)
+#else
+#define JX_SB_COL() ((void)0)
+#endif
+#if JX_EXACT_INLINE
+#define JX_RARE __device__
+#else
+#define JX_RARE __device__ __noinline__
+#endif
 
 constexpr float kMagic = 12582912.0f; /* 1.5 * 2^23: x + kMagic rounds x to an integer   */
+constexpr int kSlots = 32;            /* per-wave deferred-exact queue: block pixel slots  */
+constexpr int kItems = 64;            /*                                 and coefficients  */
 
 /* zig_zag.c:6-15: scan position of natural (row v, column u) */
 __host__ __device__ constexpr int zz_of(int v, int u)
@@ -111,6 +138,16 @@ constexpr double kAlpha0 = 0x1.6a09e667f3bccp-1;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+/* Per-wave LDS.  `stage` and `px` are adjacent: after a flush the pair is reused as 64 x
+ * 192 B to stage every lane's block for a whole-block exact recompute (overflow path). */
+struct WaveLds {
+    u32x4 stage[64 * 9];          /* one channel: block k's 8 chunks at units 9k..9k+7     */
+    u32x4 px[kSlots][12];         /* pixel rows (8 x 24 B) of blocks with queued items     */
+    uint32_t slot_blk[kSlots];    /* launch-global block index of each slot                */
+    uint32_t item[kItems];        /* slot | ch << 5 | zigzag << 7                          */
+};
+static_assert(sizeof(u32x4) * (64 * 9 + kSlots * 12) >= 64 * 192, "overflow staging");
+
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&row)[6], int k)
 {
     return (row[k >> 2] >> (8 * (k & 3))) & 0xffu;
@@ -120,7 +157,7 @@ __device__ __forceinline__ uint32_t byte_of(const uint32_t (&row)[6], int k)
  * The 8 pixel rows block `bi` of frame `f` reads, with the reference's addressing:
  * blockToCoords (src/preprocess.c:199-211) gives x0 = -8 for the last block of a block-row,
  * which with offset = (y+y0)*W + x0 + x (:159) means pixel row 8r+y-1, columns W-8..W-1;
- * for frame block-row 0, y = 0 those are the 8 bytes before the planes (g.under).
+ * for frame block-row 0, y = 0 those are the bytes in front of the planes (g.under).
  */
 __device__ __forceinline__ void load_block(const jx_geom &g, unsigned f, unsigned bi,
                                            uint32_t (&raw)[8][6])
@@ -147,146 +184,17 @@ __device__ __forceinline__ void load_block(const jx_geom &g, unsigned f, unsigne
     }
 }
 
-template <int CH>
-__device__ __forceinline__ unsigned xform_channel(uint32_t (&raw)[8][6], const jx_xform_args &a,
-                                                  bool active, int16_t *out_blk, unsigned fidx)
+__device__ __forceinline__ void raw_to_lds(const uint32_t (&raw)[8][6], u32x4 *dst)
 {
-    /* Opaque to the optimiser: forces each channel to re-convert its bytes instead of
-     * keeping 192 converted floats alive across the three channel passes (CSE). */
 #pragma unroll
-    for (int y = 0; y < 8; y++)
-#pragma unroll
-        for (int k = 0; k < 6; k++) asm volatile("" : "+v"(raw[y][k]));
-    float T[8][8];
-#pragma unroll
-    for (int y = 0; y < 8; y++) {
-        __builtin_amdgcn_sched_barrier(0);
-        float px[8];
-#pragma unroll
-        for (int x = 0; x < 8; x++) {
-            const float r = (float)byte_of(raw[y], 3 * x);
-            const float g = (float)byte_of(raw[y], 3 * x + 1);
-            const float b = (float)byte_of(raw[y], 3 * x + 2);
-            px[x] = jx_pixel<FOps, CH>(r, g, b);
-        }
-        jx_fdct8<FOps>(px, T[y]);
+    for (int k = 0; k < 12; k++) {
+        const int d = 4 * k;
+        dst[k] = u32x4{raw[d / 6][d % 6], raw[(d + 1) / 6][(d + 1) % 6],
+                       raw[(d + 2) / 6][(d + 2) % 6], raw[(d + 3) / 6][(d + 3) % 6]};
     }
-    uint32_t bits[64];     /* tm bit patterns by zig-zag index; low 16 bits = the int16    */
-    uint32_t packed[32];   /* zig-zag pairs (2k, 2k+1) as one dword, formed when complete */
-    unsigned cnt = 0;
-    const jx_qtab &tab = g_qtab[a.quality];
-    const bool force = a.force_exact != 0;
-    u32x4 *o = (u32x4 *)out_blk;
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-        float col[8], F[8];
-#pragma unroll
-        for (int y = 0; y < 8; y++) col[y] = T[y][u];
-        jx_fdct8<FOps>(col, F);
-        float d[8];
-        uint64_t any = 0;   /* wave mask: lanes with a flagged coefficient in this column */
-#pragma unroll
-        for (int v = 0; v < 8; v++) {
-            const float w = tab.w[CH][u][v];
-            const float tm = __builtin_fmaf(F[v], w, kMagic);   /* rint(F*w) + magic  */
-            const float rr = tm - kMagic;                         /* exact             */
-            d[v] = __builtin_fmaf(F[v], w, -rr);                  /* F*w - rint(F*w)   */
-            bits[zz_of(v, u)] = __float_as_uint(tm);              /* low 16 bits = int16 */
-            any |= __ballot(__builtin_fabsf(d[v]) >= tab.lim[CH][u][v]);
-        }
-        /* rare (wave-uniform branch): some lane has a coefficient inside the guard band */
-        if (__builtin_expect(force || any != 0, 0)) {
-#pragma unroll
-            for (int v = 0; v < 8; v++) {
-                if (force || __builtin_fabsf(d[v]) >= tab.lim[CH][u][v]) {
-                    if (active && cnt < JX_SLOTS)
-                        a.g.slots[fidx * JX_SLOTS + cnt] = (uint8_t)zz_of(v, u);
-                    cnt++;
-                }
-            }
-        }
-        /* pack zig-zag pairs completed by this column; store 16-B chunks completed by it
-         * (compile-time decisions: the loops are fully unrolled) */
-#pragma unroll
-        for (int k = 0; k < 32; k++)
-            if (zz_col_done(2 * k, 2 * k + 1) == u)
-                packed[k] = __builtin_amdgcn_perm(bits[2 * k + 1], bits[2 * k], 0x05040100u);
-#pragma unroll
-        for (int j = 0; j < 8; j++)
-            if (zz_chunk_done(j) == u && active)
-                o[j] = u32x4{packed[4 * j], packed[4 * j + 1], packed[4 * j + 2], packed[4 * j + 3]};
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if (active) a.g.counts[fidx] = (uint8_t)cnt;
-    return cnt;
 }
 
-/* block index of this lane in tile t (clamped into range for the tail tile) */
-__device__ __forceinline__ unsigned tile_block(unsigned t, unsigned lane, unsigned total)
-{
-    const unsigned b = t * 64u + lane;
-    return b < total ? b : total - 1;
-}
-
-/*
- * Persistent: each wave walks tiles t, t + waves, ...; the next tile's 8 pixel rows are
- * loaded into registers before the current tile is transformed, so HBM latency overlaps the
- * ~3k VALU instructions of a tile instead of stalling every wave at its start.
- */
-__global__ __launch_bounds__(JX_WG, 2) void k_xform(const jx_xform_args a)
-{
-    const jx_geom &g = a.g;
-    const unsigned nb = (unsigned)g.nb;
-    const unsigned total = nb * (unsigned)g.nframes;
-    const unsigned ntiles = (total + 63u) / 64u;
-    const unsigned lane = threadIdx.x & 63u;
-    const unsigned nwaves = gridDim.x * (JX_WG / 64);
-    unsigned t = blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6);
-    if (t >= ntiles) return;                       /* whole wave */
-    const long long cs = (long long)nb * 64;
-    uint32_t raw[8][6];
-#if JX_PREFETCH
-    {
-        const unsigned b = tile_block(t, lane, total), f = b / nb;
-        load_block(g, f, b - f * nb, raw);
-    }
-#endif
-    for (; t < ntiles; t += nwaves) {
-        const unsigned b0 = t * 64u + lane;
-        const bool active = b0 < total;
-        const unsigned b = active ? b0 : total - 1;
-        const unsigned f = b / nb, bi = b - f * nb;
-        const unsigned tn = t + nwaves;
-#if JX_PREFETCH
-        uint32_t nxt[8][6];
-        if (tn < ntiles) {
-            const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
-            load_block(g, fn, bn - fn * nb, nxt);
-        }
-#else
-        load_block(g, f, bi, raw);
-#endif
-        int16_t *ob = g.out + (long long)f * g.out_fstride + (long long)bi * 64;
-        const unsigned fi = f * 3u * nb + bi;
-        unsigned c = xform_channel<0>(raw, a, active, ob, fi);
-        __builtin_amdgcn_sched_barrier(0);
-        c += xform_channel<1>(raw, a, active, ob + cs, fi + nb);
-        __builtin_amdgcn_sched_barrier(0);
-        c += xform_channel<2>(raw, a, active, ob + 2 * cs, fi + 2u * nb);
-        const uint64_t m = __ballot(active && c != 0);
-        if (lane == 0) g.tile_mask[t] = m;
-#if JX_PREFETCH
-        if (tn < ntiles) {
-#pragma unroll
-            for (int y = 0; y < 8; y++)
-#pragma unroll
-                for (int k = 0; k < 6; k++) raw[y][k] = nxt[y][k];
-        }
-#else
-        (void)tn;
-#endif
-    }
-}
+/* ---- exact path -------------------------------------------------------------------------- */
 
 /* Exact reference value of one channel pixel, level shift included (preprocess.c:160-162,
  * 186-188); r,g,b promoted int -> double as in the reference. */
@@ -305,7 +213,7 @@ __device__ __forceinline__ double exact_pixel(int ch, int r, int g, int b)
 }
 
 /* One coefficient in the reference's exact operation order.  px = the block's 8 pixel rows
- * (24 interleaved bytes each) in this thread's LDS slice. */
+ * (24 interleaved bytes each) in LDS. */
 __device__ int16_t exact_coef(const uint8_t *px, int ch, int u, int v, int q)
 {
     double cv[8];
@@ -326,49 +234,258 @@ __device__ int16_t exact_coef(const uint8_t *px, int ch, int u, int v, int q)
     return (int16_t)(int)round(F / (double)q);      /* quantise.c:58 */
 }
 
-/*
- * One thread per 64-block tile.  Nearly every tile has tile_mask == 0 and the thread leaves
- * after one 8-byte load; a flagged block is staged into LDS once and each of its flagged
- * coefficients (or all 64 of a block-channel whose slots overflowed) is recomputed exactly.
- */
-__global__ __launch_bounds__(64) void k_fixup(const jx_fix_args a)
+__device__ __forceinline__ int16_t *coef_ptr(const jx_geom &g, unsigned b, int ch, int zz)
 {
-    __shared__ uint8_t s_px[64][192];
+    const unsigned nb = (unsigned)g.nb, f = b / nb, bi = b - f * nb;
+    return g.out + (long long)f * g.out_fstride + ((long long)ch * nb + bi) * 64 + zz;
+}
+
+/* Process every queued coefficient of the wave, lanes in parallel.  Wave-uniform call. */
+JX_RARE void flush_queue(WaveLds &W, int nitem, const jx_geom &g, int quality,
+                                         unsigned lane)
+{
+    /* the fast-path values these overwrite were stored earlier by this wave */
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int i = (int)lane; i < nitem; i += 64) {
+        const uint32_t it = W.item[i];
+        const int slot = (int)(it & 31u), ch = (int)((it >> 5) & 3u), zz = (int)(it >> 7);
+        const int uv = kUnZZ[zz], u = uv & 7, v = uv >> 3;
+        const int q = g_qtab[quality].q[ch == 0 ? 0 : 1][u * 8 + v];
+        *coef_ptr(g, W.slot_blk[slot], ch, zz) =
+            exact_coef((const uint8_t *)W.px[slot], ch, u, v, q);
+    }
+}
+
+/* Whole block-channel in exact arithmetic, one lane per block (queue overflow).  Wave-uniform
+ * call; `mine` selects the lanes whose block-channel is recomputed. */
+JX_RARE void exact_block(WaveLds &W, const uint32_t (&raw)[8][6], bool mine,
+                                         unsigned b, int ch, const jx_geom &g, int quality,
+                                         unsigned lane)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    u32x4 *mypx = W.stage + lane * 12;      /* stage+px viewed as 64 x 192 B */
+    raw_to_lds(raw, mypx);
+    if (mine) {
+        int16_t *o = coef_ptr(g, b, ch, 0);
+        const int16_t *q = g_qtab[quality].q[ch == 0 ? 0 : 1];
+        for (int zz = 0; zz < 64; zz++) {
+            const int uv = kUnZZ[zz], u = uv & 7, v = uv >> 3;
+            o[zz] = exact_coef((const uint8_t *)mypx, ch, u, v, q[u * 8 + v]);
+        }
+    }
+}
+
+/* wave-uniform deferred-exact queue state */
+struct Queue {
+    int nslot, nitem;
+};
+
+/* ---- fast path --------------------------------------------------------------------------- */
+
+template <int CH>
+__device__ __forceinline__ void xform_channel(uint32_t (&raw)[8][6], const jx_xform_args &a,
+                                              WaveLds &W, Queue &Q, int &myslot, bool active,
+                                              unsigned b, unsigned t, unsigned lane)
+{
+    const jx_geom &g = a.g;
+    /* Opaque to the optimiser: forces each channel to re-convert its bytes instead of
+     * keeping 192 converted floats alive across the three channel passes (CSE). */
+#pragma unroll
+    for (int y = 0; y < 8; y++)
+#pragma unroll
+        for (int k = 0; k < 6; k++) asm volatile("" : "+v"(raw[y][k]));
+    float T[8][8];
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+        JX_SB_ROW();
+        float px[8];
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+            const float r = (float)byte_of(raw[y], 3 * x);
+            const float gg = (float)byte_of(raw[y], 3 * x + 1);
+            const float bb = (float)byte_of(raw[y], 3 * x + 2);
+            px[x] = jx_pixel<FOps, CH>(r, gg, bb);
+        }
+        jx_fdct8<FOps>(px, T[y]);
+    }
+    uint32_t bits[64];     /* tm bit patterns by zig-zag index; low 16 bits = the int16    */
+    uint32_t packed[32];   /* zig-zag pairs (2k, 2k+1) as one dword, formed when complete */
+    bool ovf = false;      /* this lane's block-channel did not fit the queue             */
+    const jx_qtab &tab = g_qtab[a.quality];
+    const bool force = a.force_exact != 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        float col[8], F[8];
+#pragma unroll
+        for (int y = 0; y < 8; y++) col[y] = T[y][u];
+        jx_fdct8<FOps>(col, F);
+        float d[8];
+        uint64_t any = 0;   /* wave mask: lanes with a flagged coefficient in this column */
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            const float w = tab.w[CH][u][v];
+            const float tm = __builtin_fmaf(F[v], w, kMagic);   /* rint(F*w) + magic  */
+            const float rr = tm - kMagic;                         /* exact             */
+            d[v] = __builtin_fmaf(F[v], w, -rr);                  /* F*w - rint(F*w)   */
+            bits[zz_of(v, u)] = __float_as_uint(tm);              /* low 16 bits = int16 */
+            any |= __ballot(__builtin_fabsf(d[v]) >= tab.lim[CH][u][v]);
+        }
+        /* rare (wave-uniform branch): some lane has a coefficient inside the guard band */
+        if (__builtin_expect(force || any != 0, 0)) {
+            uint32_t fm = 0;
+#pragma unroll
+            for (int v = 0; v < 8; v++)
+                if (force || __builtin_fabsf(d[v]) >= tab.lim[CH][u][v]) fm |= 1u << v;
+            fm = active && !ovf ? fm : 0u;
+            const uint64_t need = __ballot(fm != 0 && myslot < 0);
+            uint64_t mv[8];
+            int nnew = 0;
+#pragma unroll
+            for (int v = 0; v < 8; v++) {
+                mv[v] = __ballot((fm >> v) & 1u);
+                nnew += __popcll(mv[v]);
+            }
+            const int nneed = __popcll(need);
+            if (Q.nslot + nneed > kSlots || Q.nitem + nnew > kItems) {
+                ovf = ovf || fm != 0;             /* whole block-channel, exactly, later */
+            } else {
+                if ((need >> lane) & 1u) {
+                    myslot = Q.nslot + (int)__builtin_amdgcn_mbcnt_hi(
+                                           (uint32_t)(need >> 32),
+                                           __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                    raw_to_lds(raw, W.px[myslot]);
+                    W.slot_blk[myslot] = b;
+                }
+                Q.nslot += nneed;
+#pragma unroll
+                for (int v = 0; v < 8; v++) {
+                    if ((fm >> v) & 1u) {
+                        const int pos = Q.nitem + (int)__builtin_amdgcn_mbcnt_hi(
+                                                      (uint32_t)(mv[v] >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mv[v], 0u));
+                        W.item[pos] = (uint32_t)myslot | (uint32_t)CH << 5 |
+                                      (uint32_t)zz_of(v, u) << 7;
+                    }
+                    Q.nitem += __popcll(mv[v]);
+                }
+            }
+        }
+        /* pack zig-zag pairs completed by this column; stage the 16-B chunks it completes
+         * (compile-time decisions: the loops are fully unrolled) */
+#pragma unroll
+        for (int k = 0; k < 32; k++)
+            if (zz_col_done(2 * k, 2 * k + 1) == u)
+                packed[k] = __builtin_amdgcn_perm(bits[2 * k + 1], bits[2 * k], 0x05040100u);
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (zz_chunk_done(j) == u)
+                W.stage[lane * 9 + j] =
+                    u32x4{packed[4 * j], packed[4 * j + 1], packed[4 * j + 2], packed[4 * j + 3]};
+        JX_SB_COL();
+    }
+
+    /* coalesced store: the wave's 64 blocks x 128 B of this channel, 1 KiB per instruction */
+    const unsigned nb = (unsigned)g.nb, total = nb * (unsigned)g.nframes;
+    const unsigned b0 = t * 64u;
+    const unsigned f0 = b0 / nb, bl = std::min(b0 + 63u, total - 1u), fl = bl / nb;
+    if (f0 == fl && b0 + 63u < total) {
+        u32x4 *dst = (u32x4 *)(g.out + (long long)f0 * g.out_fstride +
+                               ((long long)CH * nb + (b0 - f0 * nb)) * 64);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const unsigned e = (unsigned)j * 64u + lane;
+            dst[e] = W.stage[(e >> 3) * 9 + (e & 7)];
+        }
+    } else {                                   /* tile crosses a frame end or the last tile */
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const unsigned e = (unsigned)j * 64u + lane, bb = b0 + (e >> 3);
+            if (bb < total)
+                *(u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8) = W.stage[(e >> 3) * 9 + (e & 7)];
+        }
+    }
+    /* queue overflow (rare; every lane in FORCE_EXACT mode): drain the queue, then each
+     * overflowed lane recomputes its whole block-channel exactly */
+    if (__builtin_expect(__ballot(ovf) != 0, 0)) {
+        if (Q.nitem) flush_queue(W, Q.nitem, g, a.quality, lane);
+        Q.nitem = Q.nslot = 0;
+        myslot = -1;
+        exact_block(W, raw, ovf, b, CH, g, a.quality, lane);
+    }
+}
+
+/* block index of this lane in tile t (clamped into range for the tail tile) */
+__device__ __forceinline__ unsigned tile_block(unsigned t, unsigned lane, unsigned total)
+{
+    const unsigned b = t * 64u + lane;
+    return b < total ? b : total - 1;
+}
+
+/*
+ * Persistent: each wave walks tiles t, t + waves, ...; the next tile's 8 pixel rows are
+ * loaded into registers before the current tile is transformed, so HBM latency overlaps the
+ * ~3k VALU instructions of a tile instead of stalling every wave at its start.
+ */
+__global__ __launch_bounds__(JX_WG, 2) void k_xform(const jx_xform_args a)
+{
+    __shared__ WaveLds s_wave[JX_WG / 64];
     const jx_geom &g = a.g;
     const unsigned nb = (unsigned)g.nb;
     const unsigned total = nb * (unsigned)g.nframes;
     const unsigned ntiles = (total + 63u) / 64u;
-    const unsigned t = blockIdx.x * 64u + threadIdx.x;
-    if (t >= ntiles) return;
-    uint64_t mask = g.tile_mask[t];
-    uint8_t *px = s_px[threadIdx.x];
-    while (mask) {
-        const unsigned L = (unsigned)__builtin_ctzll(mask);
-        mask &= mask - 1;
-        const unsigned b = t * 64u + L;
-        if (b >= total) break;
-        const unsigned f = b / nb, bi = b - f * nb;
-        uint32_t raw[8][6];
-        load_block(g, f, bi, raw);
-#pragma unroll
-        for (int y = 0; y < 8; y++)
-#pragma unroll
-            for (int k = 0; k < 6; k++) *(uint32_t *)(px + y * 24 + 4 * k) = raw[y][k];
-        for (int ch = 0; ch < 3; ch++) {
-            const unsigned i = (f * 3u + (unsigned)ch) * nb + bi;
-            const unsigned cnt = g.counts[i];
-            if (!cnt) continue;
-            int16_t *ob = g.out + (long long)f * g.out_fstride + ((long long)ch * nb + bi) * 64;
-            const int16_t *q = g_qtab[a.quality].q[ch == 0 ? 0 : 1];
-            const unsigned n = cnt > JX_SLOTS ? 64u : cnt;
-            for (unsigned k = 0; k < n; k++) {
-                const int z = cnt > JX_SLOTS ? (int)k : (int)g.slots[(size_t)i * JX_SLOTS + k];
-                const int uv = kUnZZ[z];
-                const int u = uv & 7, v = uv >> 3;
-                ob[z] = exact_coef(px, ch, u, v, q[u * 8 + v]);
-            }
-        }
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned nwaves = gridDim.x * (JX_WG / 64);
+    unsigned t = blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6);
+    if (t >= ntiles) return;                       /* whole wave */
+    WaveLds &W = s_wave[threadIdx.x >> 6];
+    Queue Q{0, 0};
+    uint32_t raw[8][6];
+#if JX_PREFETCH
+    {
+        const unsigned b = tile_block(t, lane, total), f = b / nb;
+        load_block(g, f, b - f * nb, raw);
     }
+#endif
+    for (; t < ntiles; t += nwaves) {
+        const unsigned b0 = t * 64u + lane;
+        const bool active = b0 < total;
+        const unsigned b = active ? b0 : total - 1;
+        const unsigned tn = t + nwaves;
+#if JX_PREFETCH
+        uint32_t nxt[8][6];
+        if (tn < ntiles) {
+            const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
+            load_block(g, fn, bn - fn * nb, nxt);
+        }
+#else
+        {
+            const unsigned f = b / nb;
+            load_block(g, f, b - f * nb, raw);
+        }
+#endif
+        int myslot = -1;
+        xform_channel<0>(raw, a, W, Q, myslot, active, b, t, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        xform_channel<1>(raw, a, W, Q, myslot, active, b, t, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        xform_channel<2>(raw, a, W, Q, myslot, active, b, t, lane);
+        /* queue nearly full: drain now, while the slots' blocks are still cheap to keep */
+        if (Q.nslot > kSlots - 8 || Q.nitem > kItems - 16) {
+            flush_queue(W, Q.nitem, g, a.quality, lane);
+            Q.nitem = Q.nslot = 0;
+        }
+#if JX_PREFETCH
+        if (tn < ntiles) {
+#pragma unroll
+            for (int y = 0; y < 8; y++)
+#pragma unroll
+                for (int k = 0; k < 6; k++) raw[y][k] = nxt[y][k];
+        }
+#else
+        (void)tn;
+#endif
+    }
+    if (Q.nitem) flush_queue(W, Q.nitem, g, a.quality, lane);
 }
 
 __device__ __forceinline__ uint8_t splitmix_byte(uint64_t seed, uint64_t k)
@@ -443,11 +560,6 @@ int tables_for_current_device()
     return g_tab_rc[dev];
 }
 
-/* workspace: [tile_mask u64 x ntiles][counts u8 x 3*total][slots u8 x 3*total*JX_SLOTS] */
-size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
-size_t ws_mask_bytes(size_t total) { return align256((total + 63) / 64 * 8); }
-size_t ws_count_bytes(size_t total) { return align256(3 * total); }
-
 /* resident waves of k_xform on the current device (persistent grid size) */
 int g_resident_waves[kMaxDev];
 std::once_flag g_res_once[kMaxDev];
@@ -474,9 +586,8 @@ extern "C" {
 
 size_t jpgx_workspace_size(const jpgx_frames *fr)
 {
-    if (!fr || fr->width <= 0 || fr->row_end <= fr->row_begin || fr->nframes <= 0) return 0;
-    const size_t total = (size_t)(fr->row_end - fr->row_begin) * (fr->width / 8) * fr->nframes;
-    return ws_mask_bytes(total) + ws_count_bytes(total) + 3 * total * JX_SLOTS;
+    (void)fr;
+    return 0;   /* the exact-fixup queue lives in LDS; no device workspace is needed */
 }
 
 int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
@@ -487,8 +598,9 @@ int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *
 
 int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
                        int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream,
-                       void *event_between)
+                       void *event_after)
 {
+    (void)d_workspace;
     if (!fr || !p) return JPGX_EARG;
     int rc = jpgx_validate(fr->width, fr->height, p);
     if (rc) return rc;
@@ -496,26 +608,24 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
         fr->nframes < 1)
         return JPGX_EARG;
     if (fr->row_begin == fr->row_end) return JPGX_OK;
-    if (!d_rgb || !d_out || !d_workspace) return JPGX_EARG;
+    if (!d_rgb || !d_out) return JPGX_EARG;
     if (fr->in_pitch < (size_t)fr->width * 3 || fr->in_pitch % 8 || fr->in_frame_stride % 8 ||
         ((uintptr_t)d_rgb & 7) || ((uintptr_t)d_out & 15) || fr->out_frame_stride % 8)
         return JPGX_EARG;
     const int bpr = fr->width / 8;
     const size_t nb = (size_t)(fr->row_end - fr->row_begin) * bpr;
     const size_t total = nb * fr->nframes;
-    if (3 * total >= (1ull << 31)) return JPGX_EARG;
+    if (total + 64 >= (1ull << 32)) return JPGX_EARG;
     if (fr->nframes > 1 && fr->out_frame_stride < 3 * nb * 64) return JPGX_EARG;
+    if (fr->nframes > 1 && fr->in_frame_stride < fr->in_pitch * (size_t)(fr->row_end - fr->row_begin) * 8)
+        return JPGX_EARG;
     if (workspace_bytes < jpgx_workspace_size(fr)) return JPGX_EWORKSPACE;
 
     jx_xform_args xa;
-    jx_fix_args fa;
     memset(&xa, 0, sizeof xa);
     jx_geom &g = xa.g;
     g.rgb = d_rgb;
     g.out = d_out;
-    g.tile_mask = (uint64_t *)d_workspace;
-    g.counts = (uint8_t *)d_workspace + ws_mask_bytes(total);
-    g.slots = g.counts + ws_count_bytes(total);
     g.in_pitch = (long long)fr->in_pitch;
     g.in_fstride = (long long)fr->in_frame_stride;
     g.out_fstride = (long long)fr->out_frame_stride;
@@ -528,8 +638,6 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     if (rc) return rc;
     xa.quality = p->quality;
     xa.force_exact = (p->flags & JPGX_FLAG_FORCE_EXACT) ? 1 : 0;
-    fa.g = g;
-    fa.quality = p->quality;
 
     hipStream_t s = (hipStream_t)stream;
     const size_t ntiles = (total + 63) / 64;
@@ -538,12 +646,8 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     hipLaunchKernelGGL(k_xform, dim3(grid), dim3(JX_WG), 0, s, xa);
     rc = hip_rc(hipGetLastError());
     if (rc) return rc;
-    if (event_between) {
-        rc = hip_rc(hipEventRecord((hipEvent_t)event_between, s));
-        if (rc) return rc;
-    }
-    hipLaunchKernelGGL(k_fixup, dim3((unsigned)((ntiles + 63) / 64)), dim3(64), 0, s, fa);
-    return hip_rc(hipGetLastError());
+    if (event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
+    return rc;
 }
 
 int jpgx_gen_splitmix_gpu(uint8_t *d_dst, size_t nbytes, uint64_t seed, void *stream)
@@ -595,16 +699,15 @@ static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
     fr.row_end = r1;
     fr.nframes = 1;
     fr.in_pitch = dpitch;
+    fr.in_frame_stride = dpitch * rows;
     fr.out_frame_stride = 3 * nb_s * 64;
-    const size_t ws = jpgx_workspace_size(&fr);
     uint8_t *d_in = nullptr;
     int16_t *d_out = nullptr;
-    void *d_ws = nullptr;
     hipStream_t s = nullptr;
     int rc = JPGX_OK;
     if (hipMalloc(&d_in, rows * dpitch) != hipSuccess ||
         hipMalloc(&d_out, 3 * nb_s * 64 * sizeof(int16_t)) != hipSuccess ||
-        hipMalloc(&d_ws, ws) != hipSuccess || hipStreamCreate(&s) != hipSuccess) {
+        hipStreamCreate(&s) != hipSuccess) {
         rc = JPGX_EHIP;
     }
     if (!rc) {
@@ -612,7 +715,7 @@ static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
         rc = hip_rc(hipMemcpy2DAsync(d_in, dpitch, src, pitch, row_bytes, rows,
                                      hipMemcpyHostToDevice, s));
     }
-    if (!rc) rc = jpgx_blocks_gpu(&fr, p, d_in + halo * dpitch, d_out, d_ws, ws, s);
+    if (!rc) rc = jpgx_blocks_gpu(&fr, p, d_in + halo * dpitch, d_out, nullptr, 0, s);
     for (int ch = 0; ch < 3 && !rc; ch++)
         rc = hip_rc(hipMemcpyAsync(out + ((size_t)ch * nb + (size_t)r0 * bpr) * 64,
                                    d_out + (size_t)ch * nb_s * 64, nb_s * 64 * sizeof(int16_t),
@@ -621,7 +724,6 @@ static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
     if (s) (void)hipStreamDestroy(s);
     (void)hipFree(d_in);
     (void)hipFree(d_out);
-    (void)hipFree(d_ws);
     return rc;
 }
 

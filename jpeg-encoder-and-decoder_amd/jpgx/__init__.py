@@ -19,7 +19,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libjpgx.so")
+LIB_PATH = os.environ.get("JPGX_LIB") or os.path.join(PKG_ROOT, "lib", "libjpgx.so")
 
 NO_CHROMA_SUBSAMPLING = 0
 HORIZONTAL_SUBSAMPLING = 1

@@ -136,10 +136,13 @@ def test_invalid_arguments_gpu(cuda):
     assert e.value.rc == jpgx.EGEOMETRY
     fr = jpgx.frames(16, 16)
     out = torch.zeros((3, 4, 64), dtype=torch.int16, device=cuda)
-    small = torch.empty(8, dtype=torch.uint8, device=cuda)
-    with pytest.raises(jpgx.JpgxError) as e:
-        jpgx.blocks_gpu(fr, jpgx.default_params(16, 16, 50), rgb, out, small)
-    assert e.value.rc == jpgx.EWORKSPACE
+    with pytest.raises(jpgx.JpgxError) as e:        # misaligned input pointer
+        jpgx.blocks_gpu(fr, jpgx.default_params(16, 16, 50), rgb.data_ptr() + 3, out, 0)
+    assert e.value.rc == jpgx.EARG
+    with pytest.raises(jpgx.JpgxError) as e:        # stripe beyond the frame
+        jpgx.blocks_gpu(jpgx.frames(16, 16, rows=(1, 3)), jpgx.default_params(16, 16, 50), rgb,
+                        out, 0)
+    assert e.value.rc == jpgx.EARG
 
 
 def test_gpu_generators_match_oracle(cuda):

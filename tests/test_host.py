@@ -96,7 +96,6 @@ def test_kernel_cos_table_is_glibc():
 
 
 def test_workspace_size():
-    fr = jpgx.frames(3840, 2160, nframes=8)
-    nb = 480 * 270
-    assert jpgx.workspace_size(fr) >= 8 * 3 * nb * 8
+    # the exact-fixup queue lives in LDS: no device workspace for any geometry
+    assert jpgx.workspace_size(jpgx.frames(3840, 2160, nframes=8)) == 0
     assert jpgx.workspace_size(jpgx.frames(64, 64, rows=(3, 3))) == 0

@@ -47,6 +47,7 @@ __global__ __launch_bounds__(256) void k_pattern(Geo g)
         for (int y = 0; y < 8; y++)
 #pragma unroll
             for (int k = 0; k < 6; k++) acc = acc * 31u + raw[y][k];
+        if (!(MODE & 6) && acc == 0x12345u) g.out[b] = 1;   /* keep the loads alive */
     }
     const unsigned f = b / g.nb, bi = b - f * g.nb;
     for (int ch = 0; ch < 3; ch++) {
@@ -110,7 +111,7 @@ int main()
     run("wr_coal", [&] { hipLaunchKernelGGL(k_pattern<4>, dim3(grid), dim3(256), 0, 0, g); }, (double)out_bytes);
     run("rw_lane", [&] { hipLaunchKernelGGL(k_pattern<3>, dim3(grid), dim3(256), 0, 0, g); }, (double)(in_bytes + out_bytes));
     run("rw_coal", [&] { hipLaunchKernelGGL(k_pattern<5>, dim3(grid), dim3(256), 0, 0, g); }, (double)(in_bytes + out_bytes));
-    const size_t n16 = (in_bytes + out_bytes) / 2 / 16;
+    const size_t n16 = out_bytes / 2 / 16;   /* copy half of the output buffer onto its other half */
     run("copy", [&] { hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, 0, (const u32x4 *)dout, (u32x4 *)dout + n16, n16); }, (double)n16 * 32);
     return 0;
 }
