@@ -40,7 +40,7 @@
 namespace {
 
 #ifndef JX_PREFETCH
-#define JX_PREFETCH 1   /* load tile t+1 into registers while tile t is transformed */
+#define JX_PREFETCH 2   /* input prefetch mode, see k_xform */
 #endif
 #ifndef JX_ROW_SB       /* scheduling fence between the row DCTs of a channel          */
 #define JX_ROW_SB 1
@@ -61,6 +61,12 @@ namespace {
 #else
 #define JX_SB_COL() ((void)0)
 #endif
+#ifndef JX_WPE          /* minimum waves per SIMD the register allocation must allow    */
+#define JX_WPE 2
+#endif
+#ifndef JX_DBG_NO_EXACT  /* debug/measurement only: drop the exact path (NOT bit-exact)    */
+#define JX_DBG_NO_EXACT 0
+#endif
 #if JX_EXACT_INLINE
 #define JX_RARE __device__
 #else
@@ -68,8 +74,12 @@ namespace {
 #endif
 
 constexpr float kMagic = 12582912.0f; /* 1.5 * 2^23: x + kMagic rounds x to an integer   */
-constexpr int kSlots = 32;            /* per-wave deferred-exact queue: block pixel slots  */
-constexpr int kItems = 64;            /*                                 and coefficients  */
+#ifndef JX_SLOTS_PER_WAVE
+#define JX_SLOTS_PER_WAVE 16
+#endif
+constexpr int kSlots = JX_SLOTS_PER_WAVE; /* per-wave deferred-exact queue: pixel slots    */
+constexpr int kItems = 64;                /*                             and coefficients  */
+static_assert(kSlots <= 32, "item encoding keeps 5 bits for the slot");
 
 /* zig_zag.c:6-15: scan position of natural (row v, column u) */
 __host__ __device__ constexpr int zz_of(int v, int u)
@@ -256,15 +266,32 @@ JX_RARE void flush_queue(WaveLds &W, int nitem, const jx_geom &g, int quality,
     }
 }
 
+/* Copy block b's 8 pixel rows (reference addressing, see load_block) into LDS, one dword at
+ * a time (rare path: keeps the register budget of the fast path untouched). */
+__device__ __forceinline__ void stage_block_px(const jx_geom &g, unsigned b, uint32_t *dst)
+{
+    const unsigned nb = (unsigned)g.nb, f = b / nb, bi = b - f * nb;
+    const unsigned r = bi / (unsigned)g.bpr, c = bi - r * (unsigned)g.bpr;
+    const bool last = c == (unsigned)g.bpr - 1;
+    const bool under = last && (g.row0 + (int)r == 0);
+    const long long row = 8ll * r - (last ? 1 : 0);
+    const uint8_t *base = g.rgb + (long long)f * g.in_fstride + row * g.in_pitch + 24ll * c;
+#pragma unroll 1
+    for (int k = 0; k < 48; k++) {
+        const int y = k / 6, w = k - 6 * (k / 6);
+        dst[k] = (y == 0 && under) ? g.under[w]
+                                   : *(const uint32_t *)(base + (long long)y * g.in_pitch + 4 * w);
+    }
+}
+
 /* Whole block-channel in exact arithmetic, one lane per block (queue overflow).  Wave-uniform
  * call; `mine` selects the lanes whose block-channel is recomputed. */
-JX_RARE void exact_block(WaveLds &W, const uint32_t (&raw)[8][6], bool mine,
-                                         unsigned b, int ch, const jx_geom &g, int quality,
-                                         unsigned lane)
+JX_RARE void exact_block(WaveLds &W, bool mine, unsigned b, int ch, const jx_geom &g,
+                         int quality, unsigned lane)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     u32x4 *mypx = W.stage + lane * 12;      /* stage+px viewed as 64 x 192 B */
-    raw_to_lds(raw, mypx);
+    stage_block_px(g, b, (uint32_t *)mypx);
     if (mine) {
         int16_t *o = coef_ptr(g, b, ch, 0);
         const int16_t *q = g_qtab[quality].q[ch == 0 ? 0 : 1];
@@ -282,19 +309,16 @@ struct Queue {
 
 /* ---- fast path --------------------------------------------------------------------------- */
 
+/* Row pass of channel CH: bytes -> pixel values -> 1-D DCT of each of the 8 pixel rows. */
 template <int CH>
-__device__ __forceinline__ void xform_channel(uint32_t (&raw)[8][6], const jx_xform_args &a,
-                                              WaveLds &W, Queue &Q, int &myslot, bool active,
-                                              unsigned b, unsigned t, unsigned lane)
+__device__ __forceinline__ void xform_rows(uint32_t (&raw)[8][6], float (&T)[8][8])
 {
-    const jx_geom &g = a.g;
     /* Opaque to the optimiser: forces each channel to re-convert its bytes instead of
      * keeping 192 converted floats alive across the three channel passes (CSE). */
 #pragma unroll
     for (int y = 0; y < 8; y++)
 #pragma unroll
         for (int k = 0; k < 6; k++) asm volatile("" : "+v"(raw[y][k]));
-    float T[8][8];
 #pragma unroll
     for (int y = 0; y < 8; y++) {
         JX_SB_ROW();
@@ -308,6 +332,15 @@ __device__ __forceinline__ void xform_channel(uint32_t (&raw)[8][6], const jx_xf
         }
         jx_fdct8<FOps>(px, T[y]);
     }
+}
+
+/* Column pass, quantisation, zig-zag, LDS staging + coalesced store of channel CH. */
+template <int CH>
+__device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args &a,
+                                           WaveLds &W, Queue &Q, int &myslot, bool active,
+                                           unsigned b, unsigned t, unsigned lane)
+{
+    const jx_geom &g = a.g;
     uint32_t bits[64];     /* tm bit patterns by zig-zag index; low 16 bits = the int16    */
     uint32_t packed[32];   /* zig-zag pairs (2k, 2k+1) as one dword, formed when complete */
     bool ovf = false;      /* this lane's block-channel did not fit the queue             */
@@ -331,7 +364,7 @@ __device__ __forceinline__ void xform_channel(uint32_t (&raw)[8][6], const jx_xf
             any |= __ballot(__builtin_fabsf(d[v]) >= tab.lim[CH][u][v]);
         }
         /* rare (wave-uniform branch): some lane has a coefficient inside the guard band */
-        if (__builtin_expect(force || any != 0, 0)) {
+        if (!JX_DBG_NO_EXACT && __builtin_expect(force || any != 0, 0)) {
             uint32_t fm = 0;
 #pragma unroll
             for (int v = 0; v < 8; v++)
@@ -353,7 +386,7 @@ __device__ __forceinline__ void xform_channel(uint32_t (&raw)[8][6], const jx_xf
                     myslot = Q.nslot + (int)__builtin_amdgcn_mbcnt_hi(
                                            (uint32_t)(need >> 32),
                                            __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                    raw_to_lds(raw, W.px[myslot]);
+                    stage_block_px(g, b, (uint32_t *)W.px[myslot]);
                     W.slot_blk[myslot] = b;
                 }
                 Q.nslot += nneed;
@@ -406,11 +439,11 @@ __device__ __forceinline__ void xform_channel(uint32_t (&raw)[8][6], const jx_xf
     }
     /* queue overflow (rare; every lane in FORCE_EXACT mode): drain the queue, then each
      * overflowed lane recomputes its whole block-channel exactly */
-    if (__builtin_expect(__ballot(ovf) != 0, 0)) {
+    if (!JX_DBG_NO_EXACT && __builtin_expect(__ballot(ovf) != 0, 0)) {
         if (Q.nitem) flush_queue(W, Q.nitem, g, a.quality, lane);
         Q.nitem = Q.nslot = 0;
         myslot = -1;
-        exact_block(W, raw, ovf, b, CH, g, a.quality, lane);
+        exact_block(W, ovf, b, CH, g, a.quality, lane);
     }
 }
 
@@ -422,11 +455,14 @@ __device__ __forceinline__ unsigned tile_block(unsigned t, unsigned lane, unsign
 }
 
 /*
- * Persistent: each wave walks tiles t, t + waves, ...; the next tile's 8 pixel rows are
- * loaded into registers before the current tile is transformed, so HBM latency overlaps the
- * ~3k VALU instructions of a tile instead of stalling every wave at its start.
+ * Persistent: each wave walks tiles t, t + waves, ...  Input prefetch (JX_PREFETCH):
+ *   0  load the tile's rows at its start (the wait also drains the previous tile's stores)
+ *   1  load tile t+1 into a second register set at the start of tile t (+48 VGPRs)
+ *   2  load tile t+1 into the same registers as soon as tile t's last row pass has consumed
+ *      them; the last column pass and its stores then overlap the load latency, and the
+ *      wait at the next tile start leaves the youngest stores in flight.
  */
-__global__ __launch_bounds__(JX_WG, 2) void k_xform(const jx_xform_args a)
+__global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
 {
     __shared__ WaveLds s_wave[JX_WG / 64];
     const jx_geom &g = a.g;
@@ -451,30 +487,40 @@ __global__ __launch_bounds__(JX_WG, 2) void k_xform(const jx_xform_args a)
         const bool active = b0 < total;
         const unsigned b = active ? b0 : total - 1;
         const unsigned tn = t + nwaves;
-#if JX_PREFETCH
+#if JX_PREFETCH == 1
         uint32_t nxt[8][6];
         if (tn < ntiles) {
             const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
             load_block(g, fn, bn - fn * nb, nxt);
         }
-#else
+#elif JX_PREFETCH == 0
         {
             const unsigned f = b / nb;
             load_block(g, f, b - f * nb, raw);
         }
 #endif
         int myslot = -1;
-        xform_channel<0>(raw, a, W, Q, myslot, active, b, t, lane);
+        float T[8][8];
+        xform_rows<0>(raw, T);
+        xform_cols<0>(T, a, W, Q, myslot, active, b, t, lane);
         __builtin_amdgcn_sched_barrier(0);
-        xform_channel<1>(raw, a, W, Q, myslot, active, b, t, lane);
+        xform_rows<1>(raw, T);
+        xform_cols<1>(T, a, W, Q, myslot, active, b, t, lane);
         __builtin_amdgcn_sched_barrier(0);
-        xform_channel<2>(raw, a, W, Q, myslot, active, b, t, lane);
+        xform_rows<2>(raw, T);
+#if JX_PREFETCH == 2
+        if (tn < ntiles) {                          /* raw is dead: refill it for tile tn */
+            const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
+            load_block(g, fn, bn - fn * nb, raw);
+        }
+#endif
+        xform_cols<2>(T, a, W, Q, myslot, active, b, t, lane);
         /* queue nearly full: drain now, while the slots' blocks are still cheap to keep */
         if (Q.nslot > kSlots - 8 || Q.nitem > kItems - 16) {
             flush_queue(W, Q.nitem, g, a.quality, lane);
             Q.nitem = Q.nslot = 0;
         }
-#if JX_PREFETCH
+#if JX_PREFETCH == 1
         if (tn < ntiles) {
 #pragma unroll
             for (int y = 0; y < 8; y++)
