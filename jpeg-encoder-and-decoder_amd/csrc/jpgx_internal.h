@@ -31,9 +31,14 @@ struct jx_geom {
  * Column-major ([ch][u][v]) so one column's 8 entries are one scalar load. */
 struct jx_qtab {
     float w[3][8][8];       /* [ch][u][v]: fp32 scale of coefficient (u,v), 1/Q folded    */
-    float lim[3][8][8];     /* [ch][u][v]: |t - rint(t)| >= lim -> exact path             */
     int16_t q[2][64];       /* scaled tables, q[t][u*8+v] = Qs[u][v] as the reference
                                indexes them (src/quantise.c:58)                           */
+};
+
+/* guard band: |t - rint(t)| >= lim -> exact path.  [0] = rigorous band, [1] = FORCE_EXACT
+ * (every entry -1: every coefficient takes the exact path) */
+struct jx_limtab {
+    float lim[3][8][8];     /* [ch][u][v] */
 };
 
 #define JX_MAXQ 97

@@ -40,7 +40,7 @@
 namespace {
 
 #ifndef JX_PREFETCH
-#define JX_PREFETCH 2   /* input prefetch mode, see k_xform */
+#define JX_PREFETCH 0   /* input prefetch mode, see k_xform */
 #endif
 #ifndef JX_ROW_SB       /* scheduling fence between the row DCTs of a channel          */
 #define JX_ROW_SB 1
@@ -63,6 +63,9 @@ namespace {
 #endif
 #ifndef JX_WPE          /* minimum waves per SIMD the register allocation must allow    */
 #define JX_WPE 2
+#endif
+#ifndef JX_DBG_FLAGMODE  /* debug only: 0 full guard-band bookkeeping (the product)        */
+#define JX_DBG_FLAGMODE 0
 #endif
 #ifndef JX_DBG_NO_EXACT  /* debug/measurement only: drop the exact path (NOT bit-exact)    */
 #define JX_DBG_NO_EXACT 0
@@ -141,6 +144,7 @@ __constant__ double kCos[8][8] = {
 /* Per-quality tables (index 0 unused), constant address space so that wave-uniform reads
  * become scalar loads; filled once per device by tables_for_current_device(). */
 __constant__ jx_qtab g_qtab[JX_MAXQ + 1];
+__constant__ jx_limtab g_lim[2][JX_MAXQ + 1];
 
 /* dct.c:13 ALPHA(0) = 1/sqrt(2) as the reference's double */
 constexpr double kAlpha0 = 0x1.6a09e667f3bccp-1;
@@ -266,46 +270,119 @@ JX_RARE void flush_queue(WaveLds &W, int nitem, const jx_geom &g, int quality,
     }
 }
 
-/* Copy block b's 8 pixel rows (reference addressing, see load_block) into LDS, one dword at
- * a time (rare path: keeps the register budget of the fast path untouched). */
-__device__ __forceinline__ void stage_block_px(const jx_geom &g, unsigned b, uint32_t *dst)
-{
-    const unsigned nb = (unsigned)g.nb, f = b / nb, bi = b - f * nb;
-    const unsigned r = bi / (unsigned)g.bpr, c = bi - r * (unsigned)g.bpr;
-    const bool last = c == (unsigned)g.bpr - 1;
-    const bool under = last && (g.row0 + (int)r == 0);
-    const long long row = 8ll * r - (last ? 1 : 0);
-    const uint8_t *base = g.rgb + (long long)f * g.in_fstride + row * g.in_pitch + 24ll * c;
-#pragma unroll 1
-    for (int k = 0; k < 48; k++) {
-        const int y = k / 6, w = k - 6 * (k / 6);
-        dst[k] = (y == 0 && under) ? g.under[w]
-                                   : *(const uint32_t *)(base + (long long)y * g.in_pitch + 4 * w);
-    }
-}
-
-/* Whole block-channel in exact arithmetic, one lane per block (queue overflow).  Wave-uniform
- * call; `mine` selects the lanes whose block-channel is recomputed. */
-JX_RARE void exact_block(WaveLds &W, bool mine, unsigned b, int ch, const jx_geom &g,
-                         int quality, unsigned lane)
-{
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    u32x4 *mypx = W.stage + lane * 12;      /* stage+px viewed as 64 x 192 B */
-    stage_block_px(g, b, (uint32_t *)mypx);
-    if (mine) {
-        int16_t *o = coef_ptr(g, b, ch, 0);
-        const int16_t *q = g_qtab[quality].q[ch == 0 ? 0 : 1];
-        for (int zz = 0; zz < 64; zz++) {
-            const int uv = kUnZZ[zz], u = uv & 7, v = uv >> 3;
-            o[zz] = exact_coef((const uint8_t *)mypx, ch, u, v, q[u * 8 + v]);
-        }
-    }
-}
-
 /* wave-uniform deferred-exact queue state */
 struct Queue {
     int nslot, nitem;
 };
+
+/* number of set bits of m below this lane */
+__device__ __forceinline__ int lane_rank(uint64_t m)
+{
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ void drain(WaveLds &W, Queue &Q, int &myslot, const jx_geom &g,
+                                      int quality, unsigned lane)
+{
+    if (Q.nitem) flush_queue(W, Q.nitem, g, quality, lane);
+    Q.nitem = Q.nslot = 0;
+    myslot = -1;
+}
+
+/* Per lane: block-channels whose exact work did not fit the queue during the tile. */
+struct Pending {
+    unsigned bits;          /* bit ch: channel ch of this lane's block is pending          */
+    int idx0, idx1, idx2;   /* per channel: the single flagged zig-zag index, or -1 = all 64 */
+};
+
+/*
+ * Admit `single` lanes (one flagged coefficient, zig-zag `idx`) of channel CH into the
+ * queue without draining it (the channel passes run at full register pressure): lanes that
+ * do not fit, and block-channels with several flags (`multi`, all 64 coefficients), are
+ * left pending for settle_pending() at the end of the tile.  Wave-uniform call.
+ */
+template <int CH>
+__device__ __forceinline__ void admit_flags(WaveLds &W, Queue &Q, int &myslot,
+                                            const uint32_t (&raw)[8][6], unsigned b, bool single,
+                                            bool multi, int idx, unsigned lane, Pending &P)
+{
+    const uint64_t S = __ballot(single);
+    const uint64_t needs = S & __ballot(myslot < 0);
+    const bool admit = single && lane_rank(S) < kItems - Q.nitem &&
+                       (myslot >= 0 || lane_rank(needs) < kSlots - Q.nslot);
+    const uint64_t A = __ballot(admit);
+    const uint64_t fresh = A & needs;
+    if (admit && myslot < 0) {
+        myslot = Q.nslot + lane_rank(fresh);
+        raw_to_lds(raw, W.px[myslot]);
+        W.slot_blk[myslot] = b;
+    }
+    if (admit)
+        W.item[Q.nitem + lane_rank(A)] = (uint32_t)myslot | (uint32_t)CH << 5 | (uint32_t)idx << 7;
+    Q.nslot += __popcll(fresh);
+    Q.nitem += __popcll(A);
+    if ((single && !admit) || multi) {
+        P.bits |= 1u << CH;
+        const int id = multi ? -1 : idx;
+        if (CH == 0) P.idx0 = id;
+        if (CH == 1) P.idx1 = id;
+        if (CH == 2) P.idx2 = id;
+    }
+}
+
+/*
+ * End of tile: queue every pending block-channel, draining the queue (lane-parallel exact
+ * pass) as often as needed.  Pixel rows come from `raw`, still this tile's.  Wave-uniform.
+ */
+__device__ void settle_pending(WaveLds &W, Queue &Q, int &myslot, const uint32_t (&raw)[8][6],
+                               unsigned b, Pending &P, const jx_geom &g, int quality,
+                               unsigned lane)
+{
+#pragma unroll 1
+    for (int ch = 0; ch < 3; ch++) {
+        const bool pend = (P.bits >> ch) & 1u;
+        const int id = ch == 0 ? P.idx0 : (ch == 1 ? P.idx1 : P.idx2);
+        uint64_t S = __ballot(pend && id >= 0);
+        while (S) {                               /* singles, as many as fit per drain */
+            const uint64_t needs = S & __ballot(myslot < 0);
+            const bool admit = ((S >> lane) & 1u) && lane_rank(S) < kItems - Q.nitem &&
+                               (myslot >= 0 || lane_rank(needs) < kSlots - Q.nslot);
+            const uint64_t A = __ballot(admit);
+            if (!A) {
+                drain(W, Q, myslot, g, quality, lane);
+                continue;
+            }
+            const uint64_t fresh = A & needs;
+            if (admit && myslot < 0) {
+                myslot = Q.nslot + lane_rank(fresh);
+                raw_to_lds(raw, W.px[myslot]);
+                W.slot_blk[myslot] = b;
+            }
+            if (admit)
+                W.item[Q.nitem + lane_rank(A)] =
+                    (uint32_t)myslot | (uint32_t)ch << 5 | (uint32_t)id << 7;
+            Q.nslot += __popcll(fresh);
+            Q.nitem += __popcll(A);
+            S &= ~A;
+        }
+        uint64_t M = __ballot(pend && id < 0);
+        while (M) {                               /* whole block-channels: 64 items each */
+            const unsigned L = (unsigned)__builtin_ctzll(M);
+            M &= M - 1;
+            drain(W, Q, myslot, g, quality, lane);
+            if (lane == L) {
+                raw_to_lds(raw, W.px[0]);
+                W.slot_blk[0] = b;
+            }
+            W.item[lane] = 0u | (uint32_t)ch << 5 | lane << 7;   /* zig-zag index = lane */
+            Q.nslot = 1;
+            Q.nitem = 64;
+            drain(W, Q, myslot, g, quality, lane);
+        }
+    }
+    P.bits = 0;
+}
 
 /* ---- fast path --------------------------------------------------------------------------- */
 
@@ -336,71 +413,48 @@ __device__ __forceinline__ void xform_rows(uint32_t (&raw)[8][6], float (&T)[8][
 
 /* Column pass, quantisation, zig-zag, LDS staging + coalesced store of channel CH. */
 template <int CH>
-__device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args &a,
-                                           WaveLds &W, Queue &Q, int &myslot, bool active,
-                                           unsigned b, unsigned t, unsigned lane)
+__device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&raw)[8][6],
+                                           const jx_xform_args &a, WaveLds &W, Queue &Q,
+                                           int &myslot, Pending &P, bool active, unsigned b,
+                                           unsigned t, unsigned lane)
 {
     const jx_geom &g = a.g;
     uint32_t bits[64];     /* tm bit patterns by zig-zag index; low 16 bits = the int16    */
     uint32_t packed[32];   /* zig-zag pairs (2k, 2k+1) as one dword, formed when complete */
-    bool ovf = false;      /* this lane's block-channel did not fit the queue             */
     const jx_qtab &tab = g_qtab[a.quality];
+    const jx_limtab &band = g_lim[a.force_exact ? 1 : 0][a.quality];
     const bool force = a.force_exact != 0;
+    /* guard-band bookkeeping, branch-free: per lane the zig-zag index of its (last) flagged
+     * coefficient; wave masks of lanes with >= 1 and with >= 2 flags in this channel */
+    int idx = 0;
+    uint64_t seen = 0, dup = 0;
 #pragma unroll
     for (int u = 0; u < 8; u++) {
         float col[8], F[8];
 #pragma unroll
         for (int y = 0; y < 8; y++) col[y] = T[y][u];
         jx_fdct8<FOps>(col, F);
-        float d[8];
-        uint64_t any = 0;   /* wave mask: lanes with a flagged coefficient in this column */
 #pragma unroll
         for (int v = 0; v < 8; v++) {
             const float w = tab.w[CH][u][v];
             const float tm = __builtin_fmaf(F[v], w, kMagic);   /* rint(F*w) + magic  */
             const float rr = tm - kMagic;                         /* exact             */
-            d[v] = __builtin_fmaf(F[v], w, -rr);                  /* F*w - rint(F*w)   */
+            const float d = __builtin_fmaf(F[v], w, -rr);         /* F*w - rint(F*w)   */
             bits[zz_of(v, u)] = __float_as_uint(tm);              /* low 16 bits = int16 */
-            any |= __ballot(__builtin_fabsf(d[v]) >= tab.lim[CH][u][v]);
-        }
-        /* rare (wave-uniform branch): some lane has a coefficient inside the guard band */
-        if (!JX_DBG_NO_EXACT && __builtin_expect(force || any != 0, 0)) {
-            uint32_t fm = 0;
-#pragma unroll
-            for (int v = 0; v < 8; v++)
-                if (force || __builtin_fabsf(d[v]) >= tab.lim[CH][u][v]) fm |= 1u << v;
-            fm = active && !ovf ? fm : 0u;
-            const uint64_t need = __ballot(fm != 0 && myslot < 0);
-            uint64_t mv[8];
-            int nnew = 0;
-#pragma unroll
-            for (int v = 0; v < 8; v++) {
-                mv[v] = __ballot((fm >> v) & 1u);
-                nnew += __popcll(mv[v]);
-            }
-            const int nneed = __popcll(need);
-            if (Q.nslot + nneed > kSlots || Q.nitem + nnew > kItems) {
-                ovf = ovf || fm != 0;             /* whole block-channel, exactly, later */
-            } else {
-                if ((need >> lane) & 1u) {
-                    myslot = Q.nslot + (int)__builtin_amdgcn_mbcnt_hi(
-                                           (uint32_t)(need >> 32),
-                                           __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                    stage_block_px(g, b, (uint32_t *)W.px[myslot]);
-                    W.slot_blk[myslot] = b;
-                }
-                Q.nslot += nneed;
-#pragma unroll
-                for (int v = 0; v < 8; v++) {
-                    if ((fm >> v) & 1u) {
-                        const int pos = Q.nitem + (int)__builtin_amdgcn_mbcnt_hi(
-                                                      (uint32_t)(mv[v] >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mv[v], 0u));
-                        W.item[pos] = (uint32_t)myslot | (uint32_t)CH << 5 |
-                                      (uint32_t)zz_of(v, u) << 7;
-                    }
-                    Q.nitem += __popcll(mv[v]);
-                }
+            if (!JX_DBG_NO_EXACT) {
+                const bool fl = __builtin_fabsf(d) >= band.lim[CH][u][v];
+                const uint64_t m = __ballot(fl);
+                /* pinned here (SALU): left to the compiler, the 64 masks of a channel are
+                 * kept alive until the end and spilled to VGPR lanes */
+                uint64_t tmp;
+                asm volatile("s_and_b64 %[t], %[m], %[seen]\n\t"
+                             "s_or_b64 %[dup], %[dup], %[t]\n\t"
+                             "s_or_b64 %[seen], %[seen], %[m]\n\t"
+                             "v_cndmask_b32_e64 %[idx], %[idx], %[z], %[m]"
+                             : [dup] "+s"(dup), [seen] "+s"(seen), [t] "=&s"(tmp),
+                               [idx] "+v"(idx)
+                             : [m] "s"(m), [z] "n"(zz_of(v, u))
+                             : "scc");
             }
         }
         /* pack zig-zag pairs completed by this column; stage the 16-B chunks it completes
@@ -437,13 +491,12 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
                 *(u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8) = W.stage[(e >> 3) * 9 + (e & 7)];
         }
     }
-    /* queue overflow (rare; every lane in FORCE_EXACT mode): drain the queue, then each
-     * overflowed lane recomputes its whole block-channel exactly */
-    if (!JX_DBG_NO_EXACT && __builtin_expect(__ballot(ovf) != 0, 0)) {
-        if (Q.nitem) flush_queue(W, Q.nitem, g, a.quality, lane);
-        Q.nitem = Q.nslot = 0;
-        myslot = -1;
-        exact_block(W, ovf, b, CH, g, a.quality, lane);
+    /* some lane has a coefficient inside the guard band (about half the channel-tiles of
+     * random data at q90; wave-uniform branch): queue the exact recomputation */
+    if (!JX_DBG_NO_EXACT && seen != 0) {
+        const bool mine = active && ((seen >> lane) & 1u);
+        const bool multi = mine && (force || ((dup >> lane) & 1u));
+        admit_flags<CH>(W, Q, myslot, raw, b, mine && !multi, multi, idx, lane, P);
     }
 }
 
@@ -458,9 +511,8 @@ __device__ __forceinline__ unsigned tile_block(unsigned t, unsigned lane, unsign
  * Persistent: each wave walks tiles t, t + waves, ...  Input prefetch (JX_PREFETCH):
  *   0  load the tile's rows at its start (the wait also drains the previous tile's stores)
  *   1  load tile t+1 into a second register set at the start of tile t (+48 VGPRs)
- *   2  load tile t+1 into the same registers as soon as tile t's last row pass has consumed
- *      them; the last column pass and its stores then overlap the load latency, and the
- *      wait at the next tile start leaves the youngest stores in flight.
+ *   2  (timing builds without the exact path only) load tile t+1 into the same registers
+ *      once the last row pass has consumed them -- the exact path still needs them.
  */
 __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
 {
@@ -500,25 +552,29 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
         }
 #endif
         int myslot = -1;
+        Pending P{0u, 0, 0, 0};
         float T[8][8];
         xform_rows<0>(raw, T);
-        xform_cols<0>(T, a, W, Q, myslot, active, b, t, lane);
+        xform_cols<0>(T, raw, a, W, Q, myslot, P, active, b, t, lane);
         __builtin_amdgcn_sched_barrier(0);
         xform_rows<1>(raw, T);
-        xform_cols<1>(T, a, W, Q, myslot, active, b, t, lane);
+        xform_cols<1>(T, raw, a, W, Q, myslot, P, active, b, t, lane);
         __builtin_amdgcn_sched_barrier(0);
         xform_rows<2>(raw, T);
 #if JX_PREFETCH == 2
+        static_assert(JX_DBG_NO_EXACT, "late prefetch overwrites pixels the exact path needs");
         if (tn < ntiles) {                          /* raw is dead: refill it for tile tn */
             const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
             load_block(g, fn, bn - fn * nb, raw);
         }
 #endif
-        xform_cols<2>(T, a, W, Q, myslot, active, b, t, lane);
-        /* queue nearly full: drain now, while the slots' blocks are still cheap to keep */
-        if (Q.nslot > kSlots - 8 || Q.nitem > kItems - 16) {
-            flush_queue(W, Q.nitem, g, a.quality, lane);
-            Q.nitem = Q.nslot = 0;
+        xform_cols<2>(T, raw, a, W, Q, myslot, P, active, b, t, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!JX_DBG_NO_EXACT) {
+            /* exact work that did not fit during the tile, then drain a nearly full queue */
+            if (__ballot(P.bits != 0)) settle_pending(W, Q, myslot, raw, b, P, g, a.quality, lane);
+            if (Q.nslot > kSlots - 4 || Q.nitem > kItems - 16)
+                drain(W, Q, myslot, g, a.quality, lane);
         }
 #if JX_PREFETCH == 1
         if (tn < ntiles) {
@@ -589,7 +645,9 @@ int tables_for_current_device()
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return JPGX_ENODEV;
     std::call_once(g_tab_once[dev], [dev]() {
         std::vector<jx_qtab> host(JX_MAXQ + 1);
+        std::vector<jx_limtab> band(2 * (JX_MAXQ + 1));
         memset(host.data(), 0, host.size() * sizeof(jx_qtab));
+        memset(band.data(), 0, band.size() * sizeof(jx_limtab));
         for (int q = 1; q <= JX_MAXQ; q++) {
             float w[3][64], lim[3][64];
             jx_plan_tables(q, w, lim, host[q].q);
@@ -597,11 +655,15 @@ int tables_for_current_device()
                 for (int u = 0; u < 8; u++)
                     for (int v = 0; v < 8; v++) {
                         host[q].w[ch][u][v] = w[ch][v * 8 + u];
-                        host[q].lim[ch][u][v] = lim[ch][v * 8 + u];
+                        band[q].lim[ch][u][v] = lim[ch][v * 8 + u];
+                        band[JX_MAXQ + 1 + q].lim[ch][u][v] = -1.0f;   /* FORCE_EXACT */
                     }
         }
         g_tab_rc[dev] = hip_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_qtab), host.data(),
                                                  host.size() * sizeof(jx_qtab)));
+        if (!g_tab_rc[dev])
+            g_tab_rc[dev] = hip_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_lim), band.data(),
+                                                     band.size() * sizeof(jx_limtab)));
     });
     return g_tab_rc[dev];
 }

@@ -10,7 +10,7 @@ make -s -C "$PKG" >/dev/null
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   obj=$PKG/build/variants/$name.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -I"$ROOT/include" \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-slp-vectorize -I"$ROOT/include" \
       $flags -c "$PKG/csrc/jpgx_kernels.hip" -o "$obj"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libjpgx_$name.so" "$obj" \
       "$PKG/build/jpgx_plan.o" -lpthread
