@@ -64,8 +64,16 @@ namespace {
 #ifndef JX_WPE          /* minimum waves per SIMD the register allocation must allow    */
 #define JX_WPE 2
 #endif
-#ifndef JX_DBG_FLAGMODE  /* debug only: 0 full guard-band bookkeeping (the product)        */
+#ifndef JX_DBG_FLAGMODE  /* guard-band bookkeeping: 0 SALU masks in asm, 3 VALU count+select */
 #define JX_DBG_FLAGMODE 0
+#endif
+#ifndef JX_FLAG_ASM_VOLATILE
+#define JX_FLAG_ASM_VOLATILE 1
+#endif
+#if JX_FLAG_ASM_VOLATILE
+#define JX_FLAG_ASM_Q volatile
+#else
+#define JX_FLAG_ASM_Q
 #endif
 #ifndef JX_DBG_NO_EXACT  /* debug/measurement only: drop the exact path (NOT bit-exact)    */
 #define JX_DBG_NO_EXACT 0
@@ -428,6 +436,9 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
      * coefficient; wave masks of lanes with >= 1 and with >= 2 flags in this channel */
     int idx = 0;
     uint64_t seen = 0, dup = 0;
+#if JX_DBG_FLAGMODE == 3
+    int nfl = 0;
+#endif
 #pragma unroll
     for (int u = 0; u < 8; u++) {
         float col[8], F[8];
@@ -443,11 +454,16 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
             bits[zz_of(v, u)] = __float_as_uint(tm);              /* low 16 bits = int16 */
             if (!JX_DBG_NO_EXACT) {
                 const bool fl = __builtin_fabsf(d) >= band.lim[CH][u][v];
+#if JX_DBG_FLAGMODE == 3
+                /* per-lane count and index, all VALU (compare + 2 selects) */
+                nfl += fl ? 1 : 0;
+                idx = fl ? zz_of(v, u) : idx;
+#else
                 const uint64_t m = __ballot(fl);
-                /* pinned here (SALU): left to the compiler, the 64 masks of a channel are
-                 * kept alive until the end and spilled to VGPR lanes */
+                /* SALU mask bookkeeping kept next to its compare: left to the compiler, the
+                 * 64 masks of a channel are kept alive until the end and spilled */
                 uint64_t tmp;
-                asm volatile("s_and_b64 %[t], %[m], %[seen]\n\t"
+                asm JX_FLAG_ASM_Q("s_and_b64 %[t], %[m], %[seen]\n\t"
                              "s_or_b64 %[dup], %[dup], %[t]\n\t"
                              "s_or_b64 %[seen], %[seen], %[m]\n\t"
                              "v_cndmask_b32_e64 %[idx], %[idx], %[z], %[m]"
@@ -455,6 +471,7 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
                                [idx] "+v"(idx)
                              : [m] "s"(m), [z] "n"(zz_of(v, u))
                              : "scc");
+#endif
             }
         }
         /* pack zig-zag pairs completed by this column; stage the 16-B chunks it completes
@@ -493,6 +510,10 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
     }
     /* some lane has a coefficient inside the guard band (about half the channel-tiles of
      * random data at q90; wave-uniform branch): queue the exact recomputation */
+#if JX_DBG_FLAGMODE == 3
+    seen = __ballot(nfl > 0);
+    dup = __ballot(nfl > 1);
+#endif
     if (!JX_DBG_NO_EXACT && seen != 0) {
         const bool mine = active && ((seen >> lane) & 1u);
         const bool multi = mine && (force || ((dup >> lane) & 1u));
