@@ -67,6 +67,12 @@ namespace {
 #ifndef JX_DBG_FLAGMODE  /* guard-band bookkeeping: 0 SALU masks in asm, 3 VALU count+select */
 #define JX_DBG_FLAGMODE 0
 #endif
+#ifndef JX_DBG_UNIFORM_LIM
+#define JX_DBG_UNIFORM_LIM 0
+#endif
+#ifndef JX_DBG_NO_ADMIT
+#define JX_DBG_NO_ADMIT 0
+#endif
 #ifndef JX_FLAG_ASM_VOLATILE
 #define JX_FLAG_ASM_VOLATILE 1
 #endif
@@ -453,7 +459,11 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
             const float d = __builtin_fmaf(F[v], w, -rr);         /* F*w - rint(F*w)   */
             bits[zz_of(v, u)] = __float_as_uint(tm);              /* low 16 bits = int16 */
             if (!JX_DBG_NO_EXACT) {
+#if JX_DBG_UNIFORM_LIM   /* timing experiment only: one limit per channel (NOT the product) */
+                const bool fl = __builtin_fabsf(d) >= band.lim[CH][0][0];
+#else
                 const bool fl = __builtin_fabsf(d) >= band.lim[CH][u][v];
+#endif
 #if JX_DBG_FLAGMODE == 3
                 /* per-lane count and index, all VALU (compare + 2 selects) */
                 nfl += fl ? 1 : 0;
@@ -514,11 +524,15 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
     seen = __ballot(nfl > 0);
     dup = __ballot(nfl > 1);
 #endif
+#if JX_DBG_NO_ADMIT      /* timing experiment only: bookkeeping without acting on it */
+    if (seen != 0 && lane == 0) W.item[0] = (uint32_t)idx ^ (uint32_t)dup;
+#else
     if (!JX_DBG_NO_EXACT && seen != 0) {
         const bool mine = active && ((seen >> lane) & 1u);
         const bool multi = mine && (force || ((dup >> lane) & 1u));
         admit_flags<CH>(W, Q, myslot, raw, b, mine && !multi, multi, idx, lane, P);
     }
+#endif
 }
 
 /* block index of this lane in tile t (clamped into range for the tail tile) */
