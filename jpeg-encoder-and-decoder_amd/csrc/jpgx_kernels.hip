@@ -73,8 +73,8 @@ namespace {
 #ifndef JX_DBG_NO_ADMIT
 #define JX_DBG_NO_ADMIT 0
 #endif
-#ifndef JX_FLAG_ASM_VOLATILE
-#define JX_FLAG_ASM_VOLATILE 1
+#ifndef JX_FLAG_ASM_VOLATILE    /* 1: the flag bookkeeping asm also fences scheduling     */
+#define JX_FLAG_ASM_VOLATILE 0  /*    (measured 6% slower; kept as a knob)                */
 #endif
 #if JX_FLAG_ASM_VOLATILE
 #define JX_FLAG_ASM_Q volatile
@@ -92,10 +92,10 @@ namespace {
 
 constexpr float kMagic = 12582912.0f; /* 1.5 * 2^23: x + kMagic rounds x to an integer   */
 #ifndef JX_SLOTS_PER_WAVE
-#define JX_SLOTS_PER_WAVE 16
+#define JX_SLOTS_PER_WAVE 32
 #endif
 constexpr int kSlots = JX_SLOTS_PER_WAVE; /* per-wave deferred-exact queue: pixel slots    */
-constexpr int kItems = 64;                /*                             and coefficients  */
+constexpr int kItems = 128;               /*                             and coefficients  */
 static_assert(kSlots <= 32, "item encoding keeps 5 bits for the slot");
 
 /* zig_zag.c:6-15: scan position of natural (row v, column u) */
@@ -241,23 +241,34 @@ __device__ __forceinline__ double exact_pixel(int ch, int r, int g, int b)
 }
 
 /* One coefficient in the reference's exact operation order.  px = the block's 8 pixel rows
- * (24 interleaved bytes each) in LDS. */
-__device__ int16_t exact_coef(const uint8_t *px, int ch, int u, int v, int q)
+ * (24 interleaved bytes each, 48 dwords), already in registers. */
+template <int CH>
+__device__ __forceinline__ double exact_sum(const uint32_t (&px)[48], int u, int v)
 {
-    double cv[8];
+    double cu[8], cv[8];
 #pragma unroll
-    for (int y = 0; y < 8; y++) cv[y] = kCos[v][y];
+    for (int k = 0; k < 8; k++) {
+        cu[k] = kCos[u][k];
+        cv[k] = kCos[v][k];
+    }
     double s = 0.0;
-#pragma unroll 1
-    for (int x = 0; x < 8; x++) {            /* dct.c:46 x outer */
-        const double cux = kCos[u][x];
+#pragma unroll
+    for (int x = 0; x < 8; x++)              /* dct.c:46 x outer */
 #pragma unroll
         for (int y = 0; y < 8; y++) {        /* dct.c:47 y inner */
-            const uint8_t *p = px + y * 24 + 3 * x;
-            const double X = exact_pixel(ch, p[0], p[1], p[2]);
-            s += X * cux * cv[y];            /* (X * c_u[x]) * c_v[y], dct.c:48-50 */
+            const int o = y * 24 + 3 * x;
+            const int r = (int)((px[o >> 2] >> (8 * (o & 3))) & 0xffu);
+            const int g = (int)((px[(o + 1) >> 2] >> (8 * ((o + 1) & 3))) & 0xffu);
+            const int b = (int)((px[(o + 2) >> 2] >> (8 * ((o + 2) & 3))) & 0xffu);
+            s += exact_pixel(CH, r, g, b) * cu[x] * cv[y];   /* (X*c_u[x])*c_v[y], :48-50 */
         }
-    }
+    return s;
+}
+
+__device__ int16_t exact_coef(const uint32_t (&px)[48], int ch, int u, int v, int q)
+{
+    const double s = ch == 0 ? exact_sum<0>(px, u, v)
+                             : (ch == 1 ? exact_sum<1>(px, u, v) : exact_sum<2>(px, u, v));
     const double F = 0.25 * (u == 0 ? kAlpha0 : 1.0) * (v == 0 ? kAlpha0 : 1.0) * s;
     return (int16_t)(int)round(F / (double)q);      /* quantise.c:58 */
 }
@@ -279,8 +290,13 @@ JX_RARE void flush_queue(WaveLds &W, int nitem, const jx_geom &g, int quality,
         const int slot = (int)(it & 31u), ch = (int)((it >> 5) & 3u), zz = (int)(it >> 7);
         const int uv = kUnZZ[zz], u = uv & 7, v = uv >> 3;
         const int q = g_qtab[quality].q[ch == 0 ? 0 : 1][u * 8 + v];
-        *coef_ptr(g, W.slot_blk[slot], ch, zz) =
-            exact_coef((const uint8_t *)W.px[slot], ch, u, v, q);
+        uint32_t px[48];
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            const u32x4 d4 = W.px[slot][k];
+            px[4 * k] = d4.x; px[4 * k + 1] = d4.y; px[4 * k + 2] = d4.z; px[4 * k + 3] = d4.w;
+        }
+        *coef_ptr(g, W.slot_blk[slot], ch, zz) = exact_coef(px, ch, u, v, q);
     }
 }
 
