@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "jpgx_internal.h"
+#include "jx_consts.h"
 #include "xform_math.h"
 
 #pragma clang fp contract(off)
@@ -136,24 +137,8 @@ __constant__ uint8_t kUnZZ[64] = {
     35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
     58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
-/* cos(((2x+1)*u*M_PI)/16) exactly as glibc returns it for the reference (src/dct.c:49-50;
- * SURVEY.md Appendix B; tests/test_host.py re-derives it from the host libm). */
-__constant__ double kCos[8][8] = {
-    {0x1p+0, 0x1p+0, 0x1p+0, 0x1p+0, 0x1p+0, 0x1p+0, 0x1p+0, 0x1p+0},
-    {0x1.f6297cff75cbp-1, 0x1.a9b66290ea1a3p-1, 0x1.1c73b39ae68c9p-1, 0x1.8f8b83c69a60dp-3,
-     -0x1.8f8b83c69a608p-3, -0x1.1c73b39ae68c6p-1, -0x1.a9b66290ea1a4p-1, -0x1.f6297cff75cbp-1},
-    {0x1.d906bcf328d46p-1, 0x1.87de2a6aea964p-2, -0x1.87de2a6aea962p-2, -0x1.d906bcf328d46p-1,
-     -0x1.d906bcf328d47p-1, -0x1.87de2a6aea96dp-2, 0x1.87de2a6aea967p-2, 0x1.d906bcf328d44p-1},
-    {0x1.a9b66290ea1a3p-1, -0x1.8f8b83c69a608p-3, -0x1.f6297cff75cbp-1, -0x1.1c73b39ae68c8p-1,
-     0x1.1c73b39ae68c5p-1, 0x1.f6297cff75cbp-1, 0x1.8f8b83c69a61dp-3, -0x1.a9b66290ea1a2p-1},
-    {0x1.6a09e667f3bcdp-1, -0x1.6a09e667f3bccp-1, -0x1.6a09e667f3bcep-1, 0x1.6a09e667f3bcbp-1,
-     0x1.6a09e667f3bcep-1, -0x1.6a09e667f3bc5p-1, -0x1.6a09e667f3bc9p-1, 0x1.6a09e667f3bc4p-1},
-    {0x1.1c73b39ae68c9p-1, -0x1.f6297cff75cbp-1, 0x1.8f8b83c69a60cp-3, 0x1.a9b66290ea1a5p-1,
-     -0x1.a9b66290ea1a2p-1, -0x1.8f8b83c69a602p-3, 0x1.f6297cff75cb2p-1, -0x1.1c73b39ae68c2p-1},
-    {0x1.87de2a6aea964p-2, -0x1.d906bcf328d47p-1, 0x1.d906bcf328d44p-1, -0x1.87de2a6aea965p-2,
-     -0x1.87de2a6aea971p-2, 0x1.d906bcf328d46p-1, -0x1.d906bcf328d43p-1, 0x1.87de2a6aea95fp-2},
-    {0x1.8f8b83c69a60dp-3, -0x1.1c73b39ae68c8p-1, 0x1.a9b66290ea1a5p-1, -0x1.f6297cff75cb2p-1,
-     0x1.f6297cff75cbp-1, -0x1.a9b66290ea1a1p-1, 0x1.1c73b39ae68c2p-1, -0x1.8f8b83c69a616p-3}};
+/* cos(((2x+1)*u*M_PI)/16) exactly as glibc returns it for the reference (jx_consts.h) */
+__constant__ double kCos[8][8] = JX_COS_INIT;
 
 /* Per-quality tables (index 0 unused), constant address space so that wave-uniform reads
  * become scalar loads; filled once per device by tables_for_current_device(). */
@@ -161,7 +146,7 @@ __constant__ jx_qtab g_qtab[JX_MAXQ + 1];
 __constant__ jx_limtab g_lim[2][JX_MAXQ + 1];
 
 /* dct.c:13 ALPHA(0) = 1/sqrt(2) as the reference's double */
-constexpr double kAlpha0 = 0x1.6a09e667f3bccp-1;
+constexpr double kAlpha0 = JX_ALPHA0;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -552,7 +537,8 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
 }
 
 /* block index of this lane in tile t (clamped into range for the tail tile) */
-__device__ __forceinline__ unsigned tile_block(unsigned t, unsigned lane, unsigned total)
+[[maybe_unused]] __device__ __forceinline__ unsigned tile_block(unsigned t, unsigned lane,
+                                                                unsigned total)
 {
     const unsigned b = t * 64u + lane;
     return b < total ? b : total - 1;

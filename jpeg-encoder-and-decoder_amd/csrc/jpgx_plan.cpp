@@ -18,19 +18,12 @@
 #include <algorithm>
 
 #include "jpgx_internal.h"
+#include "jx_consts.h"
 #include "xform_math.h"
 
 /* pristine base tables, src/quantise.c:8-25 (row index = first subscript) */
-static const int kLum[8][8] = {
-    {16, 11, 10, 16, 24, 40, 51, 61},   {12, 12, 14, 19, 26, 58, 60, 55},
-    {14, 13, 16, 24, 40, 57, 69, 56},   {14, 17, 22, 29, 51, 87, 80, 62},
-    {18, 22, 37, 56, 68, 109, 103, 77}, {24, 35, 55, 64, 81, 104, 113, 92},
-    {49, 64, 78, 87, 103, 121, 120, 101}, {72, 92, 95, 98, 112, 100, 103, 99}};
-static const int kChr[8][8] = {
-    {17, 18, 24, 47, 99, 99, 99, 99}, {18, 21, 26, 66, 99, 99, 99, 99},
-    {24, 26, 56, 99, 99, 99, 99, 99}, {47, 66, 99, 99, 99, 99, 99, 99},
-    {99, 99, 99, 99, 99, 99, 99, 99}, {99, 99, 99, 99, 99, 99, 99, 99},
-    {99, 99, 99, 99, 99, 99, 99, 99}, {99, 99, 99, 99, 99, 99, 99, 99}};
+static const int kLum[8][8] = JX_Q_LUM_INIT;
+static const int kChr[8][8] = JX_Q_CHR_INIT;
 
 namespace {
 

@@ -30,13 +30,21 @@ OK, EGEOMETRY, EQUALITY, ESAMPLE, EARG, EHIP, EWORKSPACE, ENODEV = 0, -1, -2, -3
 _ERRNAMES = {-1: "EGEOMETRY", -2: "EQUALITY", -3: "ESAMPLE", -4: "EARG", -5: "EHIP",
              -6: "EWORKSPACE", -7: "ENODEV"}
 
-# every symbol include/jpgx.h declares (tests check the library exports them all)
+# every function include/jpgx.h and include/jpgx_compat.h declare (tests check the library
+# exports them all)
 EXPORTS = [
     "jpgx_validate", "jpgx_default_params", "jpgx_glibc_underflow", "jpgx_scale_table",
     "jpgx_guard_band", "jpgx_workspace_size", "jpgx_blocks_gpu", "jpgx_blocks_gpu_ev",
     "jpgx_gen_splitmix_gpu",
     "jpgx_gen_tie_gpu", "jpgx_blocks", "jpgx_blocks_multi", "jpgx_stripe",
     "jpgx_device_count", "jpgx_version",
+]
+COMPAT_EXPORTS = [
+    "jpgx_new_block", "jpgx_get_value_block", "jpgx_set_value_block", "jpgx_copy_block",
+    "jpgx_show_block", "jpgx_destroy_block", "jpgx_dct_block", "jpgx_quantise_block",
+    "jpgx_quantise_lum", "jpgx_quantise_chr", "jpgx_scale_table_inplace", "jpgx_zig_zag_block",
+    "jpgx_fill_jpgdata", "jpgx_free_jpgdata", "jpgx_dpcm", "jpgx_dpcm_dc", "jpgx_bmp_read",
+    "jpgx_free", "jpgx_encode_bmp",
 ]
 
 

@@ -1,0 +1,63 @@
+"""The N>1 path on CPU: two gloo ranks run bench.py's sharding (rank_plan: block-row stripes,
+halo row, per-rank splitmix seeds) and its max-over-ranks timing reduction; each rank computes
+its stripe with the oracle (the CPU checker -- the GPU kernel's stripe path is covered by
+test_gpu_parity), and the stitched stripes must equal the whole frame.  No data-path
+collective exists: all_gather here only brings the results to the checker."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+W, H, FRAMES = 96, 80, 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import jpgx
+    import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        plan = bench.rank_plan(W, H, FRAMES, world, rank, jpgx)
+        assert plan["B"] == FRAMES * world
+        outs = []
+        for f in range(plan["B"]):
+            # the rank's bytes, generated from its own seed, placed at their frame rows
+            stripe = O.gen_splitmix(plan["seeds"][f], W, plan["rows_px"])
+            frame = np.zeros((H, W, 3), np.uint8)
+            top = 8 * plan["r0"] - plan["halo"]
+            frame[top:top + plan["rows_px"]] = stripe
+            outs.append(O.blocks(frame, q, rows=(plan["r0"], plan["r1"])))
+        t = bench.max_over_ranks(float(rank + 1), world)
+        assert t == float(world)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (plan["r0"], plan["r1"], outs))
+        if rank == 0:
+            spans = sorted((g[0], g[1]) for g in gathered)
+            assert spans[0][0] == 0 and spans[-1][1] == H // 8
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))   # disjoint, complete
+            for f in range(FRAMES * world):
+                full = O.blocks(O.gen_splitmix(1000 + f, W, H), q)
+                stitched = np.concatenate([g[2][f] for g in sorted(gathered)], axis=1)
+                assert np.array_equal(stitched, full), f
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("q", [50, 90])
+def test_two_rank_stripes_stitch(q):
+    mp.spawn(_rank, args=(2, _free_port(), q), nprocs=2, join=True)

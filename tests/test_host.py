@@ -15,9 +15,13 @@ from test_oracle import CHR, LUM
 
 
 def test_exports_every_declared_symbol():
-    hdr = open(os.path.join(REPO, "include", "jpgx.h")).read()
-    declared = sorted(set(re.findall(r"\b(jpgx_[a-z_0-9]+)\s*\(", hdr)))
-    assert declared == sorted(jpgx.EXPORTS)
+    declared = []
+    for h, names in (("jpgx.h", jpgx.EXPORTS), ("jpgx_compat.h", jpgx.COMPAT_EXPORTS)):
+        hdr = open(os.path.join(REPO, "include", h)).read()
+        hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)          # declarations only
+        found = sorted(set(re.findall(r"\b(jpgx_[a-z_0-9]+)\s*\(", hdr)))
+        assert found == sorted(names), h
+        declared += found
     for name in declared:
         assert hasattr(jpgx.lib, name), name
 
@@ -86,8 +90,9 @@ def test_guard_band_sane():
 def test_kernel_cos_table_is_glibc():
     """The exact path's cosine doubles are those the reference's libm call returns:
     cos(((2x+1)*u*M_PI)/16) (src/dct.c:49-50)."""
-    src = open(os.path.join(PKG, "csrc", "jpgx_kernels.hip")).read()
-    body = src.split("kCos[8][8] = {")[1].split("}};")[0]
+    src = open(os.path.join(PKG, "csrc", "jx_consts.h")).read()
+    assert "kCos[8][8] = JX_COS_INIT" in open(os.path.join(PKG, "csrc", "jpgx_kernels.hip")).read()
+    body = src.split("#define JX_COS_INIT")[1].split("#define")[0]
     vals = [float.fromhex(t) for t in re.findall(r"-?0x[0-9a-f.]+p[+-]\d+", body)]
     assert len(vals) == 64
     for u in range(8):

@@ -16,6 +16,6 @@ timeout -k 10 400 python bench.py --steps $STEPS --warmup 5 > "$OUT/bench.json" 
 echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -5 "$OUT/bench.err"; [ $rc -eq 0 ] || exit $rc
 if [ "${PROF:-1}" = "1" ]; then
   cd /tmp
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps $STEPS --warmup 5 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"; rc=$?
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps $STEPS --warmup 5 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"; rc=$?
   echo "rocprof rc=$rc"; find "$OUT/prof" -name "*stats*" | head; [ $rc -eq 0 ] || exit $rc
 fi
