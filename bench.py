@@ -35,10 +35,9 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(width, height, quality, seconds, threads):
+def _port_rate(width, height, quality, seconds, threads):
     """The oracle (exact-order fp64 naive DCT with two cos() calls per term: the reference's
     own algorithmic cost, src/dct.c:43-56) on the first block-rows of one frame."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     frame = oracle.gen_splitmix(1, width, height)
     t = time.perf_counter()
@@ -48,11 +47,58 @@ def cpu_baseline(width, height, quality, seconds, threads):
     t = time.perf_counter()
     oracle.blocks(frame, quality, mode=oracle.MODE_REFCOST, nthreads=threads, rows=(0, rows))
     dt = time.perf_counter() - t
-    px = rows * 8 * width
-    return {"value": round(px / dt / 1e6, 4), "unit": "Mpixels/s", "cores": threads,
-            "kind": "port",
-            "sample": f"block-rows 0..{rows} of one {width}x{height} frame ({px} px), q={quality}, "
-                      f"oracle/cpu_ref.c exact-order fp64 with cos() per term, {dt:.1f} s"}
+    return rows * 8 * width / dt / 1e6, rows, dt
+
+
+def _reference_rate(width, quality, seconds, jpgx):
+    """The real reference (oracle/_ref/ref_dump: the reference's own preprocess -> zig_zag
+    stage sources compiled by oracle/Makefile, 1 thread) on a width x (8*rows) synthetic BMP,
+    wall time of the process; its output is compared with the GPU path's on the same image."""
+    import subprocess
+    import tempfile
+
+    import numpy as np
+    import oracle
+    exe = os.path.join(REPO, "oracle", "_ref", "ref_dump")
+
+    def run(rows, td):
+        img = oracle.gen_splitmix(1, width, 8 * rows)
+        bmp, out = os.path.join(td, "s.bmp"), os.path.join(td, "s.bin")
+        oracle.write_bmp(bmp, img)
+        t = time.perf_counter()
+        subprocess.run([exe, bmp, out, str(quality), "0"], check=True,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        dt = time.perf_counter() - t
+        ref = np.fromfile(out, np.int32).reshape(3, -1, 64)
+        return img, ref, dt
+
+    with tempfile.TemporaryDirectory() as td:
+        _, _, dt = run(2, td)
+        rows = max(2, int(seconds / max(dt / 2, 1e-4)))
+        img, ref, dt = run(rows, td)
+    gpu = jpgx.encode_blocks(img, quality)
+    return width * 8 * rows / dt / 1e6, rows, dt, bool(np.array_equal(gpu, ref))
+
+
+def cpu_baseline(width, height, quality, seconds, jpgx):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    allc = max(1, min(16, len(os.sched_getaffinity(0))))
+    p_all, rows_all, dt_all = _port_rate(width, height, quality, seconds / 3, allc)
+    extra = {"port_all_cores": {"value": round(p_all, 4), "cores": allc,
+                                "sample": f"block-rows 0..{rows_all} of a {width}x{height} "
+                                          f"frame, OpenMP over blocks, {dt_all:.1f} s"}}
+    if os.path.exists(os.path.join(REPO, "oracle", "_ref", "ref_dump")):
+        v, rows, dt, same = _reference_rate(width, quality, seconds, jpgx)
+        return {"value": round(v, 4), "unit": "Mpixels/s", "cores": 1, "kind": "reference",
+                "sample": f"{width}x{8 * rows} synthetic BMP (splitmix seed 1), q={quality}, the "
+                          f"reference's preprocess->zig_zag compiled -O2 (oracle/_ref), "
+                          f"process wall {dt:.1f} s",
+                "gpu_output_identical": same, **extra}
+    v, rows, dt = _port_rate(width, height, quality, seconds, 1)
+    return {"value": round(v, 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": f"block-rows 0..{rows} of one {width}x{height} frame ({rows * 8 * width} "
+                      f"px), q={quality}, oracle/cpu_ref.c exact-order fp64 with cos() per term, "
+                      f"{dt:.1f} s", **extra}
 
 
 def measured_traffic():
