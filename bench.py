@@ -230,7 +230,7 @@ def main():
         t_ratio, t_src = measured_traffic()
         cpu = None
         if N == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(W, H, q, args.cpu_seconds, 1)
+            cpu = cpu_baseline(W, H, q, args.cpu_seconds, jpgx)
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "Mpixels/s", "n_gpus": N,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
