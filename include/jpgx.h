@@ -102,7 +102,8 @@ int jpgx_guard_band(int quality, float scale[3][64], float lim[3][64]);
 
 /* ---- device path (pointers are device pointers; `stream` is a hipStream_t or NULL) ---- */
 
-/* Bytes of device workspace one jpgx_blocks_gpu call on `fr` needs (flag counts + slots). */
+/* Bytes of device workspace one jpgx_blocks_gpu call on `fr` needs.  Currently 0 for every
+ * geometry (the exact-path queue lives in LDS); kept so callers stay source-compatible. */
 size_t jpgx_workspace_size(const jpgx_frames *fr);
 
 /* The fused hot path: RGB -> quantised zig-zag int16 for every block of fr's stripe of every
@@ -113,8 +114,8 @@ size_t jpgx_workspace_size(const jpgx_frames *fr);
 int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
                     int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream);
 
-/* Same, and records hipEvent_t `event_between` (if non-NULL) on `stream` after the fast
- * transform kernel and before the exact-fixup kernel (for timing each one). */
+/* Same, and records hipEvent_t `event_between` (if non-NULL) on `stream` right after the
+ * transform kernel (for timing the kernel alone against an event recorded before the call). */
 int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
                        int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream,
                        void *event_between);

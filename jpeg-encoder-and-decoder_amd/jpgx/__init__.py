@@ -192,8 +192,8 @@ def blocks_gpu(fr: Frames, params: Params, d_rgb, d_out, d_ws, stream=None,
                event_between=None) -> None:
     """Launch the hot path on device tensors (uint8 input, int16 output, uint8 workspace).
     d_rgb must point at pixel (0, 8*row_begin) of frame 0 (pass a tensor view or an int).
-    event_between: a torch.cuda.Event recorded after the transform kernel, before the fixup
-    kernel (it must have been recorded once already so that its handle exists)."""
+    event_between: a torch.cuda.Event recorded right after the transform kernel (it must have
+    been recorded once already so that its handle exists)."""
     def ptr(t):
         return t if isinstance(t, int) else t.data_ptr()
     ws_bytes = d_ws.numel() if hasattr(d_ws, "numel") else workspace_size(fr)
