@@ -151,6 +151,22 @@ constexpr double kAlpha0 = JX_ALPHA0;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+#ifndef JX_NT_STORE     /* coefficient stores with the nontemporal bit (streamed, never re-read) */
+#define JX_NT_STORE 1
+#endif
+#ifndef JX_NT_LOAD      /* pixel loads with the nontemporal bit                                 */
+#define JX_NT_LOAD 0
+#endif
+
+__device__ __forceinline__ void jx_store(u32x4 *p, u32x4 v)
+{
+#if JX_NT_STORE
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 /* Per-wave LDS.  `stage` and `px` are adjacent: after a flush the pair is reused as 64 x
  * 192 B to stage every lane's block for a whole-block exact recompute (overflow path). */
 struct WaveLds {
@@ -186,8 +202,13 @@ __device__ __forceinline__ void load_block(const jx_geom &g, unsigned f, unsigne
         p = (const uint8_t *)__builtin_assume_aligned(p, 8);
         u32x4 a;
         u32x2 b;
+#if JX_NT_LOAD
+        a = __builtin_nontemporal_load((const u32x4 *)p);
+        b = __builtin_nontemporal_load((const u32x2 *)(p + 16));
+#else
         __builtin_memcpy(&a, p, 16);
         __builtin_memcpy(&b, p + 16, 8);
+#endif
         raw[y][0] = a.x; raw[y][1] = a.y; raw[y][2] = a.z; raw[y][3] = a.w;
         raw[y][4] = b.x; raw[y][5] = b.y;
     }
@@ -509,14 +530,15 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const unsigned e = (unsigned)j * 64u + lane;
-            dst[e] = W.stage[(e >> 3) * 9 + (e & 7)];
+            jx_store(dst + e, W.stage[(e >> 3) * 9 + (e & 7)]);
         }
     } else {                                   /* tile crosses a frame end or the last tile */
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const unsigned e = (unsigned)j * 64u + lane, bb = b0 + (e >> 3);
             if (bb < total)
-                *(u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8) = W.stage[(e >> 3) * 9 + (e & 7)];
+                jx_store((u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8),
+                         W.stage[(e >> 3) * 9 + (e & 7)]);
         }
     }
     /* some lane has a coefficient inside the guard band (about half the channel-tiles of
