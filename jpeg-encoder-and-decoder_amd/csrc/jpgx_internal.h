@@ -11,7 +11,6 @@
 
 #include "../../include/jpgx.h"
 
-#define JX_SLOTS 7          /* flagged-coefficient slots per block-channel before overflow */
 #define JX_WG 256           /* threads per workgroup for the transform (4 waves)           */
 
 struct jx_geom {
@@ -43,8 +42,19 @@ struct jx_limtab {
 
 #define JX_MAXQ 97
 
+/* Device workspace: per k_xform wave and channel, the blocks with a coefficient inside the
+ * guard band (no atomics: every wave owns a region), consumed by k_fix. */
+struct jx_fixlist {
+    unsigned *count;        /* [3][nwaves] items per wave and channel (all written)       */
+    uint32_t *items;        /* [3][nwaves][capw] launch-global block indices              */
+    unsigned nwaves;        /* k_xform waves of the launch                                */
+    unsigned capw;          /* items per wave and channel = 64 * tiles per wave           */
+};
+#define JX_WS_HEADER 256    /* bytes before the item lists in the workspace               */
+
 struct jx_xform_args {
     jx_geom g;
+    jx_fixlist fix;
     int quality;            /* index into the device table                                */
     int force_exact;        /* JPGX_FLAG_FORCE_EXACT: flag every coefficient              */
 };

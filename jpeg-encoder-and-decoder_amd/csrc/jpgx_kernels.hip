@@ -49,9 +49,6 @@ namespace {
 #ifndef JX_COL_SB       /* scheduling fence between the column DCTs of a channel       */
 #define JX_COL_SB 1
 #endif
-#ifndef JX_EXACT_INLINE /* inline the rare exact-path helpers (vs real calls)           */
-#define JX_EXACT_INLINE 1
-#endif
 #if JX_ROW_SB
 #define JX_SB_ROW() __builtin_amdgcn_sched_barrier(0)
 #else
@@ -65,39 +62,17 @@ namespace {
 #ifndef JX_WPE          /* minimum waves per SIMD the register allocation must allow    */
 #define JX_WPE 2
 #endif
-#ifndef JX_DBG_FLAGMODE  /* guard-band bookkeeping: 0 SALU masks in asm, 3 VALU count+select */
-#define JX_DBG_FLAGMODE 0
-#endif
-#ifndef JX_DBG_UNIFORM_LIM
-#define JX_DBG_UNIFORM_LIM 0
-#endif
-#ifndef JX_DBG_NO_ADMIT
-#define JX_DBG_NO_ADMIT 0
-#endif
-#ifndef JX_FLAG_ASM_VOLATILE    /* 1: the flag bookkeeping asm also fences scheduling     */
-#define JX_FLAG_ASM_VOLATILE 0  /*    (measured 6% slower; kept as a knob)                */
-#endif
-#if JX_FLAG_ASM_VOLATILE
-#define JX_FLAG_ASM_Q volatile
-#else
-#define JX_FLAG_ASM_Q
-#endif
 #ifndef JX_DBG_NO_EXACT  /* debug/measurement only: drop the exact path (NOT bit-exact)    */
 #define JX_DBG_NO_EXACT 0
 #endif
-#if JX_EXACT_INLINE
-#define JX_RARE __device__
-#else
-#define JX_RARE __device__ __noinline__
-#endif
 
 constexpr float kMagic = 12582912.0f; /* 1.5 * 2^23: x + kMagic rounds x to an integer   */
-#ifndef JX_SLOTS_PER_WAVE
-#define JX_SLOTS_PER_WAVE 32
+#ifndef JX_QUEUE_ITEMS
+#define JX_QUEUE_ITEMS 128
 #endif
-constexpr int kSlots = JX_SLOTS_PER_WAVE; /* per-wave deferred-exact queue: pixel slots    */
-constexpr int kItems = 128;               /*                             and coefficients  */
-static_assert(kSlots <= 32, "item encoding keeps 5 bits for the slot");
+/* per-wave, per-channel queue of blocks with a coefficient inside the guard band */
+constexpr int kItems = JX_QUEUE_ITEMS;
+static_assert(kItems >= 64, "a tile adds at most 64 items per channel");
 
 /* zig_zag.c:6-15: scan position of natural (row v, column u) */
 __host__ __device__ constexpr int zz_of(int v, int u)
@@ -130,12 +105,9 @@ __host__ __device__ constexpr int zz_chunk_done(int j)
     return m;
 }
 
-/* inverse scan: zig-zag index -> (v << 3) | u */
-__constant__ uint8_t kUnZZ[64] = {
-    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
-    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
-    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
-    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+/* scan position of natural (row v, column u) for a runtime index (jx_consts.h) */
+__constant__ int kScan[8][8] = JX_SCAN_ORDER_INIT;
+__device__ __forceinline__ int zz_of_rt(int v, int u) { return kScan[v][u]; }
 
 /* cos(((2x+1)*u*M_PI)/16) exactly as glibc returns it for the reference (jx_consts.h) */
 __constant__ double kCos[8][8] = JX_COS_INIT;
@@ -167,15 +139,11 @@ __device__ __forceinline__ void jx_store(u32x4 *p, u32x4 v)
 #endif
 }
 
-/* Per-wave LDS.  `stage` and `px` are adjacent: after a flush the pair is reused as 64 x
- * 192 B to stage every lane's block for a whole-block exact recompute (overflow path). */
+/* Per-wave LDS */
 struct WaveLds {
     u32x4 stage[64 * 9];          /* one channel: block k's 8 chunks at units 9k..9k+7     */
-    u32x4 px[kSlots][12];         /* pixel rows (8 x 24 B) of blocks with queued items     */
-    uint32_t slot_blk[kSlots];    /* launch-global block index of each slot                */
-    uint32_t item[kItems];        /* slot | ch << 5 | zigzag << 7                          */
+    uint32_t item[3][kItems];     /* per channel: queued launch-global block indices       */
 };
-static_assert(sizeof(u32x4) * (64 * 9 + kSlots * 12) >= 64 * 192, "overflow staging");
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&row)[6], int k)
 {
@@ -218,16 +186,6 @@ __device__ __forceinline__ void load_block(const jx_geom &g, unsigned f, unsigne
     }
 }
 
-__device__ __forceinline__ void raw_to_lds(const uint32_t (&raw)[8][6], u32x4 *dst)
-{
-#pragma unroll
-    for (int k = 0; k < 12; k++) {
-        const int d = 4 * k;
-        dst[k] = u32x4{raw[d / 6][d % 6], raw[(d + 1) / 6][(d + 1) % 6],
-                       raw[(d + 2) / 6][(d + 2) % 6], raw[(d + 3) / 6][(d + 3) % 6]};
-    }
-}
-
 /* ---- exact path -------------------------------------------------------------------------- */
 
 /* Exact reference value of one channel pixel, level shift included (preprocess.c:160-162,
@@ -246,10 +204,10 @@ __device__ __forceinline__ double exact_pixel(int ch, int r, int g, int b)
     return cr - 128;
 }
 
-/* One coefficient in the reference's exact operation order.  px = the block's 8 pixel rows
- * (24 interleaved bytes each, 48 dwords), already in registers. */
+/* One coefficient in the reference's exact operation order.  raw = the block's 8 pixel rows
+ * (24 interleaved bytes each) in registers. */
 template <int CH>
-__device__ __forceinline__ double exact_sum(const uint32_t (&px)[48], int u, int v)
+__device__ __forceinline__ double exact_sum(const uint32_t (&raw)[8][6], int u, int v)
 {
     double cu[8], cv[8];
 #pragma unroll
@@ -262,19 +220,18 @@ __device__ __forceinline__ double exact_sum(const uint32_t (&px)[48], int u, int
     for (int x = 0; x < 8; x++)              /* dct.c:46 x outer */
 #pragma unroll
         for (int y = 0; y < 8; y++) {        /* dct.c:47 y inner */
-            const int o = y * 24 + 3 * x;
-            const int r = (int)((px[o >> 2] >> (8 * (o & 3))) & 0xffu);
-            const int g = (int)((px[(o + 1) >> 2] >> (8 * ((o + 1) & 3))) & 0xffu);
-            const int b = (int)((px[(o + 2) >> 2] >> (8 * ((o + 2) & 3))) & 0xffu);
+            const int r = (int)byte_of(raw[y], 3 * x);
+            const int g = (int)byte_of(raw[y], 3 * x + 1);
+            const int b = (int)byte_of(raw[y], 3 * x + 2);
             s += exact_pixel(CH, r, g, b) * cu[x] * cv[y];   /* (X*c_u[x])*c_v[y], :48-50 */
         }
     return s;
 }
 
-__device__ int16_t exact_coef(const uint32_t (&px)[48], int ch, int u, int v, int q)
+template <int CH>
+__device__ __forceinline__ int16_t exact_coef(const uint32_t (&raw)[8][6], int u, int v, int q)
 {
-    const double s = ch == 0 ? exact_sum<0>(px, u, v)
-                             : (ch == 1 ? exact_sum<1>(px, u, v) : exact_sum<2>(px, u, v));
+    const double s = exact_sum<CH>(raw, u, v);
     const double F = 0.25 * (u == 0 ? kAlpha0 : 1.0) * (v == 0 ? kAlpha0 : 1.0) * s;
     return (int16_t)(int)round(F / (double)q);      /* quantise.c:58 */
 }
@@ -285,139 +242,11 @@ __device__ __forceinline__ int16_t *coef_ptr(const jx_geom &g, unsigned b, int c
     return g.out + (long long)f * g.out_fstride + ((long long)ch * nb + bi) * 64 + zz;
 }
 
-/* Process every queued coefficient of the wave, lanes in parallel.  Wave-uniform call. */
-JX_RARE void flush_queue(WaveLds &W, int nitem, const jx_geom &g, int quality,
-                                         unsigned lane)
-{
-    /* the fast-path values these overwrite were stored earlier by this wave */
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int i = (int)lane; i < nitem; i += 64) {
-        const uint32_t it = W.item[i];
-        const int slot = (int)(it & 31u), ch = (int)((it >> 5) & 3u), zz = (int)(it >> 7);
-        const int uv = kUnZZ[zz], u = uv & 7, v = uv >> 3;
-        const int q = g_qtab[quality].q[ch == 0 ? 0 : 1][u * 8 + v];
-        uint32_t px[48];
-#pragma unroll
-        for (int k = 0; k < 12; k++) {
-            const u32x4 d4 = W.px[slot][k];
-            px[4 * k] = d4.x; px[4 * k + 1] = d4.y; px[4 * k + 2] = d4.z; px[4 * k + 3] = d4.w;
-        }
-        *coef_ptr(g, W.slot_blk[slot], ch, zz) = exact_coef(px, ch, u, v, q);
-    }
-}
-
-/* wave-uniform deferred-exact queue state */
-struct Queue {
-    int nslot, nitem;
-};
-
 /* number of set bits of m below this lane */
 __device__ __forceinline__ int lane_rank(uint64_t m)
 {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-__device__ __forceinline__ void drain(WaveLds &W, Queue &Q, int &myslot, const jx_geom &g,
-                                      int quality, unsigned lane)
-{
-    if (Q.nitem) flush_queue(W, Q.nitem, g, quality, lane);
-    Q.nitem = Q.nslot = 0;
-    myslot = -1;
-}
-
-/* Per lane: block-channels whose exact work did not fit the queue during the tile. */
-struct Pending {
-    unsigned bits;          /* bit ch: channel ch of this lane's block is pending          */
-    int idx0, idx1, idx2;   /* per channel: the single flagged zig-zag index, or -1 = all 64 */
-};
-
-/*
- * Admit `single` lanes (one flagged coefficient, zig-zag `idx`) of channel CH into the
- * queue without draining it (the channel passes run at full register pressure): lanes that
- * do not fit, and block-channels with several flags (`multi`, all 64 coefficients), are
- * left pending for settle_pending() at the end of the tile.  Wave-uniform call.
- */
-template <int CH>
-__device__ __forceinline__ void admit_flags(WaveLds &W, Queue &Q, int &myslot,
-                                            const uint32_t (&raw)[8][6], unsigned b, bool single,
-                                            bool multi, int idx, unsigned lane, Pending &P)
-{
-    const uint64_t S = __ballot(single);
-    const uint64_t needs = S & __ballot(myslot < 0);
-    const bool admit = single && lane_rank(S) < kItems - Q.nitem &&
-                       (myslot >= 0 || lane_rank(needs) < kSlots - Q.nslot);
-    const uint64_t A = __ballot(admit);
-    const uint64_t fresh = A & needs;
-    if (admit && myslot < 0) {
-        myslot = Q.nslot + lane_rank(fresh);
-        raw_to_lds(raw, W.px[myslot]);
-        W.slot_blk[myslot] = b;
-    }
-    if (admit)
-        W.item[Q.nitem + lane_rank(A)] = (uint32_t)myslot | (uint32_t)CH << 5 | (uint32_t)idx << 7;
-    Q.nslot += __popcll(fresh);
-    Q.nitem += __popcll(A);
-    if ((single && !admit) || multi) {
-        P.bits |= 1u << CH;
-        const int id = multi ? -1 : idx;
-        if (CH == 0) P.idx0 = id;
-        if (CH == 1) P.idx1 = id;
-        if (CH == 2) P.idx2 = id;
-    }
-}
-
-/*
- * End of tile: queue every pending block-channel, draining the queue (lane-parallel exact
- * pass) as often as needed.  Pixel rows come from `raw`, still this tile's.  Wave-uniform.
- */
-__device__ void settle_pending(WaveLds &W, Queue &Q, int &myslot, const uint32_t (&raw)[8][6],
-                               unsigned b, Pending &P, const jx_geom &g, int quality,
-                               unsigned lane)
-{
-#pragma unroll 1
-    for (int ch = 0; ch < 3; ch++) {
-        const bool pend = (P.bits >> ch) & 1u;
-        const int id = ch == 0 ? P.idx0 : (ch == 1 ? P.idx1 : P.idx2);
-        uint64_t S = __ballot(pend && id >= 0);
-        while (S) {                               /* singles, as many as fit per drain */
-            const uint64_t needs = S & __ballot(myslot < 0);
-            const bool admit = ((S >> lane) & 1u) && lane_rank(S) < kItems - Q.nitem &&
-                               (myslot >= 0 || lane_rank(needs) < kSlots - Q.nslot);
-            const uint64_t A = __ballot(admit);
-            if (!A) {
-                drain(W, Q, myslot, g, quality, lane);
-                continue;
-            }
-            const uint64_t fresh = A & needs;
-            if (admit && myslot < 0) {
-                myslot = Q.nslot + lane_rank(fresh);
-                raw_to_lds(raw, W.px[myslot]);
-                W.slot_blk[myslot] = b;
-            }
-            if (admit)
-                W.item[Q.nitem + lane_rank(A)] =
-                    (uint32_t)myslot | (uint32_t)ch << 5 | (uint32_t)id << 7;
-            Q.nslot += __popcll(fresh);
-            Q.nitem += __popcll(A);
-            S &= ~A;
-        }
-        uint64_t M = __ballot(pend && id < 0);
-        while (M) {                               /* whole block-channels: 64 items each */
-            const unsigned L = (unsigned)__builtin_ctzll(M);
-            M &= M - 1;
-            drain(W, Q, myslot, g, quality, lane);
-            if (lane == L) {
-                raw_to_lds(raw, W.px[0]);
-                W.slot_blk[0] = b;
-            }
-            W.item[lane] = 0u | (uint32_t)ch << 5 | lane << 7;   /* zig-zag index = lane */
-            Q.nslot = 1;
-            Q.nitem = 64;
-            drain(W, Q, myslot, g, quality, lane);
-        }
-    }
-    P.bits = 0;
 }
 
 /* ---- fast path --------------------------------------------------------------------------- */
@@ -447,26 +276,35 @@ __device__ __forceinline__ void xform_rows(uint32_t (&raw)[8][6], float (&T)[8][
     }
 }
 
-/* Column pass, quantisation, zig-zag, LDS staging + coalesced store of channel CH. */
+/* Quantise one coefficient in fp32: tm = rint(F*w) + 1.5*2^23 (its low 16 bits are the int16)
+ * and d = F*w - rint(F*w), exact (the guard band tests |d|). */
+__device__ __forceinline__ void quant_coef(float F, float w, float &tm, float &d)
+{
+    tm = __builtin_fmaf(F, w, kMagic);
+    const float rr = tm - kMagic;                /* exact */
+    d = __builtin_fmaf(F, w, -rr);
+}
+
+/* per-wave queue state (wave-uniform) */
+struct Queue {
+    int n[3];               /* items in the LDS queue                                     */
+    unsigned done[3];       /* items already moved to the wave's global region            */
+};
+
+/* Column pass, quantisation, zig-zag, LDS staging + coalesced store of channel CH; block-
+ * channels with a coefficient inside the guard band are queued for the exact path. */
 template <int CH>
-__device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&raw)[8][6],
-                                           const jx_xform_args &a, WaveLds &W, Queue &Q,
-                                           int &myslot, Pending &P, bool active, unsigned b,
-                                           unsigned t, unsigned lane)
+__device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args &a, WaveLds &W,
+                                           Queue &Q, bool active, unsigned b, unsigned t,
+                                           unsigned lane)
 {
     const jx_geom &g = a.g;
     uint32_t bits[64];     /* tm bit patterns by zig-zag index; low 16 bits = the int16    */
     uint32_t packed[32];   /* zig-zag pairs (2k, 2k+1) as one dword, formed when complete */
     const jx_qtab &tab = g_qtab[a.quality];
     const jx_limtab &band = g_lim[a.force_exact ? 1 : 0][a.quality];
-    const bool force = a.force_exact != 0;
-    /* guard-band bookkeeping, branch-free: per lane the zig-zag index of its (last) flagged
-     * coefficient; wave masks of lanes with >= 1 and with >= 2 flags in this channel */
-    int idx = 0;
-    uint64_t seen = 0, dup = 0;
-#if JX_DBG_FLAGMODE == 3
-    int nfl = 0;
-#endif
+    /* wave mask of lanes with a coefficient of this channel inside the guard band */
+    uint64_t seen = 0;
 #pragma unroll
     for (int u = 0; u < 8; u++) {
         float col[8], F[8];
@@ -475,35 +313,18 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
         jx_fdct8<FOps>(col, F);
 #pragma unroll
         for (int v = 0; v < 8; v++) {
-            const float w = tab.w[CH][u][v];
-            const float tm = __builtin_fmaf(F[v], w, kMagic);   /* rint(F*w) + magic  */
-            const float rr = tm - kMagic;                         /* exact             */
-            const float d = __builtin_fmaf(F[v], w, -rr);         /* F*w - rint(F*w)   */
-            bits[zz_of(v, u)] = __float_as_uint(tm);              /* low 16 bits = int16 */
+            float tm, d;
+            quant_coef(F[v], tab.w[CH][u][v], tm, d);
+            bits[zz_of(v, u)] = __float_as_uint(tm);
             if (!JX_DBG_NO_EXACT) {
-#if JX_DBG_UNIFORM_LIM   /* timing experiment only: one limit per channel (NOT the product) */
-                const bool fl = __builtin_fabsf(d) >= band.lim[CH][0][0];
-#else
-                const bool fl = __builtin_fabsf(d) >= band.lim[CH][u][v];
-#endif
-#if JX_DBG_FLAGMODE == 3
-                /* per-lane count and index, all VALU (compare + 2 selects) */
-                nfl += fl ? 1 : 0;
-                idx = fl ? zz_of(v, u) : idx;
-#else
-                const uint64_t m = __ballot(fl);
-                /* SALU mask bookkeeping kept next to its compare: left to the compiler, the
-                 * 64 masks of a channel are kept alive until the end and spilled */
-                uint64_t tmp;
-                asm JX_FLAG_ASM_Q("s_and_b64 %[t], %[m], %[seen]\n\t"
-                             "s_or_b64 %[dup], %[dup], %[t]\n\t"
-                             "s_or_b64 %[seen], %[seen], %[m]\n\t"
-                             "v_cndmask_b32_e64 %[idx], %[idx], %[z], %[m]"
-                             : [dup] "+s"(dup), [seen] "+s"(seen), [t] "=&s"(tmp),
-                               [idx] "+v"(idx)
-                             : [m] "s"(m), [z] "n"(zz_of(v, u))
-                             : "scc");
-#endif
+                /* compare straight into a lane mask, OR-ed at once (left to the compiler,
+                 * the 64 masks of a channel are kept alive until the end and spilled) */
+                uint64_t m;
+                asm("v_cmp_ge_f32_e64 %[m], |%[d]|, %[l]\n\t"
+                    "s_or_b64 %[seen], %[seen], %[m]"
+                    : [m] "=&s"(m), [seen] "+s"(seen)
+                    : [d] "v"(d), [l] "s"(band.lim[CH][u][v])
+                    : "scc");
             }
         }
         /* pack zig-zag pairs completed by this column; stage the 16-B chunks it completes
@@ -541,21 +362,56 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
                          W.stage[(e >> 3) * 9 + (e & 7)]);
         }
     }
-    /* some lane has a coefficient inside the guard band (about half the channel-tiles of
-     * random data at q90; wave-uniform branch): queue the exact recomputation */
-#if JX_DBG_FLAGMODE == 3
-    seen = __ballot(nfl > 0);
-    dup = __ballot(nfl > 1);
-#endif
-#if JX_DBG_NO_ADMIT      /* timing experiment only: bookkeeping without acting on it */
-    if (seen != 0 && lane == 0) W.item[0] = (uint32_t)idx ^ (uint32_t)dup;
-#else
+    /* some lane has a coefficient inside the guard band (about 40% of the channel-tiles of
+     * random data at q90; wave-uniform branch): queue its block-channel */
     if (!JX_DBG_NO_EXACT && seen != 0) {
-        const bool mine = active && ((seen >> lane) & 1u);
-        const bool multi = mine && (force || ((dup >> lane) & 1u));
-        admit_flags<CH>(W, Q, myslot, raw, b, mine && !multi, multi, idx, lane, P);
+        const uint64_t M = seen & __ballot(active);
+        if ((M >> lane) & 1u) W.item[CH][Q.n[CH] + lane_rank(M)] = b;
+        Q.n[CH] += __popcll(M);
     }
-#endif
+}
+
+/* ---- exact path -------------------------------------------------------------------------- */
+
+/*
+ * Guard-band test of one block-channel (raw = its pixel rows, reloaded): the fp32 transform
+ * is recomputed by the same code, so exactly the coefficients the fast pass found inside the
+ * guard band are found again.  Bit v*8+u of the result = coefficient (u, v) is flagged.
+ */
+template <int CH>
+__device__ __forceinline__ uint64_t flagged_coefs(uint32_t (&raw)[8][6], int quality, int force)
+{
+    const jx_qtab &tab = g_qtab[quality];
+    const jx_limtab &band = g_lim[force][quality];
+    float T[8][8];
+    xform_rows<CH>(raw, T);
+    uint64_t flagged = 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        float col[8], F[8];
+#pragma unroll
+        for (int y = 0; y < 8; y++) col[y] = T[y][u];
+        jx_fdct8<FOps>(col, F);
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            float tm, d;
+            quant_coef(F[v], tab.w[CH][u][v], tm, d);
+            if (__builtin_fabsf(d) >= band.lim[CH][u][v]) flagged |= 1ull << (v * 8 + u);
+        }
+    }
+    return flagged;
+}
+
+/* Move the wave's queued blocks of channel ch to its region of the launch's lists and empty
+ * the queue.  Wave-uniform; `wave` = the k_xform wave index, `done` = items already moved. */
+__device__ __forceinline__ void flush_queue(WaveLds &W, Queue &Q, int ch, const jx_fixlist &fx,
+                                            unsigned wave, unsigned lane)
+{
+    const int n = Q.n[ch];
+    uint32_t *dst = fx.items + ((size_t)ch * fx.nwaves + wave) * fx.capw + Q.done[ch];
+    for (int i = (int)lane; i < n; i += 64) dst[i] = W.item[ch][i];
+    Q.done[ch] += n;
+    Q.n[ch] = 0;
 }
 
 /* block index of this lane in tile t (clamped into range for the tail tile) */
@@ -570,8 +426,8 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const uint32_t (&ra
  * Persistent: each wave walks tiles t, t + waves, ...  Input prefetch (JX_PREFETCH):
  *   0  load the tile's rows at its start (the wait also drains the previous tile's stores)
  *   1  load tile t+1 into a second register set at the start of tile t (+48 VGPRs)
- *   2  (timing builds without the exact path only) load tile t+1 into the same registers
- *      once the last row pass has consumed them -- the exact path still needs them.
+ *   2  load tile t+1 into the same registers once the last row pass has consumed them (the
+ *      exact path reloads its pixels)
  */
 __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
 {
@@ -583,9 +439,13 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
     const unsigned lane = threadIdx.x & 63u;
     const unsigned nwaves = gridDim.x * (JX_WG / 64);
     unsigned t = blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6);
-    if (t >= ntiles) return;                       /* whole wave */
+    const unsigned wave = t;
+    if (t >= ntiles) {                             /* whole wave: nothing to queue */
+        if (!JX_DBG_NO_EXACT && lane < 3) a.fix.count[lane * a.fix.nwaves + wave] = 0;
+        return;
+    }
     WaveLds &W = s_wave[threadIdx.x >> 6];
-    Queue Q{0, 0};
+    Queue Q{{0, 0, 0}, {0u, 0u, 0u}};
     uint32_t raw[8][6];
 #if JX_PREFETCH
     {
@@ -610,30 +470,27 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
             load_block(g, f, b - f * nb, raw);
         }
 #endif
-        int myslot = -1;
-        Pending P{0u, 0, 0, 0};
         float T[8][8];
         xform_rows<0>(raw, T);
-        xform_cols<0>(T, raw, a, W, Q, myslot, P, active, b, t, lane);
+        xform_cols<0>(T, a, W, Q, active, b, t, lane);
         __builtin_amdgcn_sched_barrier(0);
         xform_rows<1>(raw, T);
-        xform_cols<1>(T, raw, a, W, Q, myslot, P, active, b, t, lane);
+        xform_cols<1>(T, a, W, Q, active, b, t, lane);
         __builtin_amdgcn_sched_barrier(0);
         xform_rows<2>(raw, T);
 #if JX_PREFETCH == 2
-        static_assert(JX_DBG_NO_EXACT, "late prefetch overwrites pixels the exact path needs");
         if (tn < ntiles) {                          /* raw is dead: refill it for tile tn */
             const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
             load_block(g, fn, bn - fn * nb, raw);
         }
 #endif
-        xform_cols<2>(T, raw, a, W, Q, myslot, P, active, b, t, lane);
+        xform_cols<2>(T, a, W, Q, active, b, t, lane);
         __builtin_amdgcn_sched_barrier(0);
+        /* keep room for the next tile's 64 possible items per channel */
         if (!JX_DBG_NO_EXACT) {
-            /* exact work that did not fit during the tile, then drain a nearly full queue */
-            if (__ballot(P.bits != 0)) settle_pending(W, Q, myslot, raw, b, P, g, a.quality, lane);
-            if (Q.nslot > kSlots - 4 || Q.nitem > kItems - 16)
-                drain(W, Q, myslot, g, a.quality, lane);
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++)
+                if (Q.n[ch] > kItems - 64) flush_queue(W, Q, ch, a.fix, wave, lane);
         }
 #if JX_PREFETCH == 1
         if (tn < ntiles) {
@@ -646,7 +503,137 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
         (void)tn;
 #endif
     }
-    if (Q.nitem) flush_queue(W, Q.nitem, g, a.quality, lane);
+    if (!JX_DBG_NO_EXACT) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) flush_queue(W, Q, ch, a.fix, wave, lane);
+        if (lane < 3) a.fix.count[lane * a.fix.nwaves + wave] = Q.done[lane];
+    }
+}
+
+/*
+ * The exact pass over the blocks k_xform queued.  Wave (ch, group) takes the lists of channel
+ * ch of k_xform waves [kFixGroup*group, +kFixGroup) (waves never mix channels), 64 blocks at
+ * a time: (A) one lane per block reloads its pixels, re-finds its flagged coefficients and
+ * parks the pixels in LDS; (B) one lane per flagged coefficient recomputes it exactly.
+ */
+#ifndef JX_FIX_GROUP
+#define JX_FIX_GROUP 8
+#endif
+constexpr unsigned kFixGroup = JX_FIX_GROUP;
+constexpr int kFixTasks = 64 * 64;             /* FORCE_EXACT: every coefficient of 64 blocks */
+
+struct FixLds {
+    u32x4 px[64][12];                          /* pixel rows of the chunk's blocks           */
+    uint32_t blk[64];                          /* their launch-global block indices          */
+    uint16_t task[kFixTasks];                  /* lane << 6 | natural coefficient index      */
+};
+
+template <int CH>
+__device__ __forceinline__ void fix_chunk(FixLds &L, const jx_xform_args &a, unsigned b,
+                                          bool has, unsigned lane)
+{
+    const jx_geom &g = a.g;
+    const unsigned nb = (unsigned)g.nb;
+    const int force = a.force_exact ? 1 : 0;
+    uint64_t flagged = 0;
+    if (has) {                                             /* (A) */
+        const unsigned f = b / nb;
+        uint32_t raw[8][6];
+        load_block(g, f, b - f * nb, raw);
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            const int d = 4 * k;
+            L.px[lane][k] = u32x4{raw[d / 6][d % 6], raw[(d + 1) / 6][(d + 1) % 6],
+                                  raw[(d + 2) / 6][(d + 2) % 6], raw[(d + 3) / 6][(d + 3) % 6]};
+        }
+        L.blk[lane] = b;
+#ifdef JX_DBG_FIX_NO_DETECT             /* timing experiments only (NOT exact) */
+        flagged = 1ull << (raw[0][0] & 63u);
+#else
+        flagged = flagged_coefs<CH>(raw, a.quality, force);
+#endif
+    }
+    /* exclusive prefix of the per-lane task counts */
+    const unsigned n = (unsigned)__popcll(flagged);
+    unsigned incl = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned o = __shfl_up(incl, d, 64);
+        if ((int)lane >= d) incl += o;
+    }
+    const unsigned total = __builtin_amdgcn_readlane(incl, 63);
+    unsigned pos = incl - n;
+    while (flagged) {
+        const unsigned k = (unsigned)__builtin_ctzll(flagged);
+        flagged &= flagged - 1;
+        L.task[pos++] = (uint16_t)(lane << 6 | k);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const jx_qtab &tab = g_qtab[a.quality];
+    for (unsigned t = lane; t < total; t += 64) {         /* (B) */
+        const unsigned tk = L.task[t], src = tk >> 6, k = tk & 63u;
+        const int u = (int)(k & 7u), v = (int)(k >> 3);
+        uint32_t raw[8][6];
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+            const u32x4 q4 = L.px[src][j];
+            const int d = 4 * j;
+            raw[d / 6][d % 6] = q4.x;
+            raw[(d + 1) / 6][(d + 1) % 6] = q4.y;
+            raw[(d + 2) / 6][(d + 2) % 6] = q4.z;
+            raw[(d + 3) / 6][(d + 3) % 6] = q4.w;
+        }
+#ifdef JX_DBG_FIX_NO_EXACT             /* timing experiments only (NOT exact) */
+        *coef_ptr(g, L.blk[src], CH, zz_of_rt(v, u)) = (int16_t)raw[0][0];
+#else
+        *coef_ptr(g, L.blk[src], CH, zz_of_rt(v, u)) =
+            exact_coef<CH>(raw, u, v, tab.q[CH == 0 ? 0 : 1][u * 8 + v]);
+#endif
+    }
+    __builtin_amdgcn_wave_barrier();                       /* LDS reused by the next chunk */
+}
+
+__global__ __launch_bounds__(256) void k_fix(const jx_xform_args a)
+{
+    __shared__ FixLds s_fix[4];
+    const jx_fixlist &fx = a.fix;
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned groups = (fx.nwaves + kFixGroup - 1) / kFixGroup;
+    const unsigned job = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (job >= 3 * groups) return;
+    FixLds &L = s_fix[threadIdx.x >> 6];
+    const int ch = (int)(job / groups);
+    const unsigned w0 = (job - ch * groups) * kFixGroup;
+    /* counts of the group's waves -> inclusive prefix sums, broadcast to scalars */
+    unsigned cnt = 0;
+    if (lane < kFixGroup && w0 + lane < fx.nwaves) cnt = fx.count[ch * fx.nwaves + w0 + lane];
+    unsigned incl[kFixGroup];
+    unsigned run = 0;
+#pragma unroll
+    for (unsigned s = 0; s < kFixGroup; s++) {
+        run += __builtin_amdgcn_readlane(cnt, s);
+        incl[s] = run;
+    }
+    for (unsigned c0 = 0; c0 < run; c0 += 64) {
+        const unsigned i = c0 + lane;
+        const bool has = i < run;
+        unsigned b = 0;
+        if (has) {
+            unsigned s = 0, excl = 0;
+#pragma unroll
+            for (unsigned k = 0; k < kFixGroup; k++)
+                if (incl[k] <= i) {
+                    s = k + 1;
+                    excl = incl[k];
+                }
+            b = fx.items[((size_t)ch * fx.nwaves + w0 + s) * fx.capw + (i - excl)];
+        }
+        if (ch == 0) fix_chunk<0>(L, a, b, has, lane);
+        else if (ch == 1) fix_chunk<1>(L, a, b, has, lane);
+        else fix_chunk<2>(L, a, b, has, lane);
+    }
 }
 
 __device__ __forceinline__ uint8_t splitmix_byte(uint64_t seed, uint64_t k)
@@ -753,8 +740,13 @@ extern "C" {
 
 size_t jpgx_workspace_size(const jpgx_frames *fr)
 {
-    (void)fr;
-    return 0;   /* the exact-fixup queue lives in LDS; no device workspace is needed */
+    if (!fr || fr->row_end <= fr->row_begin || fr->nframes < 1 || fr->width < 8) return 0;
+    const size_t total = (size_t)(fr->row_end - fr->row_begin) * (fr->width / 8) * fr->nframes;
+    const size_t ntiles = (total + 63) / 64;
+    /* per k_xform wave (at most tiles + 3 of them) and channel: a count, and room for 64
+     * items per tile the wave walks (waves x ceil(tiles / waves) < 2 x tiles + 3) */
+    const size_t counts = (3 * (ntiles + 3) * sizeof(unsigned) + 255) & ~(size_t)255;
+    return JX_WS_HEADER + counts + 3 * (2 * ntiles + 3) * 64 * sizeof(uint32_t);
 }
 
 int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
@@ -767,7 +759,6 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
                        int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream,
                        void *event_after)
 {
-    (void)d_workspace;
     if (!fr || !p) return JPGX_EARG;
     int rc = jpgx_validate(fr->width, fr->height, p);
     if (rc) return rc;
@@ -786,7 +777,9 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     if (fr->nframes > 1 && fr->out_frame_stride < 3 * nb * 64) return JPGX_EARG;
     if (fr->nframes > 1 && fr->in_frame_stride < fr->in_pitch * (size_t)(fr->row_end - fr->row_begin) * 8)
         return JPGX_EARG;
-    if (workspace_bytes < jpgx_workspace_size(fr)) return JPGX_EWORKSPACE;
+    if (workspace_bytes < jpgx_workspace_size(fr) || !d_workspace ||
+        ((uintptr_t)d_workspace & 15))
+        return JPGX_EWORKSPACE;
 
     jx_xform_args xa;
     memset(&xa, 0, sizeof xa);
@@ -805,16 +798,35 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     if (rc) return rc;
     xa.quality = p->quality;
     xa.force_exact = (p->flags & JPGX_FLAG_FORCE_EXACT) ? 1 : 0;
-
     hipStream_t s = (hipStream_t)stream;
     const size_t ntiles = (total + 63) / 64;
     const size_t waves = std::min<size_t>(ntiles, (size_t)std::max(resident_waves(), 4));
     const unsigned grid = (unsigned)((waves + JX_WG / 64 - 1) / (JX_WG / 64));
+    const size_t nwaves = (size_t)grid * (JX_WG / 64);      /* >= waves, <= ntiles + 3   */
+    const size_t tpw = (ntiles + nwaves - 1) / nwaves;
+    xa.fix.nwaves = (unsigned)nwaves;
+    xa.fix.capw = (unsigned)(tpw * 64);
+    xa.fix.count = (unsigned *)((uint8_t *)d_workspace + JX_WS_HEADER);
+    xa.fix.items = (uint32_t *)((uint8_t *)d_workspace + JX_WS_HEADER +
+                                ((3 * nwaves * sizeof(unsigned) + 255) & ~(size_t)255));
+    /* the layout must fit the size promised by jpgx_workspace_size */
+    if (JX_WS_HEADER + ((3 * nwaves * sizeof(unsigned) + 255) & ~(size_t)255) +
+            3 * nwaves * tpw * 64 * sizeof(uint32_t) > workspace_bytes)
+        return JPGX_EWORKSPACE;
     hipLaunchKernelGGL(k_xform, dim3(grid), dim3(JX_WG), 0, s, xa);
     rc = hip_rc(hipGetLastError());
     if (rc) return rc;
     if (event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
-    return rc;
+    if (rc) return rc;
+    /* exact pass: one wave per channel and group of kFixGroup k_xform waves */
+    const size_t jobs = 3 * ((nwaves + kFixGroup - 1) / kFixGroup);
+    const unsigned fgrid = (unsigned)((jobs + 3) / 4);
+#ifndef JX_DBG_HOST_NO_FIX        /* timing experiments only (NOT exact when set) */
+    if (!JX_DBG_NO_EXACT) hipLaunchKernelGGL(k_fix, dim3(fgrid), dim3(256), 0, s, xa);
+#else
+    (void)fgrid;
+#endif
+    return hip_rc(hipGetLastError());
 }
 
 int jpgx_gen_splitmix_gpu(uint8_t *d_dst, size_t nbytes, uint64_t seed, void *stream)
@@ -870,11 +882,13 @@ static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
     fr.out_frame_stride = 3 * nb_s * 64;
     uint8_t *d_in = nullptr;
     int16_t *d_out = nullptr;
+    void *d_ws = nullptr;
+    const size_t ws = jpgx_workspace_size(&fr);
     hipStream_t s = nullptr;
     int rc = JPGX_OK;
     if (hipMalloc(&d_in, rows * dpitch) != hipSuccess ||
         hipMalloc(&d_out, 3 * nb_s * 64 * sizeof(int16_t)) != hipSuccess ||
-        hipStreamCreate(&s) != hipSuccess) {
+        hipMalloc(&d_ws, ws) != hipSuccess || hipStreamCreate(&s) != hipSuccess) {
         rc = JPGX_EHIP;
     }
     if (!rc) {
@@ -882,7 +896,7 @@ static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
         rc = hip_rc(hipMemcpy2DAsync(d_in, dpitch, src, pitch, row_bytes, rows,
                                      hipMemcpyHostToDevice, s));
     }
-    if (!rc) rc = jpgx_blocks_gpu(&fr, p, d_in + halo * dpitch, d_out, nullptr, 0, s);
+    if (!rc) rc = jpgx_blocks_gpu(&fr, p, d_in + halo * dpitch, d_out, d_ws, ws, s);
     for (int ch = 0; ch < 3 && !rc; ch++)
         rc = hip_rc(hipMemcpyAsync(out + ((size_t)ch * nb + (size_t)r0 * bpr) * 64,
                                    d_out + (size_t)ch * nb_s * 64, nb_s * 64 * sizeof(int16_t),
@@ -891,6 +905,7 @@ static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
     if (s) (void)hipStreamDestroy(s);
     (void)hipFree(d_in);
     (void)hipFree(d_out);
+    (void)hipFree(d_ws);
     return rc;
 }
 

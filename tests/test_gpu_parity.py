@@ -143,6 +143,10 @@ def test_invalid_arguments_gpu(cuda):
         jpgx.blocks_gpu(jpgx.frames(16, 16, rows=(1, 3)), jpgx.default_params(16, 16, 50), rgb,
                         out, 0)
     assert e.value.rc == jpgx.EARG
+    small = torch.empty(jpgx.workspace_size(fr) - 4, dtype=torch.uint8, device=cuda)
+    with pytest.raises(jpgx.JpgxError) as e:        # workspace too small
+        jpgx.blocks_gpu(fr, jpgx.default_params(16, 16, 50), rgb, out, small)
+    assert e.value.rc == jpgx.EWORKSPACE
 
 
 def test_gpu_generators_match_oracle(cuda):

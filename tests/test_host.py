@@ -101,6 +101,11 @@ def test_kernel_cos_table_is_glibc():
 
 
 def test_workspace_size():
-    # the exact-fixup queue lives in LDS: no device workspace for any geometry
-    assert jpgx.workspace_size(jpgx.frames(3840, 2160, nframes=8)) == 0
+    # header + per-wave counts + per-wave lists with room for every block of its tiles
+    def expect(nblocks):
+        tiles = (nblocks + 63) // 64
+        return 256 + (3 * (tiles + 3) * 4 + 255) // 256 * 256 + 3 * (2 * tiles + 3) * 256
+    nb = (3840 // 8) * (2160 // 8) * 8
+    assert jpgx.workspace_size(jpgx.frames(3840, 2160, nframes=8)) == expect(nb)
+    assert jpgx.workspace_size(jpgx.frames(64, 64, rows=(2, 5))) == expect(3 * 8)
     assert jpgx.workspace_size(jpgx.frames(64, 64, rows=(3, 3))) == 0
