@@ -43,6 +43,13 @@ namespace {
 #ifndef JX_PREFETCH
 #define JX_PREFETCH 0   /* input prefetch mode, see k_xform */
 #endif
+#ifndef JX_RELOAD       /* 1: pixels re-read (L2) per channel, issued during the previous
+                           column pass: they are not kept in registers across channels */
+#define JX_RELOAD 0
+#endif
+#ifndef JX_RELOAD_COL   /* column of the column pass at which the next loads are issued  */
+#define JX_RELOAD_COL 4
+#endif
 #ifndef JX_ROW_SB       /* scheduling fence between the row DCTs of a channel          */
 #define JX_ROW_SB 1
 #endif
@@ -59,8 +66,10 @@ namespace {
 #else
 #define JX_SB_COL() ((void)0)
 #endif
-#ifndef JX_WPE          /* minimum waves per SIMD the register allocation must allow    */
-#define JX_WPE 2
+#ifndef JX_WPE          /* minimum waves per SIMD the register allocation must allow:
+                           3 (<= 168 VGPRs; a few spills outside the tile loop) measured
+                           faster than 2 (no spills)                                     */
+#define JX_WPE 3
 #endif
 #ifndef JX_DBG_NO_EXACT  /* debug/measurement only: drop the exact path (NOT bit-exact)    */
 #define JX_DBG_NO_EXACT 0
@@ -93,12 +102,12 @@ __host__ __device__ constexpr int zz_col(int z)
     return -1;
 }
 /* the column pass after which zig-zag entries z0 and z1 are both available */
-__host__ __device__ constexpr int zz_col_done(int z0, int z1)
+[[maybe_unused]] __host__ __device__ constexpr int zz_col_done(int z0, int z1)
 {
     return zz_col(z0) > zz_col(z1) ? zz_col(z0) : zz_col(z1);
 }
 /* the column pass after which the 16-byte output chunk j (zig-zag 8j..8j+7) is complete */
-__host__ __device__ constexpr int zz_chunk_done(int j)
+[[maybe_unused]] __host__ __device__ constexpr int zz_chunk_done(int j)
 {
     int m = 0;
     for (int z = 8 * j; z < 8 * j + 8; z++) m = zz_col(z) > m ? zz_col(z) : m;
@@ -139,11 +148,32 @@ __device__ __forceinline__ void jx_store(u32x4 *p, u32x4 v)
 #endif
 }
 
+#ifndef JX_STAGE16      /* 1: each int16 goes to LDS as produced (no register packing:
+                           fewer live VGPRs, what lets 3 waves share a SIMD)             */
+#define JX_STAGE16 1
+#endif
+
 /* Per-wave LDS */
 struct WaveLds {
+#if JX_STAGE16
+    uint32_t stage[64 * 33];      /* one channel: block k at dwords 33k.. (odd stride: the
+                                     16-bit writes of 64 lanes hit 64 different banks)      */
+#else
     u32x4 stage[64 * 9];          /* one channel: block k's 8 chunks at units 9k..9k+7     */
+#endif
     uint32_t item[3][kItems];     /* per channel: queued launch-global block indices       */
 };
+
+/* 16-B unit e (block e/8, zig-zag chunk e%8) of the staged channel */
+__device__ __forceinline__ u32x4 stage_unit(const WaveLds &W, unsigned e)
+{
+#if JX_STAGE16
+    const unsigned o = (e >> 3) * 33 + (e & 7) * 4;
+    return u32x4{W.stage[o], W.stage[o + 1], W.stage[o + 2], W.stage[o + 3]};
+#else
+    return W.stage[(e >> 3) * 9 + (e & 7)];
+#endif
+}
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&row)[6], int k)
 {
@@ -293,20 +323,23 @@ struct Queue {
 
 /* Column pass, quantisation, zig-zag, LDS staging + coalesced store of channel CH; block-
  * channels with a coefficient inside the guard band are queued for the exact path. */
-template <int CH>
+template <int CH, class Pre>
 __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args &a, WaveLds &W,
                                            Queue &Q, bool active, unsigned b, unsigned t,
-                                           unsigned lane)
+                                           unsigned lane, Pre &&pre)
 {
     const jx_geom &g = a.g;
+#if !JX_STAGE16
     uint32_t bits[64];     /* tm bit patterns by zig-zag index; low 16 bits = the int16    */
     uint32_t packed[32];   /* zig-zag pairs (2k, 2k+1) as one dword, formed when complete */
+#endif
     const jx_qtab &tab = g_qtab[a.quality];
     const jx_limtab &band = g_lim[a.force_exact ? 1 : 0][a.quality];
     /* wave mask of lanes with a coefficient of this channel inside the guard band */
     uint64_t seen = 0;
 #pragma unroll
     for (int u = 0; u < 8; u++) {
+        if (u == JX_RELOAD_COL) pre();      /* e.g. issue the next pixel loads (JX_RELOAD) */
         float col[8], F[8];
 #pragma unroll
         for (int y = 0; y < 8; y++) col[y] = T[y][u];
@@ -315,7 +348,11 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
         for (int v = 0; v < 8; v++) {
             float tm, d;
             quant_coef(F[v], tab.w[CH][u][v], tm, d);
+#if JX_STAGE16
+            ((uint16_t *)W.stage)[lane * 66 + zz_of(v, u)] = (uint16_t)__float_as_uint(tm);
+#else
             bits[zz_of(v, u)] = __float_as_uint(tm);
+#endif
             if (!JX_DBG_NO_EXACT) {
                 /* compare straight into a lane mask, OR-ed at once (left to the compiler,
                  * the 64 masks of a channel are kept alive until the end and spilled) */
@@ -327,6 +364,7 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
                     : "scc");
             }
         }
+#if !JX_STAGE16
         /* pack zig-zag pairs completed by this column; stage the 16-B chunks it completes
          * (compile-time decisions: the loops are fully unrolled) */
 #pragma unroll
@@ -338,6 +376,7 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
             if (zz_chunk_done(j) == u)
                 W.stage[lane * 9 + j] =
                     u32x4{packed[4 * j], packed[4 * j + 1], packed[4 * j + 2], packed[4 * j + 3]};
+#endif
         JX_SB_COL();
     }
 
@@ -351,15 +390,14 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const unsigned e = (unsigned)j * 64u + lane;
-            jx_store(dst + e, W.stage[(e >> 3) * 9 + (e & 7)]);
+            jx_store(dst + e, stage_unit(W, e));
         }
     } else {                                   /* tile crosses a frame end or the last tile */
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const unsigned e = (unsigned)j * 64u + lane, bb = b0 + (e >> 3);
             if (bb < total)
-                jx_store((u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8),
-                         W.stage[(e >> 3) * 9 + (e & 7)]);
+                jx_store((u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8), stage_unit(W, e));
         }
     }
     /* some lane has a coefficient inside the guard band (about 40% of the channel-tiles of
@@ -447,7 +485,7 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
     WaveLds &W = s_wave[threadIdx.x >> 6];
     Queue Q{{0, 0, 0}, {0u, 0u, 0u}};
     uint32_t raw[8][6];
-#if JX_PREFETCH
+#if JX_PREFETCH || JX_RELOAD
     {
         const unsigned b = tile_block(t, lane, total), f = b / nb;
         load_block(g, f, b - f * nb, raw);
@@ -464,18 +502,38 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
             const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
             load_block(g, fn, bn - fn * nb, nxt);
         }
-#elif JX_PREFETCH == 0
+#elif JX_PREFETCH == 0 && !JX_RELOAD
         {
             const unsigned f = b / nb;
             load_block(g, f, b - f * nb, raw);
         }
 #endif
         float T[8][8];
+#if JX_RELOAD
+        const unsigned f = b / nb, bi = b - f * nb;
+        const auto reload = [&]() { load_block(g, f, bi, raw); };
+        const auto next = [&]() {
+            if (tn < ntiles) {
+                const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
+                load_block(g, fn, bn - fn * nb, raw);
+            }
+        };
         xform_rows<0>(raw, T);
-        xform_cols<0>(T, a, W, Q, active, b, t, lane);
+        xform_cols<0>(T, a, W, Q, active, b, t, lane, reload);
         __builtin_amdgcn_sched_barrier(0);
         xform_rows<1>(raw, T);
-        xform_cols<1>(T, a, W, Q, active, b, t, lane);
+        xform_cols<1>(T, a, W, Q, active, b, t, lane, reload);
+        __builtin_amdgcn_sched_barrier(0);
+        xform_rows<2>(raw, T);
+        xform_cols<2>(T, a, W, Q, active, b, t, lane, next);
+        __builtin_amdgcn_sched_barrier(0);
+#else
+        const auto none = []() {};
+        xform_rows<0>(raw, T);
+        xform_cols<0>(T, a, W, Q, active, b, t, lane, none);
+        __builtin_amdgcn_sched_barrier(0);
+        xform_rows<1>(raw, T);
+        xform_cols<1>(T, a, W, Q, active, b, t, lane, none);
         __builtin_amdgcn_sched_barrier(0);
         xform_rows<2>(raw, T);
 #if JX_PREFETCH == 2
@@ -484,8 +542,9 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
             load_block(g, fn, bn - fn * nb, raw);
         }
 #endif
-        xform_cols<2>(T, a, W, Q, active, b, t, lane);
+        xform_cols<2>(T, a, W, Q, active, b, t, lane, none);
         __builtin_amdgcn_sched_barrier(0);
+#endif
         /* keep room for the next tile's 64 possible items per channel */
         if (!JX_DBG_NO_EXACT) {
 #pragma unroll
@@ -506,7 +565,9 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
     if (!JX_DBG_NO_EXACT) {
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) flush_queue(W, Q, ch, a.fix, wave, lane);
-        if (lane < 3) a.fix.count[lane * a.fix.nwaves + wave] = Q.done[lane];
+        /* (no runtime index into Q: that would put it in scratch memory) */
+        const unsigned mine = lane == 0 ? Q.done[0] : (lane == 1 ? Q.done[1] : Q.done[2]);
+        if (lane < 3) a.fix.count[lane * a.fix.nwaves + wave] = mine;
     }
 }
 
