@@ -52,7 +52,7 @@ def run(lib):
 def main():
     names = sys.argv[1:] or sorted(os.path.basename(p)[8:-3] for p in glob.glob(f"{VAR}/libjpgx_*.so"))
     libs = {"default": os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "lib", "libjpgx.so")}
-    libs.update({n: f"{VAR}/libjpgx_{n}.so" for n in names})
+    libs.update({n: f"{VAR}/libjpgx_{n}.so" for n in names if n != "default"})
     res = {}
     for rnd in range(2):                      # interleaved rounds
         for n, lib in libs.items():
