@@ -145,6 +145,25 @@ void jpgx_free(void *p);
 int jpgx_encode_bmp(const char *path, int quality, int sample_ratio, int device, int do_dpcm,
                     jpgx_JpgData j);
 
+/* ---- 5. Entropy stage: a baseline JFIF writer (the build's own; the reference's Huffman stage
+ *         never terminates, src/huffman.c:23-235, so this has no reference to match) --------- */
+
+/* Upper bound of the file size jpgx_write_jfif can produce for a width x height image. */
+size_t jpgx_jfif_bound(int width, int height);
+
+/* Baseline sequential JFIF (8-bit, one interleaved scan, 4:4:4, ITU-T T.81 Annex K.3 Huffman
+ * tables, true DC prediction) of coef [3][nb][64] (zig-zag, raster blocks).  The DQT holds the
+ * divisors the reference applied (its scaled tables, transposed: src/quantise.c:58), so a
+ * standard decoder reproduces the reference's coefficients' image.  Returns 0, JPGX_EARG
+ * (geometry, or cap too small: *len is then the size needed), JPGX_EQUALITY. */
+int jpgx_write_jfif(const int16_t *coef, int width, int height, int quality, uint8_t *out,
+                    size_t cap, size_t *len);
+
+/* The reference's public entry point (src/headers/jpg_encode.h:85): BMP in, JPEG file out --
+ * the block transform on GPU 0, then jpgx_write_jfif.  Returns 0 or a JPGX_E* code. */
+int jpgx_encode_bmp_to_jpeg(const char *input, const char *output, int quality,
+                            int sample_ratio);
+
 #ifdef __cplusplus
 }
 #endif

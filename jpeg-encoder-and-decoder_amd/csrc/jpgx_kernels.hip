@@ -861,7 +861,18 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     xa.force_exact = (p->flags & JPGX_FLAG_FORCE_EXACT) ? 1 : 0;
     hipStream_t s = (hipStream_t)stream;
     const size_t ntiles = (total + 63) / 64;
-    const size_t waves = std::min<size_t>(ntiles, (size_t)std::max(resident_waves(), 4));
+#ifndef JX_PERSISTENT     /* 0: one wave per tile (the dispatcher refills SIMDs as waves end) */
+#define JX_PERSISTENT 1
+#endif
+    size_t waves = JX_PERSISTENT ? std::min<size_t>(ntiles, (size_t)std::max(resident_waves(), 4))
+                                 : ntiles;
+#ifndef JX_GRID_BALANCE   /* 1: fewest waves that still finish in the same number of rounds */
+#define JX_GRID_BALANCE 0
+#endif
+    if (JX_GRID_BALANCE) {
+        const size_t rounds = (ntiles + waves - 1) / waves;
+        waves = (ntiles + rounds - 1) / rounds;
+    }
     const unsigned grid = (unsigned)((waves + JX_WG / 64 - 1) / (JX_WG / 64));
     const size_t nwaves = (size_t)grid * (JX_WG / 64);      /* >= waves, <= ntiles + 3   */
     const size_t tpw = (ntiles + nwaves - 1) / nwaves;

@@ -1,0 +1,280 @@
+/*
+ * jpgx_jfif.c -- baseline JFIF writer for the block transform's output (host C99).
+ *
+ * The reference never writes a file: its huffman_encode() does not terminate and only counts
+ * symbols (src/huffman.c:23-235), and its dpcm() is an alternating-sign
+ * recurrence, not a DC prediction (src/dpcm.c:10-20).  This is the build's own entropy stage
+ * (parity unpinned): baseline sequential DCT, 8-bit, one interleaved scan, 4:4:4
+ * (the reference's output for every sample_ratio), the standard Huffman tables of ITU-T T.81
+ * Annex K.3, true DC prediction per component.
+ *
+ * The coefficients are the reference's, quirks included, and the file describes them
+ * faithfully: the DQT entries are the divisors the reference actually applied, i.e. the scaled
+ * table transposed (src/quantise.c:58).  A standard decoder therefore reproduces the
+ * reference's pipeline output -- including the effects of its Cb sign error
+ * (src/preprocess.c:161) and of the x0 = -8 last-column quirk.  AC magnitudes above 1023
+ * (possible only for chroma at q >= 93 with the sign error) are clamped to the baseline range.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/jpgx_compat.h"
+#include "../csrc/jx_consts.h"
+
+/* ITU-T T.81 Annex K.3, Tables K.3-K.6: code-length counts and symbol values */
+static const uint8_t kDcLumBits[16] = {0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0};
+static const uint8_t kDcChrBits[16] = {0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0};
+static const uint8_t kDcVals[12] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+static const uint8_t kAcLumBits[16] = {0, 2, 1, 3, 3, 2, 4, 3, 5, 5, 4, 4, 0, 0, 1, 0x7d};
+static const uint8_t kAcLumVals[162] = {
+    0x01, 0x02, 0x03, 0x00, 0x04, 0x11, 0x05, 0x12, 0x21, 0x31, 0x41, 0x06, 0x13, 0x51, 0x61,
+    0x07, 0x22, 0x71, 0x14, 0x32, 0x81, 0x91, 0xa1, 0x08, 0x23, 0x42, 0xb1, 0xc1, 0x15, 0x52,
+    0xd1, 0xf0, 0x24, 0x33, 0x62, 0x72, 0x82, 0x09, 0x0a, 0x16, 0x17, 0x18, 0x19, 0x1a, 0x25,
+    0x26, 0x27, 0x28, 0x29, 0x2a, 0x34, 0x35, 0x36, 0x37, 0x38, 0x39, 0x3a, 0x43, 0x44, 0x45,
+    0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59, 0x5a, 0x63, 0x64,
+    0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a, 0x83,
+    0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99,
+    0x9a, 0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4, 0xb5, 0xb6,
+    0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca, 0xd2, 0xd3,
+    0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe1, 0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8,
+    0xe9, 0xea, 0xf1, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+static const uint8_t kAcChrBits[16] = {0, 2, 1, 2, 4, 4, 3, 4, 7, 5, 4, 4, 0, 1, 2, 0x77};
+static const uint8_t kAcChrVals[162] = {
+    0x00, 0x01, 0x02, 0x03, 0x11, 0x04, 0x05, 0x21, 0x31, 0x06, 0x12, 0x41, 0x51, 0x07, 0x61,
+    0x71, 0x13, 0x22, 0x32, 0x81, 0x08, 0x14, 0x42, 0x91, 0xa1, 0xb1, 0xc1, 0x09, 0x23, 0x33,
+    0x52, 0xf0, 0x15, 0x62, 0x72, 0xd1, 0x0a, 0x16, 0x24, 0x34, 0xe1, 0x25, 0xf1, 0x17, 0x18,
+    0x19, 0x1a, 0x26, 0x27, 0x28, 0x29, 0x2a, 0x35, 0x36, 0x37, 0x38, 0x39, 0x3a, 0x43, 0x44,
+    0x45, 0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59, 0x5a, 0x63,
+    0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a,
+    0x82, 0x83, 0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97,
+    0x98, 0x99, 0x9a, 0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4,
+    0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca,
+    0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7,
+    0xe8, 0xe9, 0xea, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+
+/* canonical Huffman codes (T.81 Annex C) indexed by symbol */
+typedef struct {
+    uint16_t code[256];
+    uint8_t len[256];
+} HuffCodes;
+
+static void build_codes(const uint8_t bits[16], const uint8_t *vals, HuffCodes *h)
+{
+    memset(h, 0, sizeof(*h));
+    unsigned code = 0, k = 0;
+    for (int l = 1; l <= 16; l++) {
+        for (int i = 0; i < bits[l - 1]; i++, k++) {
+            h->code[vals[k]] = (uint16_t)code++;
+            h->len[vals[k]] = (uint8_t)l;
+        }
+        code <<= 1;
+    }
+}
+
+typedef struct {
+    uint8_t *p;
+    size_t n, cap;
+    uint32_t acc;     /* pending bits, MSB first */
+    int nacc;
+    int overflow;
+} Out;
+
+static void put_byte(Out *o, uint8_t b)
+{
+    if (o->n < o->cap) o->p[o->n] = b;
+    else o->overflow = 1;
+    o->n++;
+}
+
+static void put_u16(Out *o, unsigned v)
+{
+    put_byte(o, (uint8_t)(v >> 8));
+    put_byte(o, (uint8_t)v);
+}
+
+static void put_bits(Out *o, unsigned v, int nbits)
+{
+    for (int i = nbits - 1; i >= 0; i--) {
+        o->acc = (o->acc << 1) | ((v >> i) & 1u);
+        if (++o->nacc == 8) {
+            const uint8_t b = (uint8_t)o->acc;
+            put_byte(o, b);
+            if (b == 0xff) put_byte(o, 0x00);            /* byte stuffing (T.81 F.1.2.3) */
+            o->acc = 0;
+            o->nacc = 0;
+        }
+    }
+}
+
+static void flush_bits(Out *o)
+{
+    if (o->nacc) put_bits(o, 0x7fu, 8 - o->nacc);      /* pad with 1-bits */
+}
+
+/* magnitude category and the value's additional bits (T.81 F.1.2.1) */
+static int category(int v, unsigned *extra)
+{
+    const int a = v < 0 ? -v : v;
+    int s = 0;
+    while ((1 << s) <= a) s++;
+    *extra = (unsigned)(v < 0 ? v + (1 << s) - 1 : v) & ((1u << s) - 1u);
+    return s;
+}
+
+static void put_dht(Out *o, int cls_id, const uint8_t bits[16], const uint8_t *vals)
+{
+    int n = 0;
+    for (int i = 0; i < 16; i++) n += bits[i];
+    put_u16(o, 0xffc4);
+    put_u16(o, (unsigned)(2 + 1 + 16 + n));
+    put_byte(o, (uint8_t)cls_id);
+    for (int i = 0; i < 16; i++) put_byte(o, bits[i]);
+    for (int i = 0; i < n; i++) put_byte(o, vals[i]);
+}
+
+size_t jpgx_jfif_bound(int width, int height)
+{
+    if (width <= 0 || height <= 0) return 0;
+    /* headers + worst case per block (DC 2+11 bits, 63 AC x (16+10 bits)) + stuffing x2 */
+    const size_t blocks = (size_t)(width / 8 + 1) * (height / 8 + 1) * 3;
+    return 1024 + blocks * 2 * (13 + 63 * 26 + 7) / 8;
+}
+
+int jpgx_write_jfif(const int16_t *coef, int width, int height, int quality, uint8_t *out,
+                    size_t cap, size_t *len)
+{
+    if (!coef || !out || width <= 0 || height <= 0 || width % 8 || height % 8 ||
+        width > 65535 || height > 65535)
+        return JPGX_EARG;
+    int qs[2][8][8];
+    if (jpgx_scale_table(0, quality, qs[0]) || jpgx_scale_table(1, quality, qs[1]))
+        return JPGX_EQUALITY;
+    static const int scan[8][8] = JX_SCAN_ORDER_INIT;
+    Out o = {out, 0, cap, 0, 0, 0};
+
+    put_u16(&o, 0xffd8);                                   /* SOI */
+    put_u16(&o, 0xffe0);                                   /* APP0 JFIF 1.01 */
+    put_u16(&o, 16);
+    put_byte(&o, 'J'); put_byte(&o, 'F'); put_byte(&o, 'I'); put_byte(&o, 'F'); put_byte(&o, 0);
+    put_u16(&o, 0x0101);
+    put_byte(&o, 0);
+    put_u16(&o, 1);
+    put_u16(&o, 1);
+    put_byte(&o, 0); put_byte(&o, 0);
+    for (int t = 0; t < 2; t++) {                          /* DQT: the divisors applied */
+        uint8_t zz[64];
+        for (int v = 0; v < 8; v++)
+            for (int u = 0; u < 8; u++) {
+                int q = qs[t][u][v];                       /* coefficient (row v, col u) was
+                                                              divided by Qs[u][v] */
+                zz[scan[v][u]] = (uint8_t)(q < 1 ? 1 : (q > 255 ? 255 : q));
+            }
+        put_u16(&o, 0xffdb);
+        put_u16(&o, 2 + 65);
+        put_byte(&o, (uint8_t)t);
+        for (int k = 0; k < 64; k++) put_byte(&o, zz[k]);
+    }
+    put_u16(&o, 0xffc0);                                   /* SOF0 */
+    put_u16(&o, 8 + 3 * 3);
+    put_byte(&o, 8);
+    put_u16(&o, (unsigned)height);
+    put_u16(&o, (unsigned)width);
+    put_byte(&o, 3);
+    for (int c = 0; c < 3; c++) {
+        put_byte(&o, (uint8_t)(c + 1));
+        put_byte(&o, 0x11);                                /* 4:4:4 */
+        put_byte(&o, (uint8_t)(c ? 1 : 0));
+    }
+    put_dht(&o, 0x00, kDcLumBits, kDcVals);
+    put_dht(&o, 0x10, kAcLumBits, kAcLumVals);
+    put_dht(&o, 0x01, kDcChrBits, kDcVals);
+    put_dht(&o, 0x11, kAcChrBits, kAcChrVals);
+    put_u16(&o, 0xffda);                                   /* SOS */
+    put_u16(&o, 6 + 2 * 3);
+    put_byte(&o, 3);
+    for (int c = 0; c < 3; c++) {
+        put_byte(&o, (uint8_t)(c + 1));
+        put_byte(&o, (uint8_t)(c ? 0x11 : 0x00));
+    }
+    put_byte(&o, 0);
+    put_byte(&o, 63);
+    put_byte(&o, 0);
+
+    HuffCodes dc[2], ac[2];
+    build_codes(kDcLumBits, kDcVals, &dc[0]);
+    build_codes(kDcChrBits, kDcVals, &dc[1]);
+    build_codes(kAcLumBits, kAcLumVals, &ac[0]);
+    build_codes(kAcChrBits, kAcChrVals, &ac[1]);
+    const size_t nb = (size_t)(width / 8) * (height / 8);
+    int pred[3] = {0, 0, 0};
+    for (size_t i = 0; i < nb; i++)                        /* MCU = one block per component */
+        for (int c = 0; c < 3; c++) {
+            const int16_t *z = coef + ((size_t)c * nb + i) * 64;
+            const int t = c ? 1 : 0;
+            unsigned extra;
+            int diff = z[0] - pred[c];                     /* true DC prediction */
+            if (diff > 2047) diff = 2047;                  /* (never reached: |DC| <= 1364) */
+            if (diff < -2047) diff = -2047;
+            pred[c] = z[0];
+            const int s = category(diff, &extra);
+            put_bits(&o, dc[t].code[s], dc[t].len[s]);
+            put_bits(&o, extra, s);
+            int run = 0;
+            for (int k = 1; k < 64; k++) {
+                int v = z[k];
+                if (v > 1023) v = 1023;
+                if (v < -1023) v = -1023;
+                if (v == 0) {
+                    run++;
+                    continue;
+                }
+                while (run > 15) {                         /* ZRL */
+                    put_bits(&o, ac[t].code[0xf0], ac[t].len[0xf0]);
+                    run -= 16;
+                }
+                const int sa = category(v, &extra);
+                const int sym = run << 4 | sa;
+                put_bits(&o, ac[t].code[sym], ac[t].len[sym]);
+                put_bits(&o, extra, sa);
+                run = 0;
+            }
+            if (run) put_bits(&o, ac[t].code[0x00], ac[t].len[0x00]);   /* EOB */
+        }
+    flush_bits(&o);
+    put_u16(&o, 0xffd9);                                   /* EOI */
+    if (len) *len = o.n;
+    return o.overflow ? JPGX_EARG : JPGX_OK;
+}
+
+int jpgx_encode_bmp_to_jpeg(const char *input, const char *output, int quality,
+                            int sample_ratio)
+{
+    if (!input || !output) return JPGX_EARG;
+    jpgx_jpeg_data j;
+    memset(&j, 0, sizeof j);
+    int rc = jpgx_encode_bmp(input, quality, sample_ratio, 0, 0, &j);
+    if (rc) return rc;
+    const size_t nb = (size_t)j.num_blocks_Y;
+    int16_t *coef = (int16_t *)malloc(nb * 3 * 64 * sizeof(int16_t));
+    const size_t cap = jpgx_jfif_bound(j.width, j.height);
+    uint8_t *buf = (uint8_t *)malloc(cap);
+    size_t len = 0;
+    rc = (coef && buf) ? JPGX_OK : JPGX_EARG;
+    if (!rc) {
+        int **zz[3] = {j.zig_zag_Y, j.zig_zag_Cb, j.zig_zag_Cr};
+        for (int c = 0; c < 3; c++)
+            for (size_t i = 0; i < nb; i++)
+                for (int k = 0; k < 64; k++) coef[((size_t)c * nb + i) * 64 + k] = (int16_t)zz[c][i][k];
+        rc = jpgx_write_jfif(coef, j.width, j.height, quality, buf, cap, &len);
+    }
+    if (!rc) {
+        FILE *f = fopen(output, "wb");
+        if (!f || fwrite(buf, 1, len, f) != len) rc = JPGX_EARG;
+        if (f && fclose(f)) rc = JPGX_EARG;
+    }
+    jpgx_free_jpgdata(&j);
+    free(coef);
+    free(buf);
+    return rc;
+}

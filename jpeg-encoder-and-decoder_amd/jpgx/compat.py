@@ -82,6 +82,11 @@ def _setup(L):
     L.jpgx_free.restype = None
     L.jpgx_free.argtypes = [vp]
     L.jpgx_encode_bmp.argtypes = [ctypes.c_char_p, i, i, i, i, J]
+    L.jpgx_jfif_bound.restype = ctypes.c_size_t
+    L.jpgx_jfif_bound.argtypes = [i, i]
+    L.jpgx_write_jfif.argtypes = [vp, i, i, i, vp, ctypes.c_size_t,
+                                  ctypes.POINTER(ctypes.c_size_t)]
+    L.jpgx_encode_bmp_to_jpeg.argtypes = [ctypes.c_char_p, ctypes.c_char_p, i, i]
 
 
 _setup(lib)
@@ -213,3 +218,20 @@ def encode_bmp(path: str, quality: int, sample_ratio: int = 0, device: int = 0,
     _check(lib.jpgx_encode_bmp(j._path, quality, sample_ratio, device, int(do_dpcm),
                                ctypes.byref(j)), "jpgx_encode_bmp")
     return j
+
+
+def write_jfif(coef: np.ndarray, width: int, height: int, quality: int) -> bytes:
+    """int16 [3][nb][64] -> baseline JFIF bytes (jpgx_write_jfif)."""
+    coef = np.ascontiguousarray(coef, np.int16)
+    cap = lib.jpgx_jfif_bound(width, height)
+    buf = (ctypes.c_uint8 * cap)()
+    n = ctypes.c_size_t()
+    _check(lib.jpgx_write_jfif(coef.ctypes.data, width, height, quality,
+                               ctypes.cast(buf, ctypes.c_void_p), cap, ctypes.byref(n)),
+           "jpgx_write_jfif")
+    return bytes(buf[:n.value])
+
+
+def encode_bmp_to_jpeg(src: str, dst: str, quality: int, sample_ratio: int = 0) -> None:
+    _check(lib.jpgx_encode_bmp_to_jpeg(src.encode(), dst.encode(), quality, sample_ratio),
+           "jpgx_encode_bmp_to_jpeg")

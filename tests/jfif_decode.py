@@ -1,0 +1,119 @@
+"""Minimal baseline-JPEG entropy decoder (test helper): parses the markers jpgx_write_jfif
+emits (SOF0, DQT, DHT, one interleaved SOS, no restart markers) and returns the quantised
+zig-zag coefficients [ncomp][nblocks][64] and the DQT tables -- an independent check of the
+writer, written from ITU-T T.81 (Annex C canonical codes, F.2.2 decoding, F.1.2.3 stuffing)."""
+import numpy as np
+
+
+def _u16(b, i):
+    return b[i] << 8 | b[i + 1]
+
+
+class _Bits:
+    def __init__(self, data):
+        self.d, self.i, self.acc, self.n = data, 0, 0, 0
+
+    def bit(self):
+        if self.n == 0:
+            b = self.d[self.i]
+            self.i += 1
+            if b == 0xFF:
+                nxt = self.d[self.i]
+                assert nxt == 0x00, f"marker 0xFF{nxt:02X} inside entropy data"
+                self.i += 1
+            self.acc, self.n = b, 8
+        self.n -= 1
+        return (self.acc >> self.n) & 1
+
+    def bits(self, k):
+        v = 0
+        for _ in range(k):
+            v = v << 1 | self.bit()
+        return v
+
+
+def _table(bits, vals):
+    """canonical codes -> {(length, code): symbol}"""
+    out, code, k = {}, 0, 0
+    for ln in range(1, 17):
+        for _ in range(bits[ln - 1]):
+            out[(ln, code)] = vals[k]
+            code += 1
+            k += 1
+        code <<= 1
+    return out
+
+
+def _decode_sym(br, tab):
+    code = 0
+    for ln in range(1, 17):
+        code = code << 1 | br.bit()
+        if (ln, code) in tab:
+            return tab[(ln, code)]
+    raise ValueError("bad Huffman code")
+
+
+def _extend(v, s):
+    return v - (1 << s) + 1 if s and v < (1 << (s - 1)) else v
+
+
+def decode(data: bytes):
+    b = bytes(data)
+    assert b[:2] == b"\xff\xd8", "no SOI"
+    i = 2
+    dqt, dht, comps, W, H = {}, {}, [], 0, 0
+    while True:
+        assert b[i] == 0xFF
+        m = b[i + 1]
+        ln = _u16(b, i + 2)
+        seg = b[i + 4:i + 2 + ln]
+        if m == 0xDB:
+            j = 0
+            while j < len(seg):
+                assert seg[j] >> 4 == 0, "8-bit tables only"
+                dqt[seg[j] & 15] = list(seg[j + 1:j + 65])
+                j += 65
+        elif m == 0xC4:
+            j = 0
+            while j < len(seg):
+                tc_th, bits = seg[j], list(seg[j + 1:j + 17])
+                n = sum(bits)
+                dht[tc_th] = _table(bits, list(seg[j + 17:j + 17 + n]))
+                j += 17 + n
+        elif m == 0xC0:
+            assert seg[0] == 8
+            H, W = _u16(seg, 1), _u16(seg, 3)
+            comps = [(seg[6 + 3 * k], seg[7 + 3 * k], seg[8 + 3 * k]) for k in range(seg[5])]
+            assert all(c[1] == 0x11 for c in comps), "4:4:4 only"
+        elif m == 0xDA:
+            ns = seg[0]
+            sel = [(seg[1 + 2 * k], seg[2 + 2 * k]) for k in range(ns)]
+            i += 2 + ln
+            break
+        i += 2 + ln
+    nb = (W // 8) * (H // 8)
+    out = np.zeros((len(sel), nb, 64), np.int32)
+    br = _Bits(b[i:])
+    pred = [0] * len(sel)
+    for blk in range(nb):
+        for c, (_, tables) in enumerate(sel):
+            dc_t, ac_t = dht[tables >> 4], dht[0x10 | (tables & 15)]
+            s = _decode_sym(br, dc_t)
+            pred[c] += _extend(br.bits(s), s)
+            out[c, blk, 0] = pred[c]
+            k = 1
+            while k < 64:
+                rs = _decode_sym(br, ac_t)
+                r, s = rs >> 4, rs & 15
+                if s == 0:
+                    if r == 15:
+                        k += 16
+                        continue
+                    break                                  # EOB
+                k += r
+                out[c, blk, k] = _extend(br.bits(s), s)
+                k += 1
+    rest = br.d[br.i:]
+    assert rest[-2:] == b"\xff\xd9", "no EOI after the scan"
+    return {"width": W, "height": H, "coef": out, "dqt": dqt,
+            "qsel": [c[2] for c in comps]}

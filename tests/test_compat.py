@@ -155,3 +155,93 @@ def test_encode_bmp_matches_reference(golden, name):
             assert sha(C.jpgdata_zigzag(j).astype("<i4")) == ent["dpcm_sha256"][q], (name, q)
         finally:
             C.free_jpgdata(j)
+
+
+# ---- JFIF writer (the build's own entropy stage; parity unpinned: the reference's Huffman
+# stage never terminates) -- checked by decoding the file back to the coefficients -----------
+def _roundtrip(coef, W, H, q):
+    from jfif_decode import decode
+    data = C.write_jfif(coef, W, H, q)
+    d = decode(data)
+    assert (d["width"], d["height"]) == (W, H)
+    want = np.clip(coef.astype(np.int32), -1023, 1023)
+    want[:, :, 0] = coef[:, :, 0]                      # DC is not clamped
+    assert np.array_equal(d["coef"], want)
+    return data, d
+
+
+@pytest.mark.parametrize("q", [1, 25, 50, 75, 90, 97])
+def test_jfif_roundtrip_random(q):
+    W, H = 48, 40
+    coef = O.blocks(O.gen_splitmix(q, W, H), q)
+    data, d = _roundtrip(coef, W, H, q)
+    # DQT = the divisors the reference applied: its scaled tables, transposed (quantise.c:58)
+    scan = np.array([[0, 1, 5, 6, 14, 15, 27, 28], [2, 4, 7, 13, 16, 26, 29, 42],
+                     [3, 8, 12, 17, 25, 30, 41, 43], [9, 11, 18, 24, 31, 40, 44, 53],
+                     [10, 19, 23, 32, 39, 45, 52, 54], [20, 22, 33, 38, 46, 51, 55, 60],
+                     [21, 34, 37, 47, 50, 56, 59, 61], [35, 36, 48, 49, 57, 58, 62, 63]])
+    for t, base in ((0, LUM), (1, CHR)):
+        qs = np.clip(O.scale_table(base, q), 1, 255)
+        zz = np.zeros(64, np.int32)
+        for v in range(8):
+            for u in range(8):
+                zz[scan[v, u]] = qs[u, v]
+        assert d["dqt"][t] == zz.tolist()
+    assert d["qsel"] == [0, 1, 1]
+
+
+def test_jfif_roundtrip_edge_values():
+    """runs of zeros longer than 16 (ZRL), all-zero blocks (EOB only), extreme magnitudes
+    (categories 10/11), clamping above the baseline AC range, DC differences near +-2047"""
+    W, H = 24, 16
+    nb = 6
+    coef = np.zeros((3, nb, 64), np.int16)
+    coef[0, 0, 0], coef[0, 1, 0], coef[0, 2, 0] = -1024, 1016, -1024
+    coef[1, 0, 0], coef[1, 1, 0] = -1364, 672
+    coef[0, 0, 63] = 5                                # one AC after a 62-zero run
+    coef[0, 1, 1], coef[0, 1, 2] = 1023, -1023
+    coef[2, 3, 17] = 1200                             # clamped to 1023
+    coef[2, 4, 1:64] = np.arange(1, 64) * (-1) ** np.arange(63)
+    _roundtrip(coef, W, H, 97)
+
+
+def test_jfif_decodes_with_pil():
+    """a standard decoder (PIL/libjpeg) accepts the file"""
+    import io
+    Image = pytest.importorskip("PIL.Image")
+    W, H = 64, 48
+    coef = O.blocks(O.gen_splitmix(11, W, H), 75)
+    img = Image.open(io.BytesIO(C.write_jfif(coef, W, H, 75)))
+    img.load()
+    assert img.size == (W, H) and img.mode == "RGB"
+
+
+def test_jfif_small_buffer_and_bad_args():
+    import ctypes
+    from jpgx import lib
+    coef = np.zeros((3, 4, 64), np.int16)
+    buf = (ctypes.c_uint8 * 64)()
+    n = ctypes.c_size_t()
+    rc = lib.jpgx_write_jfif(coef.ctypes.data, 16, 16, 50, ctypes.cast(buf, ctypes.c_void_p), 64,
+                             ctypes.byref(n))
+    assert rc == -4 and n.value > 64                  # EARG, with the size needed
+    rc = lib.jpgx_write_jfif(coef.ctypes.data, 12, 16, 50, ctypes.cast(buf, ctypes.c_void_p), 64,
+                             ctypes.byref(n))
+    assert rc == -4
+    rc = lib.jpgx_write_jfif(coef.ctypes.data, 16, 16, 98, ctypes.cast(buf, ctypes.c_void_p), 64,
+                             ctypes.byref(n))
+    assert rc == -2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cam", "tiger"])
+def test_encode_bmp_to_jpeg_file(golden, name, tmp_path):
+    """The reference's entry point end to end: BMP -> GPU block transform -> JPEG file, whose
+    coefficients are the reference's (golden hashes of its zig_zag_* arrays)."""
+    from jfif_decode import decode
+    src = os.path.join(GOLDEN, "images", f"{name}.bmp")
+    for q, h in golden["images"][name]["coef_sha256"].items():
+        dst = str(tmp_path / f"{name}_{q}.jpg")
+        C.encode_bmp_to_jpeg(src, dst, int(q))
+        d = decode(open(dst, "rb").read())
+        assert coef_sha(d["coef"].astype(np.int16)) == h, (name, q)
