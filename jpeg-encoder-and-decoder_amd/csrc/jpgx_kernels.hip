@@ -141,6 +141,10 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void jx_store(u32x4 *p, u32x4 v)
 {
+#ifdef JX_DBG_NO_STORE      /* timing experiments only: keep the work, drop the bytes */
+    if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9e3779b9u) *p = v;
+    return;
+#endif
 #if JX_NT_STORE
     __builtin_nontemporal_store(v, p);
 #else
@@ -200,7 +204,13 @@ __device__ __forceinline__ void load_block(const jx_geom &g, unsigned f, unsigne
         p = (const uint8_t *)__builtin_assume_aligned(p, 8);
         u32x4 a;
         u32x2 b;
-#if JX_NT_LOAD
+#if defined(JX_DBG_NO_LOAD)  /* timing experiments only: synthetic bytes, no HBM reads */
+        {
+            const uint32_t s = (uint32_t)(uintptr_t)p * 2654435761u;
+            a = u32x4{s, s ^ 0x5bd1e995u, s + 0x6a09e667u, s * 3u};
+            b = u32x2{s ^ 0xbb67ae85u, s + 0x3c6ef372u};
+        }
+#elif JX_NT_LOAD
         a = __builtin_nontemporal_load((const u32x4 *)p);
         b = __builtin_nontemporal_load((const u32x2 *)(p + 16));
 #else

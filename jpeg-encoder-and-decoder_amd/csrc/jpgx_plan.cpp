@@ -152,6 +152,27 @@ void jx_under_dwords(const uint8_t under[3][8], uint32_t out[6])
     memcpy(out, row, sizeof row);
 }
 
+/* long-double evaluation of the same 1-D transform code (near-exact constants) */
+struct LDOps {
+    typedef long double T;
+    static T add(T a, T b) { return a + b; }
+    static T sub(T a, T b) { return a - b; }
+    static T mulc(T a, jx_const k) { return a * (long double)k.x; }
+    static T fmac(T a, jx_const k, T b) { return a * (long double)k.x + b; }
+    static T lit(jx_const k) { return (long double)k.x; }
+};
+
+/* Factor that turns output k of jx_fdct8 into sum_x in[x] cos((2x+1)k pi/16): evaluated on
+ * in[x] = cos((2x+1)k pi/16) (where that sum is 8 for k = 0, else 4). */
+static long double dct_kfactor(int k)
+{
+    const long double pi = 3.141592653589793238462643383279502884L;
+    long double in[8], out[8];
+    for (int x = 0; x < 8; x++) in[x] = cosl((2 * x + 1) * k * pi / 16);
+    jx_fdct8<LDOps>(in, out);
+    return (k == 0 ? 8.0L : 4.0L) / out[k];
+}
+
 int jx_plan_tables(int quality, float w[3][64], float lim[3][64], int16_t q[2][64])
 {
     int qs[2][8][8];
@@ -173,7 +194,7 @@ int jx_plan_tables(int quality, float w[3][64], float lim[3][64], int16_t q[2][6
             for (int u = 0; u < 8; u++) {
                 /* exact scale: 1/4 a(u) a(v) k(u) k(v) / Q[u][v] (dct.c:54, quantise.c:58) */
                 const long double au = u == 0 ? a0 : 1.0L, av = v == 0 ? a0 : 1.0L;
-                const long double ku = u == 4 ? a0 : 1.0L, kv = v == 4 ? a0 : 1.0L;
+                const long double ku = dct_kfactor(u), kv = dct_kfactor(v);
                 const long double ws = 0.25L * au * av * ku * kv / (long double)qs[t][u][v];
                 const float wf = (float)ws;
                 const Bnd &b = F[ch][v][u];
