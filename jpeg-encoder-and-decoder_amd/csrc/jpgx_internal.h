@@ -38,6 +38,7 @@ struct jx_qtab {
  * (every entry -1: every coefficient takes the exact path) */
 struct jx_limtab {
     float lim[3][8][8];     /* [ch][u][v] */
+    float limcol[3][8];     /* [ch][u]: min over v (one limit per column, JX_FLAG_MODE 3)  */
 };
 
 #define JX_MAXQ 97

@@ -71,6 +71,11 @@ namespace {
                            faster than 2 (no spills)                                     */
 #define JX_WPE 3
 #endif
+#ifndef JX_FLAG_MODE     /* guard-band test: 0 v_cmp into SGPR masks + s_or; 1 VALU max of
+                            |d|-lim; 2 VALU compare-or; 3 VALU max of |d| per column against
+                            the column's tightest limit (more flags, fewer instructions)     */
+#define JX_FLAG_MODE 0
+#endif
 #ifndef JX_DBG_NO_EXACT  /* debug/measurement only: drop the exact path (NOT bit-exact)    */
 #define JX_DBG_NO_EXACT 0
 #endif
@@ -347,6 +352,16 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
     const jx_limtab &band = g_lim[a.force_exact ? 1 : 0][a.quality];
     /* wave mask of lanes with a coefficient of this channel inside the guard band */
     uint64_t seen = 0;
+#if JX_FLAG_MODE == 1 || JX_FLAG_MODE == 3
+    float flagacc = -1.0f, epair = 0.0f, colmax = 0.0f;
+    (void)epair;
+    (void)colmax;
+#elif JX_FLAG_MODE == 2
+    uint32_t flagany = 0;
+#endif
+#ifdef JX_DBG_NO_STAGE
+    uint32_t dbg_acc = 0;
+#endif
 #pragma unroll
     for (int u = 0; u < 8; u++) {
         if (u == JX_RELOAD_COL) pre();      /* e.g. issue the next pixel loads (JX_RELOAD) */
@@ -359,11 +374,16 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
             float tm, d;
             quant_coef(F[v], tab.w[CH][u][v], tm, d);
 #if JX_STAGE16
+#ifdef JX_DBG_NO_STAGE              /* timing experiments only: no LDS staging writes */
+            dbg_acc ^= __float_as_uint(tm);
+#else
             ((uint16_t *)W.stage)[lane * 66 + zz_of(v, u)] = (uint16_t)__float_as_uint(tm);
+#endif
 #else
             bits[zz_of(v, u)] = __float_as_uint(tm);
 #endif
             if (!JX_DBG_NO_EXACT) {
+#if JX_FLAG_MODE == 0
                 /* compare straight into a lane mask, OR-ed at once (left to the compiler,
                  * the 64 masks of a channel are kept alive until the end and spilled) */
                 uint64_t m;
@@ -372,6 +392,38 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
                     : [m] "=&s"(m), [seen] "+s"(seen)
                     : [d] "v"(d), [l] "s"(band.lim[CH][u][v])
                     : "scc");
+#elif JX_FLAG_MODE == 1
+                /* all in VALU: e = |d| - lim, running max (>= 0 means flagged); pinned asm
+                 * like mode 0 (left to the compiler, the table loads are hoisted and spill) */
+                if (v & 1) {
+                    float e;
+                    asm("v_sub_f32_e64 %[e], |%[d]|, %[l]\n\t"
+                        "v_max3_f32 %[acc], %[acc], %[p], %[e]"
+                        : [e] "=&v"(e), [acc] "+v"(flagacc)
+                        : [d] "v"(d), [l] "s"(band.lim[CH][u][v]), [p] "v"(epair));
+                } else {
+                    asm("v_sub_f32_e64 %[e], |%[d]|, %[l]"
+                        : [e] "=v"(epair)
+                        : [d] "v"(d), [l] "s"(band.lim[CH][u][v]));
+                }
+#elif JX_FLAG_MODE == 2
+                asm("v_cmp_ge_f32_e64 vcc, |%[d]|, %[l]\n\t"
+                    "v_cndmask_b32_e64 %[f], %[f], -1, vcc"
+                    : [f] "+v"(flagany)
+                    : [d] "v"(d), [l] "s"(band.lim[CH][u][v])
+                    : "vcc");
+#elif JX_FLAG_MODE == 3
+                /* one limit per column (the column's tightest): running max of |d| */
+                if (v == 0)
+                    asm("v_max_f32_e64 %[c], |%[d]|, |%[d]|" : [c] "=v"(colmax) : [d] "v"(d));
+                else
+                    asm("v_max_f32_e64 %[c], %[c], |%[d]|" : [c] "+v"(colmax) : [d] "v"(d));
+                if (v == 7)
+                    asm("v_sub_f32_e64 %[c], %[c], %[l]\n\t"
+                        "v_max_f32_e32 %[acc], %[acc], %[c]"
+                        : [c] "+v"(colmax), [acc] "+v"(flagacc)
+                        : [l] "s"(band.limcol[CH][u]));
+#endif
             }
         }
 #if !JX_STAGE16
@@ -390,6 +442,9 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
         JX_SB_COL();
     }
 
+#ifdef JX_DBG_NO_STAGE
+    W.stage[lane] = dbg_acc;
+#endif
     /* coalesced store: the wave's 64 blocks x 128 B of this channel, 1 KiB per instruction */
     const unsigned nb = (unsigned)g.nb, total = nb * (unsigned)g.nframes;
     const unsigned b0 = t * 64u;
@@ -410,6 +465,11 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
                 jx_store((u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8), stage_unit(W, e));
         }
     }
+#if JX_FLAG_MODE == 1 || JX_FLAG_MODE == 3
+    seen = __ballot(flagacc >= 0.0f);
+#elif JX_FLAG_MODE == 2
+    seen = __ballot(flagany != 0u);
+#endif
     /* some lane has a coefficient inside the guard band (about 40% of the channel-tiles of
      * random data at q90; wave-uniform branch): queue its block-channel */
     if (!JX_DBG_NO_EXACT && seen != 0) {
@@ -775,6 +835,13 @@ int tables_for_current_device()
                         band[q].lim[ch][u][v] = lim[ch][v * 8 + u];
                         band[JX_MAXQ + 1 + q].lim[ch][u][v] = -1.0f;   /* FORCE_EXACT */
                     }
+            for (int ch = 0; ch < 3; ch++)
+                for (int u = 0; u < 8; u++) {
+                    float m = band[q].lim[ch][u][0];
+                    for (int v = 1; v < 8; v++) m = std::min(m, band[q].lim[ch][u][v]);
+                    band[q].limcol[ch][u] = m;
+                    band[JX_MAXQ + 1 + q].limcol[ch][u] = -1.0f;
+                }
         }
         g_tab_rc[dev] = hip_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_qtab), host.data(),
                                                  host.size() * sizeof(jx_qtab)));
@@ -800,6 +867,9 @@ int resident_waves()
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_xform, JX_WG, 0) != hipSuccess ||
             per_cu < 1)
             per_cu = 2;
+#ifdef JX_DBG_GRID_WGS_PER_CU   /* timing experiments: fewer resident workgroups per CU */
+        per_cu = std::min(per_cu, JX_DBG_GRID_WGS_PER_CU);
+#endif
         g_resident_waves[dev] = cus * per_cu * (JX_WG / 64);
     });
     return g_resident_waves[dev];
