@@ -84,6 +84,11 @@ constexpr float kMagic = 12582912.0f; /* 1.5 * 2^23: x + kMagic rounds x to an i
 #ifndef JX_QUEUE_ITEMS
 #define JX_QUEUE_ITEMS 128
 #endif
+#ifndef JX_FUSED_FIX    /* k_xform runs the exact pass itself, 8 queued blocks at a time: 1 after its
+                           last tile, 2 also at each tile start, under the pixel loads;
+                           0: a second kernel (k_fix) does it */
+#define JX_FUSED_FIX 1
+#endif
 /* per-wave, per-channel queue of blocks with a coefficient inside the guard band */
 constexpr int kItems = JX_QUEUE_ITEMS;
 static_assert(kItems >= 64, "a tile adds at most 64 items per channel");
@@ -510,6 +515,7 @@ __device__ __forceinline__ uint64_t flagged_coefs(uint32_t (&raw)[8][6], int qua
     return flagged;
 }
 
+#if !JX_FUSED_FIX
 /* Move the wave's queued blocks of channel ch to its region of the launch's lists and empty
  * the queue.  Wave-uniform; `wave` = the k_xform wave index, `done` = items already moved. */
 __device__ __forceinline__ void flush_queue(WaveLds &W, Queue &Q, int ch, const jx_fixlist &fx,
@@ -521,6 +527,218 @@ __device__ __forceinline__ void flush_queue(WaveLds &W, Queue &Q, int ch, const 
     Q.done[ch] += n;
     Q.n[ch] = 0;
 }
+#endif
+
+#ifndef JX_FIX_PAR      /* 1: eight lanes per block and per exact coefficient (see fix_chunk8) */
+#define JX_FIX_PAR 1
+#endif
+#ifndef JX_FIX_GROUP
+#define JX_FIX_GROUP (JX_FIX_PAR ? 2 : 8)
+#endif
+constexpr unsigned kFixGroup = JX_FIX_GROUP;
+constexpr int kFixTasks = 64 * 64;             /* FORCE_EXACT: every coefficient of 64 blocks */
+
+/* exact_coef's last step: F(u,v) = 1/4 a(u) a(v) s (dct.c:54), round(F / Q) (quantise.c:58) */
+__device__ __forceinline__ int16_t exact_finish(double s, int u, int v, int q)
+{
+    const double F = 0.25 * (u == 0 ? kAlpha0 : 1.0) * (v == 0 ? kAlpha0 : 1.0) * s;
+    return (int16_t)(int)round(F / (double)q);
+}
+
+/* pixel row y of block bi of frame f, with load_block's addressing (x0 = -8 quirk) */
+__device__ __forceinline__ void load_row(const jx_geom &g, unsigned f, unsigned bi, unsigned y,
+                                         uint32_t (&row)[6])
+{
+    const unsigned r = bi / (unsigned)g.bpr, c = bi - r * (unsigned)g.bpr;
+    const bool last = c == (unsigned)g.bpr - 1;
+    if (last && y == 0 && g.row0 + (int)r == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) row[k] = g.under[k];
+        return;
+    }
+    const long long pr = 8ll * r - (last ? 1 : 0) + y;
+    const uint8_t *p = g.rgb + (long long)f * g.in_fstride + pr * g.in_pitch + 24ll * c;
+    p = (const uint8_t *)__builtin_assume_aligned(p, 8);
+    u32x4 a;
+    u32x2 b;
+    __builtin_memcpy(&a, p, 16);
+    __builtin_memcpy(&b, p + 16, 8);
+    row[0] = a.x; row[1] = a.y; row[2] = a.z; row[3] = a.w;
+    row[4] = b.x; row[5] = b.y;
+}
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* LDS of one k_fix wave, 8 blocks at a time */
+struct FixLds8 {
+    uint32_t px[8][8][6];                      /* [block][row] pixel rows                    */
+    union {
+        float T[64 * 9];                       /* (A) row-DCT outputs, (block*8 + row)*9 + u */
+        double prod[8][8][8];                  /* (B) [task slot][x][y] terms of exact sums  */
+    };
+    uint32_t blk[8];                           /* launch-global block indices                */
+    uint8_t bch[8];                            /* and their channels                         */
+    uint16_t task[8 * 64];                     /* block << 6 | natural coefficient index     */
+};
+
+/* jx_pixel for a per-lane channel (all three formed, one kept: same fp32 operations) */
+__device__ __forceinline__ float pixel_rt(int ch, float r, float g, float b)
+{
+    const float y = jx_pixel<FOps, 0>(r, g, b), cb = jx_pixel<FOps, 1>(r, g, b),
+                cr = jx_pixel<FOps, 2>(r, g, b);
+    return ch == 0 ? y : (ch == 1 ? cb : cr);
+}
+
+/*
+ * Exact pass over up to 8 blocks, eight lanes each (lane = block << 3 | j):
+ * (A) lane j loads pixel row j, parks it in LDS and runs the fp32 row transform; then lane j
+ *     runs column j (the same FOps code as k_xform, so the same coefficients come out inside
+ *     the guard band) and tests its 8 coefficients;
+ * (B) eight flagged coefficients at a time, eight lanes each: lane x forms the 8 terms
+ *     (X(x,y) c_u[x]) c_v[y] of its column in fp64, then one lane sums the 64 terms in the
+ *     reference's x-outer / y-inner order (dct.c:46-50) -- the same additions in the same
+ *     order as exact_sum, spread so that the products run in parallel.
+ */
+__device__ __forceinline__ void fix_chunk8(FixLds8 &L, const jx_xform_args &a, unsigned b, int ch,
+                                           bool has, unsigned lane)
+{
+    const jx_geom &g = a.g;
+    const unsigned nb = (unsigned)g.nb;
+    const unsigned i = lane >> 3, j = lane & 7u;
+    const jx_qtab &tab = g_qtab[a.quality];
+    const jx_limtab &band = g_lim[a.force_exact ? 1 : 0][a.quality];
+    if (has) {                                             /* (A) rows */
+        const unsigned f = b / nb;
+        uint32_t row[6];
+        load_row(g, f, b - f * nb, j, row);
+#pragma unroll
+        for (int k = 0; k < 6; k++) L.px[i][j][k] = row[k];
+        if (j == 0) {
+            L.blk[i] = b;
+            L.bch[i] = (uint8_t)ch;
+        }
+        float px[8], T[8];
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+            const float r = (float)byte_of(row, 3 * x);
+            const float gg = (float)byte_of(row, 3 * x + 1);
+            const float bb = (float)byte_of(row, 3 * x + 2);
+            px[x] = pixel_rt(ch, r, gg, bb);
+        }
+        jx_fdct8<FOps>(px, T);
+#pragma unroll
+        for (int u = 0; u < 8; u++) L.T[(i * 8 + j) * 9 + u] = T[u];
+    }
+    wave_sync_lds();
+    unsigned flags = 0;                                    /* bit v: coefficient (u = j, v) */
+    if (has) {                                             /* (A) column u = j */
+        float col[8], F[8];
+#pragma unroll
+        for (int y = 0; y < 8; y++) col[y] = L.T[(i * 8 + y) * 9 + j];
+        jx_fdct8<FOps>(col, F);
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            float tm, d;
+            quant_coef(F[v], tab.w[ch][j][v], tm, d);
+#ifdef JX_DBG_FIX_NO_DETECT             /* timing experiments only (NOT exact) */
+            (void)band;
+            if (v == 0 && ((__float_as_uint(d) >> 7) & 7u) == j) flags |= 1u;
+#else
+            if (__builtin_fabsf(d) >= band.lim[ch][j][v]) flags |= 1u << v;
+#endif
+        }
+    }
+    /* exclusive prefix of the per-lane task counts -> task list */
+    const unsigned n = (unsigned)__popc(flags);
+    unsigned incl = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned o = __shfl_up(incl, d, 64);
+        if ((int)lane >= d) incl += o;
+    }
+    const unsigned total = __builtin_amdgcn_readlane(incl, 63);
+    unsigned pos = incl - n;
+    while (flags) {
+        const unsigned v = (unsigned)__builtin_ctz(flags);
+        flags &= flags - 1;
+        L.task[pos++] = (uint16_t)(i << 6 | v << 3 | j);
+    }
+    wave_sync_lds();
+    const unsigned x = j;
+    /* in k_xform (JX_FUSED_FIX) the blocks' tile stores came from other lanes: they must
+     * have landed before the exact values are written over them */
+    if (total) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (unsigned t0 = 0; t0 < total; t0 += 8) {           /* (B) */
+        const unsigned t = t0 + i;
+        const bool live = t < total;
+        const unsigned tk = live ? L.task[t] : 0u, src = tk >> 6, k = tk & 63u;
+        const int u = (int)(k & 7u), v = (int)(k >> 3);
+        const int tch = live ? (int)L.bch[src] : 0;
+        if (live) {
+            const double cu = kCos[u][x];
+            const int k0 = (int)(3 * x) >> 2, sh = (int)(3 * x) & 3;
+#pragma unroll
+            for (int y = 0; y < 8; y++) {
+                /* the 3 bytes of pixel x: dwords k0 and k0+1 (k0 + 1 <= 5) */
+                const uint64_t w = (uint64_t)L.px[src][y][k0] |
+                                   ((uint64_t)L.px[src][y][k0 + 1 < 6 ? k0 + 1 : 5] << 32);
+                const uint32_t p3 = (uint32_t)(w >> (8 * sh));
+                const int r = (int)(p3 & 0xffu), gg = (int)((p3 >> 8) & 0xffu),
+                          bb = (int)((p3 >> 16) & 0xffu);
+                L.prod[i][x][y] = exact_pixel(tch, r, gg, bb) * cu * kCos[v][y];
+            }
+        }
+        wave_sync_lds();
+        if (live && x == 0) {
+            double s = 0.0;
+#pragma unroll
+            for (int xx = 0; xx < 8; xx++)
+#pragma unroll
+                for (int y = 0; y < 8; y++) s += L.prod[i][xx][y];
+#ifdef JX_DBG_FIX_NO_EXACT             /* timing experiments only (NOT exact) */
+            *coef_ptr(g, L.blk[src], tch, zz_of_rt(v, u)) = (int16_t)s;
+#else
+            *coef_ptr(g, L.blk[src], tch, zz_of_rt(v, u)) =
+                exact_finish(s, u, v, tab.q[tch == 0 ? 0 : 1][u * 8 + v]);
+#endif
+        }
+        wave_sync_lds();                                   /* prod reused */
+    }
+}
+
+static_assert(sizeof(FixLds8) <= sizeof(WaveLds::stage), "FixLds8 lives in the staging area");
+#if JX_FUSED_FIX
+
+/* Exact pass of up to 8 queued blocks, taken from the tails of the three channel queues in
+ * turn, inside k_xform (the staging area is free between tiles; fix_chunk8 waits for the
+ * wave's tile stores before it writes). */
+__device__ __forceinline__ void fix_queued(WaveLds &W, int (&n)[3], const jx_xform_args &a,
+                                        unsigned lane)
+{
+    const int k0 = std::min(n[0], 8), k1 = std::min(n[1], 8 - k0),
+              k2 = std::min(n[2], 8 - k0 - k1);
+    const int i = (int)(lane >> 3);
+    int ch = 2, at = n[2] - k2 + (i - k0 - k1);
+    if (i < k0) {
+        ch = 0;
+        at = n[0] - k0 + i;
+    } else if (i < k0 + k1) {
+        ch = 1;
+        at = n[1] - k1 + (i - k0);
+    }
+    const bool has = i < k0 + k1 + k2;
+    const unsigned b = has ? W.item[ch][at] : 0u;
+    n[0] -= k0;
+    n[1] -= k1;
+    n[2] -= k2;
+    fix_chunk8(*reinterpret_cast<FixLds8 *>(W.stage), a, b, ch, has, lane);
+}
+#endif
 
 /* block index of this lane in tile t (clamped into range for the tail tile) */
 [[maybe_unused]] __device__ __forceinline__ unsigned tile_block(unsigned t, unsigned lane,
@@ -578,6 +796,10 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
             load_block(g, f, b - f * nb, raw);
         }
 #endif
+#if JX_FUSED_FIX == 2
+        /* exact pass of earlier tiles' blocks while this tile's pixels are in flight */
+        if (!JX_DBG_NO_EXACT && Q.n[0] + Q.n[1] + Q.n[2] > 0) fix_queued(W, Q.n, a, lane);
+#endif
         float T[8][8];
 #if JX_RELOAD
         const unsigned f = b / nb, bi = b - f * nb;
@@ -615,12 +837,20 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
         xform_cols<2>(T, a, W, Q, active, b, t, lane, none);
         __builtin_amdgcn_sched_barrier(0);
 #endif
+#if JX_FUSED_FIX
+        if (!JX_DBG_NO_EXACT) {
+            /* only when a queue could overflow (rare): the rest waits for the kernel's end */
+            while (Q.n[0] > kItems - 64 || Q.n[1] > kItems - 64 || Q.n[2] > kItems - 64)
+                fix_queued(W, Q.n, a, lane);
+        }
+#else
         /* keep room for the next tile's 64 possible items per channel */
         if (!JX_DBG_NO_EXACT) {
 #pragma unroll
             for (int ch = 0; ch < 3; ch++)
                 if (Q.n[ch] > kItems - 64) flush_queue(W, Q, ch, a.fix, wave, lane);
         }
+#endif
 #if JX_PREFETCH == 1
         if (tn < ntiles) {
 #pragma unroll
@@ -632,6 +862,12 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
         (void)tn;
 #endif
     }
+#if JX_FUSED_FIX
+    if (!JX_DBG_NO_EXACT) {
+        while (Q.n[0] + Q.n[1] + Q.n[2] > 0) fix_queued(W, Q.n, a, lane);
+    }
+    (void)wave;
+#else
     if (!JX_DBG_NO_EXACT) {
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) flush_queue(W, Q, ch, a.fix, wave, lane);
@@ -639,6 +875,7 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
         const unsigned mine = lane == 0 ? Q.done[0] : (lane == 1 ? Q.done[1] : Q.done[2]);
         if (lane < 3) a.fix.count[lane * a.fix.nwaves + wave] = mine;
     }
+#endif
 }
 
 /*
@@ -647,12 +884,6 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
  * a time: (A) one lane per block reloads its pixels, re-finds its flagged coefficients and
  * parks the pixels in LDS; (B) one lane per flagged coefficient recomputes it exactly.
  */
-#ifndef JX_FIX_GROUP
-#define JX_FIX_GROUP 8
-#endif
-constexpr unsigned kFixGroup = JX_FIX_GROUP;
-constexpr int kFixTasks = 64 * 64;             /* FORCE_EXACT: every coefficient of 64 blocks */
-
 struct FixLds {
     u32x4 px[64][12];                          /* pixel rows of the chunk's blocks           */
     uint32_t blk[64];                          /* their launch-global block indices          */
@@ -726,6 +957,46 @@ __device__ __forceinline__ void fix_chunk(FixLds &L, const jx_xform_args &a, uns
     __builtin_amdgcn_wave_barrier();                       /* LDS reused by the next chunk */
 }
 
+#if !JX_FUSED_FIX
+#if JX_FIX_PAR
+__global__ __launch_bounds__(256) void k_fix(const jx_xform_args a)
+{
+    __shared__ FixLds8 s_fix[4];
+    const jx_fixlist &fx = a.fix;
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned groups = (fx.nwaves + kFixGroup - 1) / kFixGroup;
+    const unsigned job = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (job >= 3 * groups) return;
+    FixLds8 &L = s_fix[threadIdx.x >> 6];
+    const int ch = (int)(job / groups);
+    const unsigned w0 = (job - ch * groups) * kFixGroup;
+    unsigned cnt = 0;
+    if (lane < kFixGroup && w0 + lane < fx.nwaves) cnt = fx.count[ch * fx.nwaves + w0 + lane];
+    unsigned incl[kFixGroup];
+    unsigned run = 0;
+#pragma unroll
+    for (unsigned s = 0; s < kFixGroup; s++) {
+        run += __builtin_amdgcn_readlane(cnt, s);
+        incl[s] = run;
+    }
+    for (unsigned c0 = 0; c0 < run; c0 += 8) {
+        const unsigned idx = c0 + (lane >> 3);
+        const bool has = idx < run;
+        unsigned b = 0;
+        if (has) {
+            unsigned s = 0, excl = 0;
+#pragma unroll
+            for (unsigned k = 0; k < kFixGroup; k++)
+                if (incl[k] <= idx) {
+                    s = k + 1;
+                    excl = incl[k];
+                }
+            b = fx.items[((size_t)ch * fx.nwaves + w0 + s) * fx.capw + (idx - excl)];
+        }
+        fix_chunk8(L, a, b, ch, has, lane);
+    }
+}
+#else
 __global__ __launch_bounds__(256) void k_fix(const jx_xform_args a)
 {
     __shared__ FixLds s_fix[4];
@@ -766,6 +1037,8 @@ __global__ __launch_bounds__(256) void k_fix(const jx_xform_args a)
         else fix_chunk<2>(L, a, b, has, lane);
     }
 }
+#endif
+#endif  /* !JX_FUSED_FIX */
 
 __device__ __forceinline__ uint8_t splitmix_byte(uint64_t seed, uint64_t k)
 {
@@ -973,7 +1246,7 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     /* exact pass: one wave per channel and group of kFixGroup k_xform waves */
     const size_t jobs = 3 * ((nwaves + kFixGroup - 1) / kFixGroup);
     const unsigned fgrid = (unsigned)((jobs + 3) / 4);
-#ifndef JX_DBG_HOST_NO_FIX        /* timing experiments only (NOT exact when set) */
+#if !defined(JX_DBG_HOST_NO_FIX) && !JX_FUSED_FIX   /* (HOST_NO_FIX: timing only, NOT exact) */
     if (!JX_DBG_NO_EXACT) hipLaunchKernelGGL(k_fix, dim3(fgrid), dim3(256), 0, s, xa);
 #else
     (void)fgrid;
