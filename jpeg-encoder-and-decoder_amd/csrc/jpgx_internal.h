@@ -32,6 +32,8 @@ struct jx_qtab {
     float w[3][8][8];       /* [ch][u][v]: fp32 scale of coefficient (u,v), 1/Q folded    */
     int16_t q[2][64];       /* scaled tables, q[t][u*8+v] = Qs[u][v] as the reference
                                indexes them (src/quantise.c:58)                           */
+    float wp[3][4][8][2];   /* packed path: [ch][j][v] = (w(u0,v), w(u1,v)) for the column
+                               pair j = (u0,u1) = (0,4), (2,6), (1,3), (5,7) (jx_pk_k)    */
 };
 
 /* guard band: |t - rint(t)| >= lim -> exact path.  [0] = rigorous band, [1] = FORCE_EXACT
@@ -39,6 +41,8 @@ struct jx_qtab {
 struct jx_limtab {
     float lim[3][8][8];     /* [ch][u][v] */
     float limcol[3][8];     /* [ch][u]: min over v (one limit per column, JX_FLAG_MODE 3)  */
+    float lsq[3][4][8][2];  /* packed path: a float <= lim^2 (or -1 where lim < 0), pair
+                               order as jx_qtab.wp: flag when d*d - lsq >= 0                */
 };
 
 #define JX_MAXQ 97
@@ -67,6 +71,8 @@ extern "C" {
 /* host plan (jpgx_plan.cpp) */
 int jx_plan_tables(int quality, float w[3][64], float lim[3][64], int16_t q[2][64]);
 void jx_under_dwords(const uint8_t under[3][8], uint32_t out[6]);
+/* packed-pair vs scalar transform, bit for bit (host; returns the mismatch count) */
+long long jx_selftest_pk(long long nblocks, unsigned long long seed);
 #ifdef __cplusplus
 }
 #endif

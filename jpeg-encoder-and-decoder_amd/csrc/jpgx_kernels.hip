@@ -341,6 +341,43 @@ struct Queue {
     unsigned done[3];       /* items already moved to the wave's global region            */
 };
 
+/* The staged channel CH of tile t leaves as coalesced stores; lanes in `seen` (a coefficient
+ * of this channel inside the guard band) queue their block-channel for the exact pass. */
+template <int CH>
+__device__ __forceinline__ void store_and_queue(const jx_xform_args &a, WaveLds &W, Queue &Q,
+                                                bool active, unsigned b, unsigned t,
+                                                unsigned lane, uint64_t seen)
+{
+    const jx_geom &g = a.g;
+    /* coalesced store: the wave's 64 blocks x 128 B of this channel, 1 KiB per instruction */
+    const unsigned nb = (unsigned)g.nb, total = nb * (unsigned)g.nframes;
+    const unsigned b0 = t * 64u;
+    const unsigned f0 = b0 / nb, bl = std::min(b0 + 63u, total - 1u), fl = bl / nb;
+    if (f0 == fl && b0 + 63u < total) {
+        u32x4 *dst = (u32x4 *)(g.out + (long long)f0 * g.out_fstride +
+                               ((long long)CH * nb + (b0 - f0 * nb)) * 64);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const unsigned e = (unsigned)j * 64u + lane;
+            jx_store(dst + e, stage_unit(W, e));
+        }
+    } else {                                   /* tile crosses a frame end or the last tile */
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const unsigned e = (unsigned)j * 64u + lane, bb = b0 + (e >> 3);
+            if (bb < total)
+                jx_store((u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8), stage_unit(W, e));
+        }
+    }
+    /* some lane has a coefficient inside the guard band (about 40% of the channel-tiles of
+     * random data at q90; wave-uniform branch): queue its block-channel */
+    if (!JX_DBG_NO_EXACT && seen != 0) {
+        const uint64_t M = seen & __ballot(active);
+        if ((M >> lane) & 1u) W.item[CH][Q.n[CH] + lane_rank(M)] = b;
+        Q.n[CH] += __popcll(M);
+    }
+}
+
 /* Column pass, quantisation, zig-zag, LDS staging + coalesced store of channel CH; block-
  * channels with a coefficient inside the guard band are queued for the exact path. */
 template <int CH, class Pre>
@@ -348,7 +385,6 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
                                            Queue &Q, bool active, unsigned b, unsigned t,
                                            unsigned lane, Pre &&pre)
 {
-    const jx_geom &g = a.g;
 #if !JX_STAGE16
     uint32_t bits[64];     /* tm bit patterns by zig-zag index; low 16 bits = the int16    */
     uint32_t packed[32];   /* zig-zag pairs (2k, 2k+1) as one dword, formed when complete */
@@ -450,38 +486,136 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
 #ifdef JX_DBG_NO_STAGE
     W.stage[lane] = dbg_acc;
 #endif
-    /* coalesced store: the wave's 64 blocks x 128 B of this channel, 1 KiB per instruction */
-    const unsigned nb = (unsigned)g.nb, total = nb * (unsigned)g.nframes;
-    const unsigned b0 = t * 64u;
-    const unsigned f0 = b0 / nb, bl = std::min(b0 + 63u, total - 1u), fl = bl / nb;
-    if (f0 == fl && b0 + 63u < total) {
-        u32x4 *dst = (u32x4 *)(g.out + (long long)f0 * g.out_fstride +
-                               ((long long)CH * nb + (b0 - f0 * nb)) * 64);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const unsigned e = (unsigned)j * 64u + lane;
-            jx_store(dst + e, stage_unit(W, e));
-        }
-    } else {                                   /* tile crosses a frame end or the last tile */
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const unsigned e = (unsigned)j * 64u + lane, bb = b0 + (e >> 3);
-            if (bb < total)
-                jx_store((u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8), stage_unit(W, e));
-        }
-    }
 #if JX_FLAG_MODE == 1 || JX_FLAG_MODE == 3
     seen = __ballot(flagacc >= 0.0f);
 #elif JX_FLAG_MODE == 2
     seen = __ballot(flagany != 0u);
 #endif
-    /* some lane has a coefficient inside the guard band (about 40% of the channel-tiles of
-     * random data at q90; wave-uniform branch): queue its block-channel */
-    if (!JX_DBG_NO_EXACT && seen != 0) {
-        const uint64_t M = seen & __ballot(active);
-        if ((M >> lane) & 1u) W.item[CH][Q.n[CH] + lane_rank(M)] = b;
-        Q.n[CH] += __popcll(M);
+    store_and_queue<CH>(a, W, Q, active, b, t, lane, seen);
+}
+
+/* ---- fast path, packed ------------------------------------------------------------------
+ * The same fp32 operations as xform_rows / xform_cols, two per v_pk_*_f32 instruction
+ * (xform_math.h, checked bit for bit against the scalar code by jx_selftest_pk):
+ *   rows:    pixel pairs (x, x+1); jx_fdct8_pk splits each row DCT over the pair's two lanes
+ *            and leaves the row's coefficients in the pairs (0,4) (2,6) (1,3) (5,7);
+ *   columns: each such pair of columns runs jx_fdct8 in lock-step, one column per lane;
+ *   quantiser and guard band per coefficient pair, the band test as d*d - lsq >= 0 (lsq <=
+ *   lim^2) folded into one running max per lane: no per-coefficient compare or scalar op.
+ */
+#ifndef JX_PACKED
+#define JX_PACKED 0
+#endif
+#ifndef JX_PK_ROWS
+#define JX_PK_ROWS 2
+#endif
+#ifndef JX_Q_SB          /* scheduling fences between the quantiser stages (packed path) */
+#define JX_Q_SB 1
+#endif
+#if JX_Q_SB
+#define JX_SB_Q() __builtin_amdgcn_sched_barrier(0)
+#else
+#define JX_SB_Q() ((void)0)
+#endif
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+struct DevPair {
+    typedef f2 V;
+    static __host__ __device__ __forceinline__ V mk(float a, float b) { return V{a, b}; }
+    static __host__ __device__ __forceinline__ float lo(V a) { return a.x; }
+    static __host__ __device__ __forceinline__ float hi(V a) { return a.y; }
+    static __host__ __device__ __forceinline__ V add(V a, V b) { return a + b; }
+    static __host__ __device__ __forceinline__ V sub(V a, V b) { return a - b; }
+    static __host__ __device__ __forceinline__ V mul(V a, V b) { return a * b; }
+    static __host__ __device__ __forceinline__ V fma(V a, V b, V c)
+    {
+        return __builtin_elementwise_fma(a, b, c);
     }
+};
+typedef PairOps<DevPair> DevPO;
+
+/* Row pass of channel CH, packed: T[y][j] = row y's coefficient pair j (jx_pk_k order). */
+template <int CH>
+__device__ __forceinline__ void xform_rows_pk(uint32_t (&raw)[8][6], f2 (&T)[8][4])
+{
+#pragma unroll
+    for (int y = 0; y < 8; y++)
+#pragma unroll
+        for (int k = 0; k < 6; k++) asm volatile("" : "+v"(raw[y][k]));
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+        if (y % JX_PK_ROWS == 0) JX_SB_ROW();   /* JX_PK_ROWS rows interleave (hides the
+                                                   dependent-issue gaps of one row's chain) */
+        f2 px[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int x0 = 6 * k, x1 = 6 * k + 3;      /* byte offsets of pixels 2k, 2k+1 */
+            const f2 r = f2{(float)byte_of(raw[y], x0), (float)byte_of(raw[y], x1)};
+            const f2 gg = f2{(float)byte_of(raw[y], x0 + 1), (float)byte_of(raw[y], x1 + 1)};
+            const f2 bb = f2{(float)byte_of(raw[y], x0 + 2), (float)byte_of(raw[y], x1 + 2)};
+            px[k] = jx_pixel<DevPO, CH>(r, gg, bb);
+        }
+        jx_fdct8_pk<DevPair>(px, T[y]);
+    }
+}
+
+/* Column pass, quantisation, guard band, zig-zag staging of channel CH, packed.  Each column
+ * pair's eight coefficient pairs go through the quantiser stage by stage (eight independent
+ * packed operations per stage: no dependent back-to-back pairs, which would cost wait states),
+ * and the band test reduces through a max3 tree. */
+template <int CH>
+__device__ __forceinline__ void xform_cols_pk(f2 (&T)[8][4], const jx_xform_args &a, WaveLds &W,
+                                              Queue &Q, bool active, unsigned b, unsigned t,
+                                              unsigned lane)
+{
+    const jx_qtab &tab = g_qtab[a.quality];
+    const jx_limtab &band = g_lim[a.force_exact ? 1 : 0][a.quality];
+    const f2 M2 = f2{kMagic, kMagic};
+    float acc = -1.0f;                   /* max over the channel of d*d - lsq (>= 0: flagged) */
+    uint16_t *st = (uint16_t *)W.stage + lane * 66;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        f2 col[8], F[8], tm[8], rr[8], d[8];
+#pragma unroll
+        for (int y = 0; y < 8; y++) col[y] = T[y][j];
+        jx_fdct8<DevPO>(col, F);
+        JX_SB_Q();
+#pragma unroll
+        for (int v = 0; v < 8; v++)
+            tm[v] = DevPair::fma(F[v], f2{tab.wp[CH][j][v][0], tab.wp[CH][j][v][1]}, M2);
+        JX_SB_Q();
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            st[zz_of(v, jx_pk_k(j, 0))] = (uint16_t)__float_as_uint(tm[v].x);
+            st[zz_of(v, jx_pk_k(j, 1))] = (uint16_t)__float_as_uint(tm[v].y);
+        }
+        if (!JX_DBG_NO_EXACT) {
+#pragma unroll
+            for (int v = 0; v < 8; v++) rr[v] = tm[v] - M2;
+            JX_SB_Q();
+#pragma unroll
+            for (int v = 0; v < 8; v++)
+                d[v] = DevPair::fma(F[v], f2{tab.wp[CH][j][v][0], tab.wp[CH][j][v][1]}, -rr[v]);
+            JX_SB_Q();
+#pragma unroll
+            for (int v = 0; v < 8; v++)
+                d[v] = DevPair::fma(d[v], d[v], -f2{band.lsq[CH][j][v][0], band.lsq[CH][j][v][1]});
+            JX_SB_Q();
+            /* 16 values + acc through 8 max3: el(i) = element i of d[0].x, d[0].y, d[1].x, ... */
+            const auto el = [&](int i) { return (i & 1) ? d[i >> 1].y : d[i >> 1].x; };
+            const auto mx3 = [](float x, float y, float z) {
+                return __builtin_fmaxf(__builtin_fmaxf(x, y), z);
+            };
+            const float m0 = mx3(acc, el(0), el(1)), m1 = mx3(el(2), el(3), el(4));
+            const float m2 = mx3(el(5), el(6), el(7)), m3 = mx3(el(8), el(9), el(10));
+            const float m4 = mx3(el(11), el(12), el(13)), m5 = __builtin_fmaxf(el(14), el(15));
+            acc = __builtin_fmaxf(mx3(m0, m1, m2), mx3(m3, m4, m5));
+        }
+        JX_SB_COL();
+    }
+    const uint64_t seen = JX_DBG_NO_EXACT ? 0ull : __ballot(acc >= 0.0f);
+    store_and_queue<CH>(a, W, Q, active, b, t, lane, seen);
 }
 
 /* ---- exact path -------------------------------------------------------------------------- */
@@ -819,6 +953,24 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
         xform_rows<2>(raw, T);
         xform_cols<2>(T, a, W, Q, active, b, t, lane, next);
         __builtin_amdgcn_sched_barrier(0);
+#elif JX_PACKED
+        f2 TP[8][4];
+        (void)T;
+        xform_rows_pk<0>(raw, TP);
+        xform_cols_pk<0>(TP, a, W, Q, active, b, t, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        xform_rows_pk<1>(raw, TP);
+        xform_cols_pk<1>(TP, a, W, Q, active, b, t, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        xform_rows_pk<2>(raw, TP);
+#if JX_PREFETCH == 2
+        if (tn < ntiles) {                          /* raw is dead: refill it for tile tn */
+            const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
+            load_block(g, fn, bn - fn * nb, raw);
+        }
+#endif
+        xform_cols_pk<2>(TP, a, W, Q, active, b, t, lane);
+        __builtin_amdgcn_sched_barrier(0);
 #else
         const auto none = []() {};
         xform_rows<0>(raw, T);
@@ -1115,6 +1267,23 @@ int tables_for_current_device()
                     band[q].limcol[ch][u] = m;
                     band[JX_MAXQ + 1 + q].limcol[ch][u] = -1.0f;
                 }
+            /* packed path: pair order, squared limits rounded down (d*d >= lsq is implied by
+             * |d| >= lim, so every coefficient the band flags is still flagged) */
+            for (int ch = 0; ch < 3; ch++)
+                for (int j = 0; j < 4; j++)
+                    for (int v = 0; v < 8; v++)
+                        for (int l = 0; l < 2; l++) {
+                            const int u = jx_pk_k(j, l);
+                            host[q].wp[ch][j][v][l] = w[ch][v * 8 + u];
+                            const double lm = (double)band[q].lim[ch][u][v];
+                            float s = -1.0f;
+                            if (lm > 0) {
+                                s = (float)(lm * lm);
+                                if ((double)s > lm * lm) s = nextafterf(s, 0.0f);
+                            }
+                            band[q].lsq[ch][j][v][l] = s;
+                            band[JX_MAXQ + 1 + q].lsq[ch][j][v][l] = -1.0f;
+                        }
         }
         g_tab_rc[dev] = hip_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_qtab), host.data(),
                                                  host.size() * sizeof(jx_qtab)));

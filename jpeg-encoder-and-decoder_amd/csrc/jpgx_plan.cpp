@@ -228,3 +228,122 @@ void jpgx_stripe(int block_rows, int nshards, int k, int *row_begin, int *row_en
 const char *jpgx_version(void) { return "jpgx 0.1 (gfx950)"; }
 
 }  /* extern "C" */
+
+/* ---- packed-pair equivalence (host) --------------------------------------------------------
+ * The kernel's packed path (xform_math.h: PairOps, jx_fdct8_pk) must produce, lane by lane, the
+ * very fp32 values of the scalar FOps code the guard band was derived for.  HostPair evaluates
+ * the packed code with one correctly rounded scalar operation per lane, as v_pk_* does. */
+namespace {
+struct HF2 {
+    float x, y;
+};
+struct HostPair {
+    typedef HF2 V;
+    static V mk(float a, float b) { return V{a, b}; }
+    static float lo(V a) { return a.x; }
+    static float hi(V a) { return a.y; }
+    static V add(V a, V b) { return V{a.x + b.x, a.y + b.y}; }
+    static V sub(V a, V b) { return V{a.x - b.x, a.y - b.y}; }
+    static V mul(V a, V b) { return V{a.x * b.x, a.y * b.y}; }
+    static V fma(V a, V b, V c) { return V{fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)}; }
+};
+
+inline uint32_t bits(float f)
+{
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+
+uint64_t sm64(uint64_t &s)
+{
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* one block-channel both ways: scalar rows/cols (the bound's code) vs the kernel's packed
+ * order (rows: jx_fdct8_pk on pixel pairs; columns: jx_fdct8 over PairOps on column pairs) */
+template <int CH>
+long long block_mismatch(const uint8_t px[8][8][3], const float w[64])
+{
+    typedef PairOps<HostPair> PO;
+    float T[8][8], Fs[8][8];
+    for (int y = 0; y < 8; y++) {
+        float in[8];
+        for (int x = 0; x < 8; x++)
+            in[x] = jx_pixel<FOps, CH>((float)px[y][x][0], (float)px[y][x][1], (float)px[y][x][2]);
+        jx_fdct8<FOps>(in, T[y]);
+    }
+    for (int u = 0; u < 8; u++) {
+        float col[8], out[8];
+        for (int y = 0; y < 8; y++) col[y] = T[y][u];
+        jx_fdct8<FOps>(col, out);
+        for (int v = 0; v < 8; v++) Fs[v][u] = out[v];
+    }
+    HF2 Tp[8][4];
+    for (int y = 0; y < 8; y++) {
+        HF2 in[4];
+        for (int k = 0; k < 4; k++) {
+            const HF2 r{(float)px[y][2 * k][0], (float)px[y][2 * k + 1][0]};
+            const HF2 g{(float)px[y][2 * k][1], (float)px[y][2 * k + 1][1]};
+            const HF2 b{(float)px[y][2 * k][2], (float)px[y][2 * k + 1][2]};
+            in[k] = jx_pixel<PO, CH>(r, g, b);
+        }
+        jx_fdct8_pk<HostPair>(in, Tp[y]);
+    }
+    long long bad = 0;
+    const float magic = 12582912.0f;
+    for (int j = 0; j < 4; j++) {
+        HF2 col[8], out[8];
+        for (int y = 0; y < 8; y++) col[y] = Tp[y][j];
+        jx_fdct8<PO>(col, out);
+        for (int v = 0; v < 8; v++)
+            for (int l = 0; l < 2; l++) {
+                const int u = jx_pk_k(j, l);
+                const float Fp = l ? out[v].y : out[v].x;
+                if (bits(Fp) != bits(Fs[v][u])) bad++;
+                /* quantiser: tm = fma(F,w,M), d = fma(F,w,-(tm-M)) in both forms */
+                const float ww = w[v * 8 + u];
+                const HF2 Fw = HostPair::mk(Fp, Fp), W = HostPair::mk(ww, ww);
+                const HF2 tm = HostPair::fma(Fw, W, HostPair::mk(magic, magic));
+                const HF2 rr = HostPair::sub(tm, HostPair::mk(magic, magic));
+                const HF2 d = HostPair::fma(Fw, W, HostPair::mk(-rr.x, -rr.y));
+                const float tms = fmaf(Fs[v][u], ww, magic), ds = fmaf(Fs[v][u], ww, -(tms - magic));
+                if (bits(tm.x) != bits(tms) || bits(d.x) != bits(ds)) bad++;
+            }
+    }
+    return bad;
+}
+}  // namespace
+
+extern "C" long long jx_selftest_pk(long long nblocks, unsigned long long seed)
+{
+    float w[3][64], lim[3][64];
+    int16_t q[2][64];
+    jx_plan_tables(90, w, lim, q);
+    uint64_t s = seed;
+    long long bad = 0;
+    uint8_t px[8][8][3];
+    for (long long n = 0; n < nblocks; n++) {
+        const int kind = (int)(n % 4);  /* random, flat, two-level, ramps */
+        const uint64_t r0 = sm64(s);
+        for (int y = 0; y < 8; y++)
+            for (int x = 0; x < 8; x++)
+                for (int c = 0; c < 3; c++) {
+                    uint8_t v;
+                    if (kind == 0) v = (uint8_t)(sm64(s) >> 56);
+                    else if (kind == 1) v = (uint8_t)(r0 >> (8 * c));
+                    else if (kind == 2) v = ((r0 >> (x + 8 * y)) & 1) ? 255 : (uint8_t)(r0 >> 40);
+                    else v = (uint8_t)((x * (int)(r0 & 31) + y * (int)((r0 >> 5) & 31) + c * 7) & 255);
+                    px[y][x][c] = v;
+                }
+        bad += block_mismatch<0>(px, w[0]) + block_mismatch<1>(px, w[1]) + block_mismatch<2>(px, w[2]);
+    }
+    return bad;
+}
+
+extern "C" {
+
+}  /* extern "C" */

@@ -130,6 +130,68 @@ JX_HD void jx_fdct8(const typename O::T *in, typename O::T *out)
 #if !JX_DCT_AAN
 /* Factor the computed out[k] must be multiplied by to give sum_x in[x] cos((2x+1)k pi/16). */
 JX_HD double jx_dct_kfactor(int k) { return k == 4 ? JX_C4 : 1.0; }
+
+/* ---- packed pairs ------------------------------------------------------------------------
+ * The same fp32 operations, two per instruction (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32 on
+ * gfx950, whose lane-wise results are those of the scalar instructions).  P is a pair policy:
+ *   V           the pair type,  mk(a,b) / lo(v) / hi(v)
+ *   add sub mul fma             lane-wise fp32 operations, one rounding each
+ * Every function below performs, lane by lane, exactly the scalar operation sequence of the
+ * FOps code above, so the guard band bounds (BoundOps over that scalar code) hold unchanged;
+ * jx_selftest_pk (jpgx_plan.cpp) checks the equivalence bit for bit on the host.
+ */
+
+/* O-policy over pairs: two independent instances of the scalar code, one per lane */
+template <class P>
+struct PairOps {
+    typedef typename P::V T;
+    static JX_HD T add(T a, T b) { return P::add(a, b); }
+    static JX_HD T sub(T a, T b) { return P::sub(a, b); }
+    static JX_HD T mulc(T a, jx_const k) { return P::mul(a, P::mk(k.f, k.f)); }
+    static JX_HD T fmac(T a, jx_const k, T b) { return P::fma(a, P::mk(k.f, k.f), b); }
+    static JX_HD T lit(jx_const k) { return P::mk(k.f, k.f); }
+};
+
+/*
+ * One 8-point jx_fdct8 with its work split over the two lanes of every pair: 17 packed
+ * operations instead of 34 scalar ones.  in = (x0,x1),(x2,x3),(x4,x5),(x6,x7); out = the
+ * pairs (out0,out4),(out2,out6),(out1,out3),(out5,out7).  Swapped and broadcast operands
+ * become op_sel modifiers, negated ones neg modifiers (a + (-b) == a - b exactly).
+ */
+template <class P>
+JX_HD void jx_fdct8_pk(const typename P::V *in, typename P::V *out)
+{
+    typedef typename P::V V;
+#define JX_F(c) ((float)(c))
+    const V x76 = P::mk(P::hi(in[3]), P::lo(in[3])), x54 = P::mk(P::hi(in[2]), P::lo(in[2]));
+    const V s01 = P::add(in[0], x76), d01 = P::sub(in[0], x76);   /* (s0,s1), (d0,d1) */
+    const V s23 = P::add(in[1], x54), d23 = P::sub(in[1], x54);   /* (s2,s3), (d2,d3) */
+    const V s32 = P::mk(P::hi(s23), P::lo(s23));
+    const V e01 = P::add(s01, s32), e23 = P::sub(s01, s32);       /* (e0,e1), (e2,e3) */
+    /* (e0+e1, e0-e1) as fma(e1, (1,-1), e0): fma(x, +-1, y) rounds y +- x once, exactly as
+     * the scalar add/sub (a lane-dependent sign has no neg modifier) */
+    out[0] = P::fma(P::mk(P::hi(e01), P::hi(e01)), P::mk(1.0f, -1.0f), P::mk(P::lo(e01), P::lo(e01)));
+    const V e2 = P::mk(P::lo(e23), P::lo(e23)), e3 = P::mk(P::hi(e23), P::hi(e23));
+    out[1] = P::fma(e2, P::mk(JX_F(JX_C2), JX_F(JX_C6)), P::mul(e3, P::mk(JX_F(JX_C6), JX_F(-JX_C2))));
+    const V d0 = P::mk(P::lo(d01), P::lo(d01)), d1 = P::mk(P::hi(d01), P::hi(d01));
+    const V d2 = P::mk(P::lo(d23), P::lo(d23)), d3 = P::mk(P::hi(d23), P::hi(d23));
+    out[2] = P::fma(d0, P::mk(JX_F(JX_C1), JX_F(JX_C3)),
+             P::fma(d1, P::mk(JX_F(JX_C3), JX_F(-JX_C7)),
+             P::fma(d2, P::mk(JX_F(JX_C5), JX_F(-JX_C1)),
+             P::mul(d3, P::mk(JX_F(JX_C7), JX_F(-JX_C5))))));
+    out[3] = P::fma(d0, P::mk(JX_F(JX_C5), JX_F(JX_C7)),
+             P::fma(d1, P::mk(JX_F(-JX_C1), JX_F(-JX_C5)),
+             P::fma(d2, P::mk(JX_F(JX_C7), JX_F(JX_C3)),
+             P::mul(d3, P::mk(JX_F(JX_C3), JX_F(-JX_C1))))));
+#undef JX_F
+}
+
+/* coefficient index k of lane 0 / lane 1 of output pair j of jx_fdct8_pk */
+JX_HD constexpr int jx_pk_k(int j, int lane)
+{
+    return lane == 0 ? (j == 0 ? 0 : j == 1 ? 2 : j == 2 ? 1 : 5)
+                     : (j == 0 ? 4 : j == 1 ? 6 : j == 2 ? 3 : 7);
+}
 #endif
 
 #endif

@@ -109,3 +109,16 @@ def test_workspace_size():
     assert jpgx.workspace_size(jpgx.frames(3840, 2160, nframes=8)) == expect(nb)
     assert jpgx.workspace_size(jpgx.frames(64, 64, rows=(2, 5))) == expect(3 * 8)
     assert jpgx.workspace_size(jpgx.frames(64, 64, rows=(3, 3))) == 0
+
+
+def test_packed_transform_matches_scalar_bit_for_bit():
+    """The packed-pair transform (xform_math.h: jx_fdct8_pk, PairOps) performs, lane by lane,
+    the scalar operation sequence the guard band was derived for: identical fp32 row/column
+    outputs and quantiser values on random, flat, two-level and ramp blocks (host evaluation,
+    jpgx_plan.cpp jx_selftest_pk)."""
+    import ctypes
+    f = jpgx.lib.jx_selftest_pk
+    f.restype = ctypes.c_longlong
+    f.argtypes = [ctypes.c_longlong, ctypes.c_ulonglong]
+    assert f(20000, 1) == 0
+    assert f(20000, 0x9E3779B97F4A7C15) == 0
