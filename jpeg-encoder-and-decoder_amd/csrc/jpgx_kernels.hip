@@ -43,6 +43,9 @@ namespace {
 #ifndef JX_PREFETCH
 #define JX_PREFETCH 0   /* input prefetch mode, see k_xform */
 #endif
+#ifndef JX_CHLOOP       /* 1: the three channels run one rolled copy of the channel body */
+#define JX_CHLOOP 0
+#endif
 #ifndef JX_RELOAD       /* 1: pixels re-read (L2) per channel, issued during the previous
                            column pass: they are not kept in registers across channels */
 #define JX_RELOAD 0
@@ -301,9 +304,70 @@ __device__ __forceinline__ int lane_rank(uint64_t m)
 
 /* ---- fast path --------------------------------------------------------------------------- */
 
+#ifndef JX_MIX           /* 1: colour conversion by v_fma_mix_f32 straight from the bytes */
+#define JX_MIX 0
+#endif
+
+/* The eight pixel values of channel CH (level shift included) of one pixel row (24 bytes).
+ * JX_MIX: each pair of bytes becomes two f16 subnormals b*2^-24 (one v_perm_b32), which
+ * v_fma_mix_f32 multiplies exactly by the f32 constant k*2^24: fma(b*2^-24, k*2^24, c) rounds
+ * b*k + c once, the very value of jx_pixel's fmaf(b, k, c) (the plain product b*k as
+ * fma(., ., -0), also exact with its sign) -- no byte->f32 conversions at all.  Needs f16
+ * denormals (the default kernel mode); the parity tests check every output bit. */
+/* jx_pixel<FOps, CH> for a (uniform) runtime channel: the same fmaf sequence, constants by
+ * select; fma(b, k, -0) is the plain product b*k bit for bit (sign of zero included). */
+__device__ __forceinline__ float pixel_k(const int CH, float r, float g, float b)
+{
+    const float k0 = CH == 0 ? JX_K(0.299).f : (CH == 1 ? JX_K(-0.168736).f : JX_K(0.5).f);
+    const float k1 = CH == 0 ? JX_K(0.587).f : (CH == 1 ? JX_K(0.331264).f : JX_K(-0.418688).f);
+    const float k2 = CH == 0 ? JX_K(0.114).f : (CH == 1 ? JX_K(-0.5).f : JX_K(-0.081312).f);
+    const float k3 = CH == 0 ? JX_K(-128.0).f : -0.0f;
+    return __builtin_fmaf(r, k0, __builtin_fmaf(g, k1, __builtin_fmaf(b, k2, k3)));
+}
+
+__device__ __forceinline__ void row_pixels(const int CH, const uint32_t (&row)[6], float (&px)[8])
+{
+#if JX_MIX
+    uint32_t h[12];                          /* h[k] = bytes 2k, 2k+1 as f16 subnormals */
+#pragma unroll
+    for (int k = 0; k < 12; k++)
+        h[k] = __builtin_amdgcn_perm(row[k >> 1], row[k >> 1], (k & 1) ? 0x0c070c06u : 0x0c050c04u);
+    const auto in = [&](int i) {              /* byte i of the row, times 2^-24 */
+        const uint32_t w = h[i >> 1];
+        const uint16_t b16 = (i & 1) ? (uint16_t)(w >> 16) : (uint16_t)w;
+        return (float)__builtin_bit_cast(_Float16, b16);
+    };
+    constexpr float S = 16777216.0f;
+    float nz = -0.0f;                      /* opaque: fma(x, y, -0) must not become a mul */
+    asm volatile("" : "+v"(nz));
+#define JX_KS(v) (JX_K(v).f * S)
+#pragma unroll
+    for (int x = 0; x < 8; x++) {
+        const float r = in(3 * x), gg = in(3 * x + 1), bb = in(3 * x + 2);
+        if (CH == 0)
+            px[x] = __builtin_fmaf(r, JX_KS(0.299), __builtin_fmaf(gg, JX_KS(0.587),
+                    __builtin_fmaf(bb, JX_KS(0.114), JX_K(-128.0).f)));
+        else if (CH == 1)
+            px[x] = __builtin_fmaf(r, JX_KS(-0.168736), __builtin_fmaf(gg, JX_KS(0.331264),
+                    __builtin_fmaf(bb, JX_KS(-0.5), nz)));
+        else
+            px[x] = __builtin_fmaf(r, JX_KS(0.5), __builtin_fmaf(gg, JX_KS(-0.418688),
+                    __builtin_fmaf(bb, JX_KS(-0.081312), nz)));
+    }
+#undef JX_KS
+#else
+#pragma unroll
+    for (int x = 0; x < 8; x++) {
+        const float r = (float)byte_of(row, 3 * x);
+        const float gg = (float)byte_of(row, 3 * x + 1);
+        const float bb = (float)byte_of(row, 3 * x + 2);
+        px[x] = pixel_k(CH, r, gg, bb);
+    }
+#endif
+}
+
 /* Row pass of channel CH: bytes -> pixel values -> 1-D DCT of each of the 8 pixel rows. */
-template <int CH>
-__device__ __forceinline__ void xform_rows(uint32_t (&raw)[8][6], float (&T)[8][8])
+__device__ __forceinline__ void xform_rows(const int CH, uint32_t (&raw)[8][6], float (&T)[8][8])
 {
     /* Opaque to the optimiser: forces each channel to re-convert its bytes instead of
      * keeping 192 converted floats alive across the three channel passes (CSE). */
@@ -315,13 +379,7 @@ __device__ __forceinline__ void xform_rows(uint32_t (&raw)[8][6], float (&T)[8][
     for (int y = 0; y < 8; y++) {
         JX_SB_ROW();
         float px[8];
-#pragma unroll
-        for (int x = 0; x < 8; x++) {
-            const float r = (float)byte_of(raw[y], 3 * x);
-            const float gg = (float)byte_of(raw[y], 3 * x + 1);
-            const float bb = (float)byte_of(raw[y], 3 * x + 2);
-            px[x] = jx_pixel<FOps, CH>(r, gg, bb);
-        }
+        row_pixels(CH, raw[y], px);
         jx_fdct8<FOps>(px, T[y]);
     }
 }
@@ -343,8 +401,7 @@ struct Queue {
 
 /* The staged channel CH of tile t leaves as coalesced stores; lanes in `seen` (a coefficient
  * of this channel inside the guard band) queue their block-channel for the exact pass. */
-template <int CH>
-__device__ __forceinline__ void store_and_queue(const jx_xform_args &a, WaveLds &W, Queue &Q,
+__device__ __forceinline__ void store_and_queue(const int CH, const jx_xform_args &a, WaveLds &W, Queue &Q,
                                                 bool active, unsigned b, unsigned t,
                                                 unsigned lane, uint64_t seen)
 {
@@ -356,10 +413,15 @@ __device__ __forceinline__ void store_and_queue(const jx_xform_args &a, WaveLds 
     if (f0 == fl && b0 + 63u < total) {
         u32x4 *dst = (u32x4 *)(g.out + (long long)f0 * g.out_fstride +
                                ((long long)CH * nb + (b0 - f0 * nb)) * 64);
+        /* unit e = 64j + lane is at dword o0 + 264j: one base, recomputed here (opaque) so
+         * that eight loop-invariant addresses are not hoisted out of the tile loop and spilled */
+        unsigned o0 = (lane >> 3) * 33 + (lane & 7) * 4;
+        asm volatile("" : "+v"(o0));
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            const unsigned e = (unsigned)j * 64u + lane;
-            jx_store(dst + e, stage_unit(W, e));
+            const unsigned o = o0 + 264u * (unsigned)j;
+            jx_store(dst + (unsigned)j * 64u + lane,
+                     u32x4{W.stage[o], W.stage[o + 1], W.stage[o + 2], W.stage[o + 3]});
         }
     } else {                                   /* tile crosses a frame end or the last tile */
 #pragma unroll
@@ -373,15 +435,20 @@ __device__ __forceinline__ void store_and_queue(const jx_xform_args &a, WaveLds 
      * random data at q90; wave-uniform branch): queue its block-channel */
     if (!JX_DBG_NO_EXACT && seen != 0) {
         const uint64_t M = seen & __ballot(active);
-        if ((M >> lane) & 1u) W.item[CH][Q.n[CH] + lane_rank(M)] = b;
-        Q.n[CH] += __popcll(M);
+        /* (selects, not Q.n[CH]: a runtime index would put Q in scratch memory) */
+        const int n = CH == 0 ? Q.n[0] : (CH == 1 ? Q.n[1] : Q.n[2]);
+        if ((M >> lane) & 1u) W.item[CH][n + lane_rank(M)] = b;
+        const int nn = n + __popcll(M);
+        Q.n[0] = CH == 0 ? nn : Q.n[0];
+        Q.n[1] = CH == 1 ? nn : Q.n[1];
+        Q.n[2] = CH == 2 ? nn : Q.n[2];
     }
 }
 
 /* Column pass, quantisation, zig-zag, LDS staging + coalesced store of channel CH; block-
  * channels with a coefficient inside the guard band are queued for the exact path. */
-template <int CH, class Pre>
-__device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args &a, WaveLds &W,
+template <class Pre>
+__device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const jx_xform_args &a, WaveLds &W,
                                            Queue &Q, bool active, unsigned b, unsigned t,
                                            unsigned lane, Pre &&pre)
 {
@@ -491,7 +558,7 @@ __device__ __forceinline__ void xform_cols(float (&T)[8][8], const jx_xform_args
 #elif JX_FLAG_MODE == 2
     seen = __ballot(flagany != 0u);
 #endif
-    store_and_queue<CH>(a, W, Q, active, b, t, lane, seen);
+    store_and_queue(CH, a, W, Q, active, b, t, lane, seen);
 }
 
 /* ---- fast path, packed ------------------------------------------------------------------
@@ -548,6 +615,14 @@ __device__ __forceinline__ void xform_rows_pk(uint32_t (&raw)[8][6], f2 (&T)[8][
         if (y % JX_PK_ROWS == 0) JX_SB_ROW();   /* JX_PK_ROWS rows interleave (hides the
                                                    dependent-issue gaps of one row's chain) */
         f2 px[4];
+#if JX_MIX
+        {
+            float p1[8];
+            row_pixels(CH, raw[y], p1);
+#pragma unroll
+            for (int k = 0; k < 4; k++) px[k] = f2{p1[2 * k], p1[2 * k + 1]};
+        }
+#else
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int x0 = 6 * k, x1 = 6 * k + 3;      /* byte offsets of pixels 2k, 2k+1 */
@@ -556,6 +631,7 @@ __device__ __forceinline__ void xform_rows_pk(uint32_t (&raw)[8][6], f2 (&T)[8][
             const f2 bb = f2{(float)byte_of(raw[y], x0 + 2), (float)byte_of(raw[y], x1 + 2)};
             px[k] = jx_pixel<DevPO, CH>(r, gg, bb);
         }
+#endif
         jx_fdct8_pk<DevPair>(px, T[y]);
     }
 }
@@ -569,8 +645,13 @@ __device__ __forceinline__ void xform_cols_pk(f2 (&T)[8][4], const jx_xform_args
                                               Queue &Q, bool active, unsigned b, unsigned t,
                                               unsigned lane)
 {
-    const jx_qtab &tab = g_qtab[a.quality];
-    const jx_limtab &band = g_lim[a.force_exact ? 1 : 0][a.quality];
+    /* table addresses re-derived per channel from opaque scalars (hoisted, they were kept
+     * in spilled registers and reloaded from scratch behind vmcnt waits) */
+    int qv = a.quality * 2 + (a.force_exact ? 1 : 0);
+    asm volatile("" : "+v"(qv));
+    const int qf = __builtin_amdgcn_readfirstlane(qv), qq = qf >> 1, fe = qf & 1;
+    const jx_qtab &tab = g_qtab[qq];
+    const jx_limtab &band = g_lim[fe][qq];
     const f2 M2 = f2{kMagic, kMagic};
     float acc = -1.0f;                   /* max over the channel of d*d - lsq (>= 0: flagged) */
     uint16_t *st = (uint16_t *)W.stage + lane * 66;
@@ -615,7 +696,7 @@ __device__ __forceinline__ void xform_cols_pk(f2 (&T)[8][4], const jx_xform_args
         JX_SB_COL();
     }
     const uint64_t seen = JX_DBG_NO_EXACT ? 0ull : __ballot(acc >= 0.0f);
-    store_and_queue<CH>(a, W, Q, active, b, t, lane, seen);
+    store_and_queue(CH, a, W, Q, active, b, t, lane, seen);
 }
 
 /* ---- exact path -------------------------------------------------------------------------- */
@@ -631,7 +712,7 @@ __device__ __forceinline__ uint64_t flagged_coefs(uint32_t (&raw)[8][6], int qua
     const jx_qtab &tab = g_qtab[quality];
     const jx_limtab &band = g_lim[force][quality];
     float T[8][8];
-    xform_rows<CH>(raw, T);
+    xform_rows(CH, raw, T);
     uint64_t flagged = 0;
 #pragma unroll
     for (int u = 0; u < 8; u++) {
@@ -912,6 +993,9 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
         const unsigned b = tile_block(t, lane, total), f = b / nb;
         load_block(g, f, b - f * nb, raw);
     }
+#if JX_PREFETCH == 2
+    __builtin_amdgcn_s_waitcnt(0xF70);              /* vmcnt(0): same state as the back edge */
+#endif
 #endif
     for (; t < ntiles; t += nwaves) {
         const unsigned b0 = t * 64u + lane;
@@ -944,14 +1028,14 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
                 load_block(g, fn, bn - fn * nb, raw);
             }
         };
-        xform_rows<0>(raw, T);
-        xform_cols<0>(T, a, W, Q, active, b, t, lane, reload);
+        xform_rows(0, raw, T);
+        xform_cols(0, T, a, W, Q, active, b, t, lane, reload);
         __builtin_amdgcn_sched_barrier(0);
-        xform_rows<1>(raw, T);
-        xform_cols<1>(T, a, W, Q, active, b, t, lane, reload);
+        xform_rows(1, raw, T);
+        xform_cols(1, T, a, W, Q, active, b, t, lane, reload);
         __builtin_amdgcn_sched_barrier(0);
-        xform_rows<2>(raw, T);
-        xform_cols<2>(T, a, W, Q, active, b, t, lane, next);
+        xform_rows(2, raw, T);
+        xform_cols(2, T, a, W, Q, active, b, t, lane, next);
         __builtin_amdgcn_sched_barrier(0);
 #elif JX_PACKED
         f2 TP[8][4];
@@ -971,23 +1055,41 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
 #endif
         xform_cols_pk<2>(TP, a, W, Q, active, b, t, lane);
         __builtin_amdgcn_sched_barrier(0);
+#elif JX_CHLOOP
+        /* one copy of the channel body (a third of the code), channel as a uniform value */
+        const auto none = []() {};
+#pragma nounroll
+        for (int ch = 0; ch < 3; ch++) {
+            int chv = ch;
+            asm volatile("" : "+s"(chv));           /* keep the loop rolled */
+            xform_rows(chv, raw, T);
+            xform_cols(chv, T, a, W, Q, active, b, t, lane, none);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #else
         const auto none = []() {};
-        xform_rows<0>(raw, T);
-        xform_cols<0>(T, a, W, Q, active, b, t, lane, none);
+        xform_rows(0, raw, T);
+        xform_cols(0, T, a, W, Q, active, b, t, lane, none);
         __builtin_amdgcn_sched_barrier(0);
-        xform_rows<1>(raw, T);
-        xform_cols<1>(T, a, W, Q, active, b, t, lane, none);
+        xform_rows(1, raw, T);
+        xform_cols(1, T, a, W, Q, active, b, t, lane, none);
         __builtin_amdgcn_sched_barrier(0);
-        xform_rows<2>(raw, T);
+        xform_rows(2, raw, T);
 #if JX_PREFETCH == 2
         if (tn < ntiles) {                          /* raw is dead: refill it for tile tn */
             const unsigned bn = tile_block(tn, lane, total), fn = bn / nb;
             load_block(g, fn, bn - fn * nb, raw);
         }
+        __builtin_amdgcn_sched_barrier(0);          /* issue them here, ahead of the column pass */
 #endif
-        xform_cols<2>(T, a, W, Q, active, b, t, lane, none);
+        xform_cols(2, T, a, W, Q, active, b, t, lane, none);
         __builtin_amdgcn_sched_barrier(0);
+#if JX_PREFETCH == 2
+        /* the next tile's pixels, but not this channel's 8 coefficient stores issued after
+         * them: vmcnt counts loads and stores in order, and without this explicit count the
+         * wait at the loop head is vmcnt(0), which also drains those stores every tile */
+        __builtin_amdgcn_s_waitcnt(0xF78);          /* vmcnt(8), expcnt/lgkmcnt: no wait */
+#endif
 #endif
 #if JX_FUSED_FIX
         if (!JX_DBG_NO_EXACT) {

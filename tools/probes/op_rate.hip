@@ -38,6 +38,25 @@ __global__ __launch_bounds__(256) void k(float *o, int iters, float s)
                     asm volatile("v_cmp_ge_f32_e64 %[m], |%[d]|, %[l]" : [m] "=s"(m) : [d] "v"(a[i]), [l] "s"(s));
                 } else if (MODE == 7) {   // v_add_f32 e32
                     asm volatile("v_add_f32_e32 %0, %1, %0" : "+v"(a[i]) : "v"(s));
+                } else if (MODE == 8) {   // v_perm_b32
+                    asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "s"(0x0c010c00u));
+                } else if (MODE == 9) {   // v_fma_mix_f32 (f16 lo of src0, f32 src1/src2)
+                    asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(a[i]) : "v"(u[i]), "s"(s));
+                } else if (MODE == 10) {  // v_cvt_f32_u32
+                    asm volatile("v_cvt_f32_u32_e32 %0, %1" : "=v"(a[i]) : "v"(u[i]));
+                } else if (MODE == 11) {  // v_dot2_f32_f16
+                    asm volatile("v_dot2_f32_f16 %0, %1, %2, %0" : "+v"(a[i]) : "v"(u[i]), "v"(u[(i + 1) & 7]));
+                } else if (MODE == 12) {  // dependent fma chain (latency): one chain
+                    asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(a[0]) : "v"(s));
+                } else if (MODE == 13) {  // dependent pk_fma chain (latency): one chain
+                    typedef float f2 __attribute__((ext_vector_type(2)));
+                    f2 t = f2{a[0], a[1]};
+                    asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(t) : "v"(f2{s, s}));
+                    a[0] = t.x; a[1] = t.y;
+                } else if (MODE == 14) {  // v_bfe_u32
+                    asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(u[i]));
+                } else if (MODE == 15) {  // v_mul_f32 e32
+                    asm volatile("v_mul_f32_e32 %0, %1, %0" : "+v"(a[i]) : "v"(s));
                 }
             }
     }
@@ -56,13 +75,15 @@ int main()
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const char *nm[8] = {"v_fma_f32 e64", "v_fmac_f32 e32 sgpr", "v_cvt_f32_ubyte1", "v_cmp e64 + s_or",
-                         "ds_write_b16", "v_max3_f32", "v_cmp e64 only", "v_add_f32 e32"};
+    const char *nm[16] = {"v_fma_f32 e64", "v_fmac_f32 e32 sgpr", "v_cvt_f32_ubyte1", "v_cmp e64 + s_or",
+                         "ds_write_b16", "v_max3_f32", "v_cmp e64 only", "v_add_f32 e32",
+                         "v_perm_b32", "v_fma_mix_f32", "v_cvt_f32_u32", "v_dot2_f32_f16",
+                         "fma dep chain", "pk_fma dep chain", "v_bfe_u32", "v_mul_f32 e32"};
     typedef void (*fn_t)(float *, int, float);
-    fn_t fns[8] = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>, k<7>};
-    for (int wps = 1; wps <= 4; wps++) {
+    fn_t fns[16] = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>, k<7>, k<8>, k<9>, k<10>, k<11>, k<12>, k<13>, k<14>, k<15>};
+    for (int wps = 1; wps <= 3; wps += 2) {
         const int grid = cus * wps;
-        for (int mode = 0; mode < 8; mode++) {
+        for (int mode = 0; mode < 16; mode++) {
             hipLaunchKernelGGL(fns[mode], dim3(grid), dim3(256), 0, 0, o, 10, 1.0001f);
             hipEventRecord(e0);
             hipLaunchKernelGGL(fns[mode], dim3(grid), dim3(256), 0, 0, o, iters, 1.0001f);
