@@ -43,6 +43,9 @@ namespace {
 #ifndef JX_PREFETCH
 #define JX_PREFETCH 0   /* input prefetch mode, see k_xform */
 #endif
+#ifndef JX_TPF          /* 1: quantiser tables of the next column loaded one column ahead */
+#define JX_TPF 1
+#endif
 #ifndef JX_CHLOOP       /* 1: the three channels run one rolled copy of the channel body */
 #define JX_CHLOOP 0
 #endif
@@ -417,12 +420,17 @@ __device__ __forceinline__ void store_and_queue(const int CH, const jx_xform_arg
          * that eight loop-invariant addresses are not hoisted out of the tile loop and spilled */
         unsigned o0 = (lane >> 3) * 33 + (lane & 7) * 4;
         asm volatile("" : "+v"(o0));
+        /* all eight LDS reads first, one wait, then the eight stores (interleaved, every
+         * store waited for its own read) */
+        u32x4 unit[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const unsigned o = o0 + 264u * (unsigned)j;
-            jx_store(dst + (unsigned)j * 64u + lane,
-                     u32x4{W.stage[o], W.stage[o + 1], W.stage[o + 2], W.stage[o + 3]});
+            unit[j] = u32x4{W.stage[o], W.stage[o + 1], W.stage[o + 2], W.stage[o + 3]};
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 8; j++) jx_store(dst + (unsigned)j * 64u + lane, unit[j]);
     } else {                                   /* tile crosses a frame end or the last tile */
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -470,9 +478,28 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
 #ifdef JX_DBG_NO_STAGE
     uint32_t dbg_acc = 0;
 #endif
+    /* JX_TPF: column u+1's scale and band values are read at the top of column u (scalar loads
+     * in flight under its DCT) instead of right before their use, where every column paid the
+     * scalar-load latency plus, through the shared lgkm counter, its pending LDS writes */
+    float wc[8], lc[8];
+#pragma unroll
+    for (int v = 0; v < 8; v++) {
+        wc[v] = tab.w[CH][0][v];
+        lc[v] = band.lim[CH][0][v];
+    }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
         if (u == JX_RELOAD_COL) pre();      /* e.g. issue the next pixel loads (JX_RELOAD) */
+        float wn[8], ln[8];
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            wn[v] = JX_TPF && u < 7 ? tab.w[CH][u + 1][v] : 0.0f;
+            ln[v] = JX_TPF && u < 7 ? band.lim[CH][u + 1][v] : 0.0f;
+            if (!JX_TPF) {
+                wc[v] = tab.w[CH][u][v];
+                lc[v] = band.lim[CH][u][v];
+            }
+        }
         float col[8], F[8];
 #pragma unroll
         for (int y = 0; y < 8; y++) col[y] = T[y][u];
@@ -480,7 +507,7 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
 #pragma unroll
         for (int v = 0; v < 8; v++) {
             float tm, d;
-            quant_coef(F[v], tab.w[CH][u][v], tm, d);
+            quant_coef(F[v], wc[v], tm, d);
 #if JX_STAGE16
 #ifdef JX_DBG_NO_STAGE              /* timing experiments only: no LDS staging writes */
             dbg_acc ^= __float_as_uint(tm);
@@ -498,7 +525,7 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
                 asm("v_cmp_ge_f32_e64 %[m], |%[d]|, %[l]\n\t"
                     "s_or_b64 %[seen], %[seen], %[m]"
                     : [m] "=&s"(m), [seen] "+s"(seen)
-                    : [d] "v"(d), [l] "s"(band.lim[CH][u][v])
+                    : [d] "v"(d), [l] "s"(lc[v])
                     : "scc");
 #elif JX_FLAG_MODE == 1
                 /* all in VALU: e = |d| - lim, running max (>= 0 means flagged); pinned asm
@@ -508,17 +535,17 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
                     asm("v_sub_f32_e64 %[e], |%[d]|, %[l]\n\t"
                         "v_max3_f32 %[acc], %[acc], %[p], %[e]"
                         : [e] "=&v"(e), [acc] "+v"(flagacc)
-                        : [d] "v"(d), [l] "s"(band.lim[CH][u][v]), [p] "v"(epair));
+                        : [d] "v"(d), [l] "s"(lc[v]), [p] "v"(epair));
                 } else {
                     asm("v_sub_f32_e64 %[e], |%[d]|, %[l]"
                         : [e] "=v"(epair)
-                        : [d] "v"(d), [l] "s"(band.lim[CH][u][v]));
+                        : [d] "v"(d), [l] "s"(lc[v]));
                 }
 #elif JX_FLAG_MODE == 2
                 asm("v_cmp_ge_f32_e64 vcc, |%[d]|, %[l]\n\t"
                     "v_cndmask_b32_e64 %[f], %[f], -1, vcc"
                     : [f] "+v"(flagany)
-                    : [d] "v"(d), [l] "s"(band.lim[CH][u][v])
+                    : [d] "v"(d), [l] "s"(lc[v])
                     : "vcc");
 #elif JX_FLAG_MODE == 3
                 /* one limit per column (the column's tightest): running max of |d| */
@@ -547,6 +574,13 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
                 W.stage[lane * 9 + j] =
                     u32x4{packed[4 * j], packed[4 * j + 1], packed[4 * j + 2], packed[4 * j + 3]};
 #endif
+        if (JX_TPF) {
+#pragma unroll
+            for (int v = 0; v < 8; v++) {
+                wc[v] = wn[v];
+                lc[v] = ln[v];
+            }
+        }
         JX_SB_COL();
     }
 
@@ -932,7 +966,8 @@ static_assert(sizeof(FixLds8) <= sizeof(WaveLds::stage), "FixLds8 lives in the s
 /* Exact pass of up to 8 queued blocks, taken from the tails of the three channel queues in
  * turn, inside k_xform (the staging area is free between tiles; fix_chunk8 waits for the
  * wave's tile stores before it writes). */
-__device__ __forceinline__ void fix_queued(WaveLds &W, int (&n)[3], const jx_xform_args &a,
+template <class WL>
+__device__ __forceinline__ void fix_queued(WL &W, int (&n)[3], const jx_xform_args &a,
                                         unsigned lane)
 {
     const int k0 = std::min(n[0], 8), k1 = std::min(n[1], 8 - k0),
@@ -1055,6 +1090,17 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
 #endif
         xform_cols_pk<2>(TP, a, W, Q, active, b, t, lane);
         __builtin_amdgcn_sched_barrier(0);
+#elif defined(JX_DBG_NO_COMPUTE)
+        /* timing experiments only: the same loads, LDS staging and stores, no transform */
+        (void)T;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+#pragma unroll
+            for (int z = 0; z < 64; z += 2)
+                W.stage[lane * 33 + z / 2] = raw[(z >> 3) & 7][(z + ch) % 6] + (uint32_t)z;
+            store_and_queue(ch, a, W, Q, active, b, t, lane, 0ull);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #elif JX_CHLOOP
         /* one copy of the channel body (a third of the code), channel as a uniform value */
         const auto none = []() {};
@@ -1130,6 +1176,242 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
         if (lane < 3) a.fix.count[lane * a.fix.nwaves + wave] = mine;
     }
 #endif
+}
+
+/* ---- k_xform2: two lanes per block ----------------------------------------------------------
+ * Lane l < 32 holds pixel rows 0-3 of block l of the tile, lane l + 32 rows 4-7: half the
+ * registers of one lane per block (raw 24, row outputs 32), so five waves share a SIMD instead
+ * of three.  Row pass: each lane transforms its four rows.  Transpose: v_permlane32_swap
+ * exchanges, per (row r, column k < 4), the lower lanes' column 4+k against the upper lanes'
+ * column k, after which lane l has columns 0-3 and lane l + 32 columns 4-7 of the block, all
+ * eight rows.  Column pass: four columns per lane, the same jx_fdct8 in the same input order,
+ * so every fp32 value equals the one-lane kernel's (and the guard band holds unchanged).  The
+ * quantiser's scale and band now differ between the two half-waves: they come from a small
+ * per-workgroup LDS copy of the quality's tables, [ch][half][k][v] = (w, lim). */
+#ifndef JX_K2
+#define JX_K2 0
+#endif
+#ifndef JX_K2_WPE
+#define JX_K2_WPE 4
+#endif
+constexpr int kItems2 = 64;                 /* per channel; a tile adds at most 32 */
+
+struct WaveLds2 {
+    union {
+        uint32_t stage[32 * 33];            /* one channel: block k at dwords 33k..      */
+        FixLds8 fix;                        /* exact pass, between tiles                 */
+    };
+    uint32_t item[3][kItems2];
+};
+
+/* pixel rows 4h..4h+3 of block bi of frame f (load_block's addressing, x0 = -8 quirk) */
+__device__ __forceinline__ void load_half(const jx_geom &g, unsigned f, unsigned bi, unsigned h,
+                                          uint32_t (&raw)[4][6])
+{
+    const unsigned r = bi / (unsigned)g.bpr, c = bi - r * (unsigned)g.bpr;
+    const bool last = c == (unsigned)g.bpr - 1;
+    const bool under = last && (g.row0 + (int)r == 0) && h == 0;
+    const long long row = 8ll * r - (last ? 1 : 0) + 4 * (long long)h;
+    const uint8_t *base = g.rgb + (long long)f * g.in_fstride + row * g.in_pitch + 24ll * c;
+#pragma unroll
+    for (int y = 0; y < 4; y++) {
+        const uint8_t *p = base + (long long)(y == 0 && under ? 1 : y) * g.in_pitch;
+        p = (const uint8_t *)__builtin_assume_aligned(p, 8);
+        u32x4 a4;
+        u32x2 b2;
+        __builtin_memcpy(&a4, p, 16);
+        __builtin_memcpy(&b2, p + 16, 8);
+        raw[y][0] = a4.x; raw[y][1] = a4.y; raw[y][2] = a4.z; raw[y][3] = a4.w;
+        raw[y][4] = b2.x; raw[y][5] = b2.y;
+    }
+    if (under) {                    /* one lane in rare tiles: a real branch, not six selects
+                                       whose operands would have to stay live in registers */
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 6; k++) raw[0][k] = g.under[k];
+    }
+}
+
+/* one channel of the tile: rows, transpose, columns, quantiser, staging, store, queue */
+__shared__ __attribute__((aligned(16))) float s_tab2[3][2][4][8];  /* [ch][half][k][v] = w(4half+k, v) */
+
+__device__ __forceinline__ void xform2_channel(const int CH, uint32_t (&raw)[4][6],
+                                               const jx_xform_args &a, WaveLds2 &W, int (&qn)[3],
+                                               bool active, unsigned b, unsigned t, unsigned lane)
+{
+    const jx_geom &g = a.g;
+    const unsigned h = lane >> 5, bl = lane & 31u;
+#pragma unroll
+    for (int y = 0; y < 4; y++)
+#pragma unroll
+        for (int k = 0; k < 6; k++) asm volatile("" : "+v"(raw[y][k]));
+    float T[4][8];
+#pragma unroll
+    for (int y = 0; y < 4; y++) {
+        JX_SB_ROW();
+        float px[8];
+        row_pixels(CH, raw[y], px);
+        jx_fdct8<FOps>(px, T[y]);
+    }
+    /* transpose: C[k][y] = column (4h + k), row y */
+    float C[4][8];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(T[r][k]),
+                                                             __float_as_uint(T[r][4 + k]), false, false);
+            C[k][r] = __uint_as_float(sw[0]);
+            C[k][4 + r] = __uint_as_float(sw[1]);
+        }
+    uint64_t seen = 0;
+    /* per-lane staging base and half index, opaque here: the 32 per-coefficient addresses
+     * (base + zig-zag offset, which differs between the halves) are formed in the loop, one
+     * multiply-add each, instead of being hoisted into 32 spilled registers */
+    unsigned hv = h, sbase = bl * 66;
+    asm volatile("" : "+v"(hv), "+v"(sbase));
+    uint16_t *st = (uint16_t *)W.stage + sbase;
+    /* this half's scales: one LDS base per channel (opaque, so the per-coefficient addresses
+     * become instruction offsets, not hoisted registers); the band is shared by the two
+     * halves (limh: the tighter of columns k and 4+k), a scalar operand */
+    unsigned tqo = (unsigned)(CH * 2 + h) * 32u;
+    asm volatile("" : "+v"(tqo));
+    const float4 *tq = (const float4 *)(&s_tab2[0][0][0][0] + tqo);   /* 16-B aligned rows */
+    int qv = a.quality * 2 + (a.force_exact ? 1 : 0);
+    asm volatile("" : "+v"(qv));
+    const int qf = __builtin_amdgcn_readfirstlane(qv);
+    const jx_limtab &band = g_lim[qf & 1][qf >> 1];
+    float wc[8], lc[8];
+    {
+        const float4 w0 = tq[0], w1 = tq[1];
+        wc[0] = w0.x; wc[1] = w0.y; wc[2] = w0.z; wc[3] = w0.w;
+        wc[4] = w1.x; wc[5] = w1.y; wc[6] = w1.z; wc[7] = w1.w;
+    }
+#pragma unroll
+    for (int v = 0; v < 8; v++) lc[v] = band.limh[CH][0][v];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        JX_SB_COL();
+        float wn[8], ln[8];
+        {
+            const float4 w0 = k < 3 ? tq[2 * k + 2] : float4{}, w1 = k < 3 ? tq[2 * k + 3] : float4{};
+            wn[0] = w0.x; wn[1] = w0.y; wn[2] = w0.z; wn[3] = w0.w;
+            wn[4] = w1.x; wn[5] = w1.y; wn[6] = w1.z; wn[7] = w1.w;
+        }
+#pragma unroll
+        for (int v = 0; v < 8; v++) ln[v] = k < 3 ? band.limh[CH][k + 1][v] : 0.0f;
+        float F[8];
+        jx_fdct8<FOps>(C[k], F);
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            float tm, d;
+            quant_coef(F[v], wc[v], tm, d);
+            /* zig-zag position of (u = 4h + k, v) as arithmetic on compile-time constants (a
+             * select of two constants became a per-lane table load) */
+            const int z0 = zz_of(v, k), dz = zz_of(v, 4 + k) - zz_of(v, k);
+            st[z0 + (int)hv * dz] = (uint16_t)__float_as_uint(tm);
+            if (!JX_DBG_NO_EXACT) {
+                uint64_t m;
+                asm("v_cmp_ge_f32_e64 %[m], |%[d]|, %[l]\n\t"
+                    "s_or_b64 %[seen], %[seen], %[m]"
+                    : [m] "=&s"(m), [seen] "+s"(seen)
+                    : [d] "v"(d), [l] "s"(lc[v])
+                    : "scc");
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            wc[v] = wn[v];
+            lc[v] = ln[v];
+        }
+    }
+    /* 32 blocks x 128 B: four 1-KiB coalesced stores */
+    const unsigned nb = (unsigned)g.nb, total = nb * (unsigned)g.nframes;
+    const unsigned b0 = t * 32u;
+    const unsigned f0 = b0 / nb, blast = std::min(b0 + 31u, total - 1u), fl = blast / nb;
+    if (f0 == fl && b0 + 31u < total) {
+        u32x4 *dst = (u32x4 *)(g.out + (long long)f0 * g.out_fstride +
+                               ((long long)CH * nb + (b0 - f0 * nb)) * 64);
+        unsigned o0 = (lane >> 3) * 33 + (lane & 7) * 4;
+        asm volatile("" : "+v"(o0));
+        u32x4 unit[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const unsigned o = o0 + 264u * (unsigned)j;
+            unit[j] = u32x4{W.stage[o], W.stage[o + 1], W.stage[o + 2], W.stage[o + 3]};
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) jx_store(dst + (unsigned)j * 64u + lane, unit[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const unsigned e = (unsigned)j * 64u + lane, bb = b0 + (e >> 3);
+            if (bb < total) {
+                const unsigned o = (e >> 3) * 33 + (e & 7) * 4;
+                jx_store((u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8),
+                         u32x4{W.stage[o], W.stage[o + 1], W.stage[o + 2], W.stage[o + 3]});
+            }
+        }
+    }
+    /* a block is flagged when either of its lanes is: fold the upper half onto the lower */
+    if (!JX_DBG_NO_EXACT && seen != 0) {
+        const uint64_t act = __ballot(active);
+        const uint32_t M = (uint32_t)((seen | (seen >> 32)) & act);
+        const int n = CH == 0 ? qn[0] : (CH == 1 ? qn[1] : qn[2]);
+        if (h == 0 && ((M >> bl) & 1u))
+            W.item[CH][n + __builtin_amdgcn_mbcnt_lo(M, 0u)] = b;
+        const int nn = n + __popc(M);
+        qn[0] = CH == 0 ? nn : qn[0];
+        qn[1] = CH == 1 ? nn : qn[1];
+        qn[2] = CH == 2 ? nn : qn[2];
+    }
+}
+
+__global__ __launch_bounds__(JX_WG, JX_K2_WPE) void k_xform2(const jx_xform_args a)
+{
+    __shared__ WaveLds2 s_wave[JX_WG / 64];
+    const jx_geom &g = a.g;
+    {
+        const jx_qtab &tab = g_qtab[a.quality];
+        for (unsigned i = threadIdx.x; i < 3 * 2 * 4 * 8; i += blockDim.x) {
+            const unsigned ch = i / 64, hh = (i / 32) & 1, k = (i / 8) & 3, v = i & 7;
+            s_tab2[ch][hh][k][v] = tab.w[ch][4 * hh + k][v];
+        }
+        __syncthreads();
+    }
+    const unsigned nb = (unsigned)g.nb;
+    const unsigned total = nb * (unsigned)g.nframes;
+    const unsigned ntiles = (total + 31u) / 32u;
+    const unsigned lane = threadIdx.x & 63u, h = lane >> 5, bl = lane & 31u;
+    const unsigned nwaves = gridDim.x * (JX_WG / 64);
+    unsigned t = blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6);
+    if (t >= ntiles) return;
+    WaveLds2 &W = s_wave[threadIdx.x >> 6];
+    int qn[3] = {0, 0, 0};
+    for (; t < ntiles; t += nwaves) {
+        const unsigned b0 = t * 32u + bl;
+        const bool active = b0 < total;
+        const unsigned b = active ? b0 : total - 1;
+        uint32_t raw[4][6];
+        {
+            const unsigned f = b / nb;
+            load_half(g, f, b - f * nb, h, raw);
+        }
+        xform2_channel(0, raw, a, W, qn, active, b, t, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        xform2_channel(1, raw, a, W, qn, active, b, t, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        xform2_channel(2, raw, a, W, qn, active, b, t, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!JX_DBG_NO_EXACT) {
+            while (qn[0] > kItems2 - 32 || qn[1] > kItems2 - 32 || qn[2] > kItems2 - 32)
+                fix_queued(W, qn, a, lane);
+        }
+    }
+    if (!JX_DBG_NO_EXACT) {
+        while (qn[0] + qn[1] + qn[2] > 0) fix_queued(W, qn, a, lane);
+    }
 }
 
 /*
@@ -1369,6 +1651,13 @@ int tables_for_current_device()
                     band[q].limcol[ch][u] = m;
                     band[JX_MAXQ + 1 + q].limcol[ch][u] = -1.0f;
                 }
+            for (int ch = 0; ch < 3; ch++)
+                for (int k = 0; k < 4; k++)
+                    for (int v = 0; v < 8; v++) {
+                        band[q].limh[ch][k][v] =
+                            std::min(band[q].lim[ch][k][v], band[q].lim[ch][4 + k][v]);
+                        band[JX_MAXQ + 1 + q].limh[ch][k][v] = -1.0f;
+                    }
             /* packed path: pair order, squared limits rounded down (d*d >= lsq is implied by
              * |d| >= lim, so every coefficient the band flags is still flagged) */
             for (int ch = 0; ch < 3; ch++)
@@ -1408,7 +1697,8 @@ int resident_waves()
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_xform, JX_WG, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, JX_K2 ? k_xform2 : k_xform, JX_WG,
+                                                          0) != hipSuccess ||
             per_cu < 1)
             per_cu = 2;
 #ifdef JX_DBG_GRID_WGS_PER_CU   /* timing experiments: fewer resident workgroups per CU */
@@ -1484,6 +1774,17 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     xa.quality = p->quality;
     xa.force_exact = (p->flags & JPGX_FLAG_FORCE_EXACT) ? 1 : 0;
     hipStream_t s = (hipStream_t)stream;
+    if (JX_K2) {
+        /* two lanes per block: 32-block tiles, persistent grid, exact pass inside */
+        const size_t nt2 = (total + 31) / 32;
+        const size_t w2 = std::min<size_t>(nt2, (size_t)std::max(resident_waves(), 4));
+        const unsigned grid2 = (unsigned)((w2 + JX_WG / 64 - 1) / (JX_WG / 64));
+        hipLaunchKernelGGL(k_xform2, dim3(grid2), dim3(JX_WG), 0, s, xa);
+        rc = hip_rc(hipGetLastError());
+        if (rc) return rc;
+        if (event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
+        return rc;
+    }
     const size_t ntiles = (total + 63) / 64;
 #ifndef JX_PERSISTENT     /* 0: one wave per tile (the dispatcher refills SIMDs as waves end) */
 #define JX_PERSISTENT 1
