@@ -54,6 +54,13 @@ extern "C" {
 
 /* flags */
 #define JPGX_FLAG_FORCE_EXACT 1u /* send every coefficient through the exact fp64 path     */
+/* EXTENSION (no reference counterpart: src/downsample.c:24-32 only prints): with sample_ratio
+ * 1 or 2, really subsample the chroma -- level-shifted Cb/Cr averaged over the horizontal pixel
+ * pair (4:2:2) or the 2x2 quad (4:2:0), in that order; the (W/2) x H or (W/2) x (H/2) planes are
+ * tiled in raster order (the x0 = -8 quirk stays a property of the 4:4:4 tiling only).  Y is
+ * unchanged.  Frame output becomes Y [nb][64], Cb [nbc][64], Cr [nbc][64] contiguous, nbc =
+ * jpgx_chroma_blocks(); for 4:2:0 stripes must start and end on even block rows. */
+#define JPGX_FLAG_SUBSAMPLE 2u
 
 typedef struct jpgx_params {
     int quality;              /* 1..97                                                    */
@@ -99,6 +106,11 @@ int jpgx_scale_table(int which, int quality, int out[8][8]);
  * whose fp32 quotient lies within lim of a rounding boundary is recomputed exactly.
  * Also returns the fp32 per-coefficient scale.  For tests and documentation. */
 int jpgx_guard_band(int quality, float scale[3][64], float lim[3][64]);
+
+/* Chroma blocks per channel of the stripe [row_begin, row_end) of a width-pixel frame: nb =
+ * (row_end-row_begin)*width/8 without JPGX_FLAG_SUBSAMPLE (or sample_ratio 0), else
+ * rows*width/16 (4:2:2) or rows/2*width/16 (4:2:0). */
+size_t jpgx_chroma_blocks(int width, int row_begin, int row_end, int sample_ratio, unsigned flags);
 
 /* ---- device path (pointers are device pointers; `stream` is a hipStream_t or NULL) ---- */
 

@@ -64,6 +64,8 @@ struct jx_xform_args {
     jx_fixlist fix;
     int quality;            /* index into the device table                                */
     int force_exact;        /* JPGX_FLAG_FORCE_EXACT: flag every coefficient              */
+    int luma_only;          /* k_xform: channel 0 only (chroma from k_chroma)             */
+    int sub;                /* k_chroma: 1 = true 4:2:2, 2 = true 4:2:0                   */
 };
 
 
@@ -72,6 +74,8 @@ extern "C" {
 #endif
 /* host plan (jpgx_plan.cpp) */
 int jx_plan_tables(int quality, float w[3][64], float lim[3][64], int16_t q[2][64]);
+/* the same for true chroma subsampling: sub 1 = 4:2:2 averages, 2 = 4:2:0 (chroma bounds) */
+int jx_plan_tables_mode(int quality, int sub, float w[3][64], float lim[3][64], int16_t q[2][64]);
 void jx_under_dwords(const uint8_t under[3][8], uint32_t out[6]);
 /* packed-pair vs scalar transform, bit for bit (host; returns the mismatch count) */
 long long jx_selftest_pk(long long nblocks, unsigned long long seed);

@@ -141,6 +141,8 @@ __constant__ double kCos[8][8] = JX_COS_INIT;
  * become scalar loads; filled once per device by tables_for_current_device(). */
 __constant__ jx_qtab g_qtab[JX_MAXQ + 1];
 __constant__ jx_limtab g_lim[2][JX_MAXQ + 1];
+/* true chroma subsampling (k_chroma): [sub-1][force][q], chroma bounds of averaged samples */
+__constant__ jx_limtab g_limsub[2][2][JX_MAXQ + 1];
 
 /* dct.c:13 ALPHA(0) = 1/sqrt(2) as the reference's double */
 constexpr double kAlpha0 = JX_ALPHA0;
@@ -465,7 +467,8 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
     uint32_t packed[32];   /* zig-zag pairs (2k, 2k+1) as one dword, formed when complete */
 #endif
     const jx_qtab &tab = g_qtab[a.quality];
-    const jx_limtab &band = g_lim[a.force_exact ? 1 : 0][a.quality];
+    const int fe = a.force_exact ? 1 : 0;
+    const jx_limtab &band = a.sub ? g_limsub[a.sub - 1][fe][a.quality] : g_lim[fe][a.quality];
     /* wave mask of lanes with a coefficient of this channel inside the guard band */
     uint64_t seen = 0;
 #if JX_FLAG_MODE == 1 || JX_FLAG_MODE == 3
@@ -1117,6 +1120,7 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
         xform_rows(0, raw, T);
         xform_cols(0, T, a, W, Q, active, b, t, lane, none);
         __builtin_amdgcn_sched_barrier(0);
+        if (!a.luma_only) {                      /* (true subsampling: chroma in k_chroma) */
         xform_rows(1, raw, T);
         xform_cols(1, T, a, W, Q, active, b, t, lane, none);
         __builtin_amdgcn_sched_barrier(0);
@@ -1130,6 +1134,7 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
 #endif
         xform_cols(2, T, a, W, Q, active, b, t, lane, none);
         __builtin_amdgcn_sched_barrier(0);
+        }
 #if JX_PREFETCH == 2
         /* the next tile's pixels, but not this channel's 8 coefficient stores issued after
          * them: vmcnt counts loads and stores in order, and without this explicit count the
@@ -1176,6 +1181,133 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
         if (lane < 3) a.fix.count[lane * a.fix.nwaves + wave] = mine;
     }
 #endif
+}
+
+/* ---- k_chroma: true 4:2:2 / 4:2:0 chroma (extension) ---------------------------------------
+ * The reference's subsample_422/420 (src/downsample.c:24-32) only print; oracle/cpu_ref.h
+ * defines the semantics this kernel implements: level-shifted Cb/Cr (preprocess.c:161-162,
+ * 186-188) averaged over the horizontal pixel pair (4:2:2) or the 2x2 quad (4:2:0) -- the
+ * Notes' "level shift before chroma subsample" -- tiled in raster order on the (W/2) x H or
+ * (W/2) x (H/2) plane, then the same DCT, transposed chroma quantisation, zig-zag, guard band
+ * (bounds of the averaged samples, g_limsub) and exact fallback.  One lane per chroma block,
+ * one channel at a time, pixel rows read as they are transformed (no 96-register tile).
+ * g.bpr = chroma blocks per row, g.nb = chroma blocks per frame stripe, g.out offset so that
+ * channel ch lands at out + (nb_y + (ch-1) nbc) * 64 of each frame. */
+
+/* exact sample (level shift, then the average), the oracle's double operations */
+__device__ __forceinline__ double exact_chroma(const jx_geom &g, int sub, int ch, unsigned f,
+                                               unsigned X, unsigned Y)
+{
+    const uint8_t *p = g.rgb + (long long)f * g.in_fstride +
+                       (long long)(sub == 2 ? 2 * Y : Y) * g.in_pitch + 6ll * X;
+    const double e0 = exact_pixel(ch, p[0], p[1], p[2]), e1 = exact_pixel(ch, p[3], p[4], p[5]);
+    if (sub == 1) return (e0 + e1) * 0.5;
+    const uint8_t *q = p + g.in_pitch;
+    const double e2 = exact_pixel(ch, q[0], q[1], q[2]), e3 = exact_pixel(ch, q[3], q[4], q[5]);
+    return ((e0 + e1) + (e2 + e3)) * 0.25;
+}
+
+/* Exact recomputation of every queued block of channel ch (the whole block: the exact value
+ * is the definition), one coefficient per lane; written over the fast values once the
+ * tile's stores have landed. */
+__device__ void fix_chroma(WaveLds &W, Queue &Q, int ch, const jx_xform_args &a, unsigned lane)
+{
+    const jx_geom &g = a.g;
+    const int n = ch == 1 ? Q.n[1] : Q.n[2];
+    if (n == 0) return;
+    double *smp = reinterpret_cast<double *>(W.stage);
+    const unsigned nb = (unsigned)g.nb, bpr = (unsigned)g.bpr;
+    const int u = (int)(lane & 7u), v = (int)(lane >> 3);
+    const int qd = g_qtab[a.quality].q[1][u * 8 + v];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int i = 0; i < n; i++) {
+        const unsigned b = W.item[ch][i];
+        const unsigned f = b / nb, bi = b - f * nb, by = bi / bpr, bx = bi - by * bpr;
+        smp[lane] = exact_chroma(g, a.sub, ch, f, 8 * bx + (lane & 7u), 8 * by + (lane >> 3));
+        wave_sync_lds();
+        double s = 0.0;
+#pragma unroll
+        for (int x = 0; x < 8; x++)              /* dct.c:46-50: x outer, y inner */
+#pragma unroll
+            for (int y = 0; y < 8; y++) s += smp[y * 8 + x] * kCos[u][x] * kCos[v][y];
+        *coef_ptr(g, b, ch, zz_of_rt(v, u)) = exact_finish(s, u, v, qd);
+        wave_sync_lds();
+    }
+    if (ch == 1) Q.n[1] = 0; else Q.n[2] = 0;
+}
+
+template <int SUB>
+__device__ __forceinline__ void chroma_rows(const int CH, const jx_geom &g, unsigned f, unsigned bx,
+                                            unsigned by, float (&T)[8][8])
+{
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+        JX_SB_ROW();
+        const unsigned Y = 8 * by + y;
+        const uint8_t *p = g.rgb + (long long)f * g.in_fstride +
+                           (long long)(SUB == 2 ? 2 * Y : Y) * g.in_pitch + 48ll * bx;
+        p = (const uint8_t *)__builtin_assume_aligned(p, 8);
+        uint32_t r0[12], r1[12];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            u32x2 w;
+            __builtin_memcpy(&w, p + 8 * k, 8);
+            r0[2 * k] = w.x; r0[2 * k + 1] = w.y;
+            if (SUB == 2) {
+                __builtin_memcpy(&w, p + g.in_pitch + 8 * k, 8);
+                r1[2 * k] = w.x; r1[2 * k + 1] = w.y;
+            }
+        }
+        const auto bt = [](const uint32_t (&r)[12], int i) {
+            return (float)((r[i >> 2] >> (8 * (i & 3))) & 0xffu);
+        };
+        float smp[8];
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+            const int i0 = 6 * x, i1 = 6 * x + 3;        /* bytes of pixels 2x, 2x+1 */
+            const float p0 = pixel_k(CH, bt(r0, i0), bt(r0, i0 + 1), bt(r0, i0 + 2));
+            const float p1 = pixel_k(CH, bt(r0, i1), bt(r0, i1 + 1), bt(r0, i1 + 2));
+            if (SUB == 1) {
+                smp[x] = (p0 + p1) * 0.5f;
+            } else {
+                const float q0 = pixel_k(CH, bt(r1, i0), bt(r1, i0 + 1), bt(r1, i0 + 2));
+                const float q1 = pixel_k(CH, bt(r1, i1), bt(r1, i1 + 1), bt(r1, i1 + 2));
+                smp[x] = ((p0 + p1) + (q0 + q1)) * 0.25f;
+            }
+        }
+        jx_fdct8<FOps>(smp, T[y]);
+    }
+}
+
+template <int SUB>
+__global__ __launch_bounds__(JX_WG, 3) void k_chroma(const jx_xform_args a)
+{
+    __shared__ WaveLds s_wave[JX_WG / 64];
+    const jx_geom &g = a.g;
+    const unsigned nb = (unsigned)g.nb, bpr = (unsigned)g.bpr;
+    const unsigned total = nb * (unsigned)g.nframes;
+    const unsigned ntiles = (total + 63u) / 64u;
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned nwaves = gridDim.x * (JX_WG / 64);
+    unsigned t = blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6);
+    if (t >= ntiles) return;
+    WaveLds &W = s_wave[threadIdx.x >> 6];
+    Queue Q{{0, 0, 0}, {0u, 0u, 0u}};
+    const auto none = []() {};
+    for (; t < ntiles; t += nwaves) {
+        const unsigned b0 = t * 64u + lane;
+        const bool active = b0 < total;
+        const unsigned b = active ? b0 : total - 1;
+        const unsigned f = b / nb, bi = b - f * nb, by = bi / bpr, bx = bi - by * bpr;
+#pragma unroll
+        for (int ch = 1; ch <= 2; ch++) {
+            float T[8][8];
+            chroma_rows<SUB>(ch, g, f, bx, by, T);
+            xform_cols(ch, T, a, W, Q, active, b, t, lane, none);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!JX_DBG_NO_EXACT) fix_chroma(W, Q, ch, a, lane);
+        }
+    }
 }
 
 /* ---- k_xform2: two lanes per block ----------------------------------------------------------
@@ -1676,8 +1808,28 @@ int tables_for_current_device()
                             band[JX_MAXQ + 1 + q].lsq[ch][j][v][l] = -1.0f;
                         }
         }
+        /* true subsampling: chroma bounds of the averaged samples, [sub-1][force][q] */
+        std::vector<jx_limtab> bsub(2 * 2 * (JX_MAXQ + 1));
+        memset(bsub.data(), 0, bsub.size() * sizeof(jx_limtab));
+        for (int sm = 1; sm <= 2; sm++)
+            for (int q = 1; q <= JX_MAXQ; q++) {
+                float w[3][64], lim[3][64];
+                int16_t qq[2][64];
+                jx_plan_tables_mode(q, sm, w, lim, qq);
+                jx_limtab &bn = bsub[((sm - 1) * 2 + 0) * (JX_MAXQ + 1) + q];
+                jx_limtab &bf = bsub[((sm - 1) * 2 + 1) * (JX_MAXQ + 1) + q];
+                for (int ch = 0; ch < 3; ch++)
+                    for (int u = 0; u < 8; u++)
+                        for (int v = 0; v < 8; v++) {
+                            bn.lim[ch][u][v] = lim[ch][v * 8 + u];
+                            bf.lim[ch][u][v] = -1.0f;
+                        }
+            }
         g_tab_rc[dev] = hip_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_qtab), host.data(),
                                                  host.size() * sizeof(jx_qtab)));
+        if (!g_tab_rc[dev])
+            g_tab_rc[dev] = hip_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_limsub), bsub.data(),
+                                                     bsub.size() * sizeof(jx_limtab)));
         if (!g_tab_rc[dev])
             g_tab_rc[dev] = hip_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_lim), band.data(),
                                                      band.size() * sizeof(jx_limtab)));
@@ -1713,6 +1865,14 @@ int resident_waves()
 
 extern "C" {
 
+size_t jpgx_chroma_blocks(int width, int row_begin, int row_end, int sample_ratio, unsigned flags)
+{
+    if (width <= 0 || row_end < row_begin) return 0;
+    const size_t rows = (size_t)(row_end - row_begin);
+    if (!(flags & JPGX_FLAG_SUBSAMPLE) || sample_ratio == 0) return rows * (size_t)(width / 8);
+    return (sample_ratio == 2 ? rows / 2 : rows) * (size_t)(width / 16);
+}
+
 size_t jpgx_workspace_size(const jpgx_frames *fr)
 {
     if (!fr || fr->row_end <= fr->row_begin || fr->nframes < 1 || fr->width < 8) return 0;
@@ -1740,6 +1900,9 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     if (fr->row_begin < 0 || fr->row_end > fr->height / 8 || fr->row_begin > fr->row_end ||
         fr->nframes < 1)
         return JPGX_EARG;
+    const bool sub = (p->flags & JPGX_FLAG_SUBSAMPLE) != 0;
+    if (sub && p->sample_ratio == 0) return JPGX_ESAMPLE;
+    if (sub && p->sample_ratio == 2 && ((fr->row_begin | fr->row_end) & 1)) return JPGX_EARG;
     if (fr->row_begin == fr->row_end) return JPGX_OK;
     if (!d_rgb || !d_out) return JPGX_EARG;
     if (fr->in_pitch < (size_t)fr->width * 3 || fr->in_pitch % 8 || fr->in_frame_stride % 8 ||
@@ -1749,7 +1912,10 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     const size_t nb = (size_t)(fr->row_end - fr->row_begin) * bpr;
     const size_t total = nb * fr->nframes;
     if (total + 64 >= (1ull << 32)) return JPGX_EARG;
-    if (fr->nframes > 1 && fr->out_frame_stride < 3 * nb * 64) return JPGX_EARG;
+    const size_t nbc = sub ? jpgx_chroma_blocks(fr->width, fr->row_begin, fr->row_end,
+                                                p->sample_ratio, p->flags)
+                           : nb;
+    if (fr->nframes > 1 && fr->out_frame_stride < (nb + 2 * nbc) * 64) return JPGX_EARG;
     if (fr->nframes > 1 && fr->in_frame_stride < fr->in_pitch * (size_t)(fr->row_end - fr->row_begin) * 8)
         return JPGX_EARG;
     if (workspace_bytes < jpgx_workspace_size(fr) || !d_workspace ||
@@ -1774,7 +1940,8 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     xa.quality = p->quality;
     xa.force_exact = (p->flags & JPGX_FLAG_FORCE_EXACT) ? 1 : 0;
     hipStream_t s = (hipStream_t)stream;
-    if (JX_K2) {
+    xa.luma_only = sub ? 1 : 0;
+    if (JX_K2 && !sub) {
         /* two lanes per block: 32-block tiles, persistent grid, exact pass inside */
         const size_t nt2 = (total + 31) / 32;
         const size_t w2 = std::min<size_t>(nt2, (size_t)std::max(resident_waves(), 4));
@@ -1813,6 +1980,24 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     hipLaunchKernelGGL(k_xform, dim3(grid), dim3(JX_WG), 0, s, xa);
     rc = hip_rc(hipGetLastError());
     if (rc) return rc;
+    if (sub) {
+        /* true 4:2:2 / 4:2:0 chroma: Cb at out + nb*64, Cr at out + (nb + nbc)*64 per frame */
+        jx_xform_args xc = xa;
+        xc.luma_only = 0;
+        xc.sub = p->sample_ratio;
+        xc.g.bpr = fr->width / 16;
+        xc.g.nb = (int)nbc;
+        xc.g.out = d_out + (long long)nb * 64 - (long long)nbc * 64;
+        const size_t ctiles = (nbc * fr->nframes + 63) / 64;
+        const size_t cw = std::min<size_t>(ctiles, (size_t)std::max(resident_waves(), 4));
+        const unsigned cgrid = (unsigned)((cw + JX_WG / 64 - 1) / (JX_WG / 64));
+        if (p->sample_ratio == 1)
+            hipLaunchKernelGGL(k_chroma<1>, dim3(cgrid), dim3(JX_WG), 0, s, xc);
+        else
+            hipLaunchKernelGGL(k_chroma<2>, dim3(cgrid), dim3(JX_WG), 0, s, xc);
+        rc = hip_rc(hipGetLastError());
+        if (rc) return rc;
+    }
     if (event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
     if (rc) return rc;
     /* exact pass: one wave per channel and group of kFixGroup k_xform waves */
@@ -1855,7 +2040,8 @@ int jpgx_device_count(void)
 }
 
 /* One GPU, one stripe: H2D of the stripe (+ the pixel row above it), run, D2H of the
- * stripe's three channel ranges into the whole-image [3][nb][64] host output. */
+ * stripe's three channel ranges into the whole-image host output: [3][nb][64], or with
+ * JPGX_FLAG_SUBSAMPLE Y [nb][64] + Cb, Cr [nbc][64]. */
 static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
                       const jpgx_params *p, int16_t *out, int device, int r0, int r1)
 {
@@ -1867,6 +2053,9 @@ static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
     const int halo = r0 > 0 ? 1 : 0;
     const size_t rows = (size_t)(r1 - r0) * 8 + halo;
     const size_t nb_s = (size_t)(r1 - r0) * bpr, nb = (size_t)(height / 8) * bpr;
+    const size_t nbc_s = jpgx_chroma_blocks(width, r0, r1, p->sample_ratio, p->flags);
+    const size_t nbc = jpgx_chroma_blocks(width, 0, height / 8, p->sample_ratio, p->flags);
+    const size_t c0 = jpgx_chroma_blocks(width, 0, r0, p->sample_ratio, p->flags);
     jpgx_frames fr;
     memset(&fr, 0, sizeof fr);
     fr.width = width;
@@ -1876,7 +2065,7 @@ static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
     fr.nframes = 1;
     fr.in_pitch = dpitch;
     fr.in_frame_stride = dpitch * rows;
-    fr.out_frame_stride = 3 * nb_s * 64;
+    fr.out_frame_stride = (nb_s + 2 * nbc_s) * 64;
     uint8_t *d_in = nullptr;
     int16_t *d_out = nullptr;
     void *d_ws = nullptr;
@@ -1884,7 +2073,7 @@ static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
     hipStream_t s = nullptr;
     int rc = JPGX_OK;
     if (hipMalloc(&d_in, rows * dpitch) != hipSuccess ||
-        hipMalloc(&d_out, 3 * nb_s * 64 * sizeof(int16_t)) != hipSuccess ||
+        hipMalloc(&d_out, (nb_s + 2 * nbc_s) * 64 * sizeof(int16_t)) != hipSuccess ||
         hipMalloc(&d_ws, ws) != hipSuccess || hipStreamCreate(&s) != hipSuccess) {
         rc = JPGX_EHIP;
     }
@@ -1894,10 +2083,13 @@ static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
                                      hipMemcpyHostToDevice, s));
     }
     if (!rc) rc = jpgx_blocks_gpu(&fr, p, d_in + halo * dpitch, d_out, d_ws, ws, s);
-    for (int ch = 0; ch < 3 && !rc; ch++)
-        rc = hip_rc(hipMemcpyAsync(out + ((size_t)ch * nb + (size_t)r0 * bpr) * 64,
-                                   d_out + (size_t)ch * nb_s * 64, nb_s * 64 * sizeof(int16_t),
+    for (int ch = 0; ch < 3 && !rc; ch++) {
+        const size_t dst = ch == 0 ? (size_t)r0 * bpr : nb + (size_t)(ch - 1) * nbc + c0;
+        const size_t srcb = ch == 0 ? 0 : nb_s + (size_t)(ch - 1) * nbc_s;
+        const size_t cnt = ch == 0 ? nb_s : nbc_s;
+        rc = hip_rc(hipMemcpyAsync(out + dst * 64, d_out + srcb * 64, cnt * 64 * sizeof(int16_t),
                                    hipMemcpyDeviceToHost, s));
+    }
     if (!rc) rc = hip_rc(hipStreamSynchronize(s));
     if (s) (void)hipStreamDestroy(s);
     (void)hipFree(d_in);
@@ -1927,10 +2119,14 @@ int jpgx_blocks_multi(const uint8_t *rgb, int width, int height, size_t pitch,
     if (ngpus > jpgx_device_count()) return JPGX_ENODEV;
     std::vector<int> rcs(ngpus, JPGX_OK);
     std::vector<std::thread> th;
+    /* true 4:2:0 stripes split MCU rows (pairs of block rows) */
+    const int unit = (p->flags & JPGX_FLAG_SUBSAMPLE) && p->sample_ratio == 2 ? 2 : 1;
     for (int k = 0; k < ngpus; k++) {
         th.emplace_back([&, k]() {
             int r0, r1;
-            jpgx_stripe(height / 8, ngpus, k, &r0, &r1);
+            jpgx_stripe(height / 8 / unit, ngpus, k, &r0, &r1);
+            r0 *= unit;
+            r1 *= unit;
             rcs[k] = run_stripe(rgb, width, height, pitch, p, out, k, r0, r1);
         });
     }

@@ -64,12 +64,18 @@ struct BoundOps {
     static Bnd lit(jx_const k) { return Bnd{k.x, k.x, fabs((double)k.f - k.x)}; }
 };
 
+/* sub: 0 = one pixel per sample (4:4:4 and the reference's parity modes); 1 = the average
+ * (p0 + p1) * 0.5 of two independent pixels (true 4:2:2); 2 = ((p00 + p01) + (p10 + p11)) * 0.25
+ * (true 4:2:0), the kernel's (k_chroma) operation order */
 template <int CH>
-void coef_bounds(Bnd F[8][8])
+void coef_bounds(Bnd F[8][8], int sub = 0)
 {
     const Bnd byte{0.0, 255.0, 0.0};
     Bnd px[8], row[8];
-    const Bnd p = jx_pixel<BoundOps, CH>(byte, byte, byte);
+    Bnd p = jx_pixel<BoundOps, CH>(byte, byte, byte);
+    if (sub == 1) p = BoundOps::mulc(BoundOps::add(p, p), JX_K(0.5));
+    if (sub == 2)
+        p = BoundOps::mulc(BoundOps::add(BoundOps::add(p, p), BoundOps::add(p, p)), JX_K(0.25));
     for (int x = 0; x < 8; x++) px[x] = p;
     jx_fdct8<BoundOps>(px, row);   /* every pixel row has the same bound */
     for (int u = 0; u < 8; u++) {
@@ -173,7 +179,7 @@ static long double dct_kfactor(int k)
     return (k == 0 ? 8.0L : 4.0L) / out[k];
 }
 
-int jx_plan_tables(int quality, float w[3][64], float lim[3][64], int16_t q[2][64])
+int jx_plan_tables_mode(int quality, int sub, float w[3][64], float lim[3][64], int16_t q[2][64])
 {
     int qs[2][8][8];
     int rc = jpgx_scale_table(0, quality, qs[0]);
@@ -184,9 +190,9 @@ int jx_plan_tables(int quality, float w[3][64], float lim[3][64], int16_t q[2][6
             for (int v = 0; v < 8; v++) q[t][u * 8 + v] = (int16_t)qs[t][u][v];
 
     Bnd F[3][8][8];
-    coef_bounds<0>(F[0]);
-    coef_bounds<1>(F[1]);
-    coef_bounds<2>(F[2]);
+    coef_bounds<0>(F[0]);                  /* luma is never averaged */
+    coef_bounds<1>(F[1], sub);
+    coef_bounds<2>(F[2], sub);
     const long double a0 = 1.0L / sqrtl(2.0L);
     for (int ch = 0; ch < 3; ch++) {
         const int t = ch == 0 ? 0 : 1;
@@ -209,6 +215,11 @@ int jx_plan_tables(int quality, float w[3][64], float lim[3][64], int16_t q[2][6
             }
     }
     return JPGX_OK;
+}
+
+int jx_plan_tables(int quality, float w[3][64], float lim[3][64], int16_t q[2][64])
+{
+    return jx_plan_tables_mode(quality, 0, w, lim, q);
 }
 
 int jpgx_guard_band(int quality, float scale[3][64], float lim[3][64])

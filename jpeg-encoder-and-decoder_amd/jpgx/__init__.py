@@ -25,6 +25,7 @@ NO_CHROMA_SUBSAMPLING = 0
 HORIZONTAL_SUBSAMPLING = 1
 HORIZONTAL_VERTICAL_SUBSAMPLING = 2
 FLAG_FORCE_EXACT = 1
+FLAG_SUBSAMPLE = 2      # true 4:2:2 / 4:2:0 chroma (extension; see include/jpgx.h)
 
 OK, EGEOMETRY, EQUALITY, ESAMPLE, EARG, EHIP, EWORKSPACE, ENODEV = 0, -1, -2, -3, -4, -5, -6, -7
 _ERRNAMES = {-1: "EGEOMETRY", -2: "EQUALITY", -3: "ESAMPLE", -4: "EARG", -5: "EHIP",
@@ -37,7 +38,7 @@ EXPORTS = [
     "jpgx_guard_band", "jpgx_workspace_size", "jpgx_blocks_gpu", "jpgx_blocks_gpu_ev",
     "jpgx_gen_splitmix_gpu",
     "jpgx_gen_tie_gpu", "jpgx_blocks", "jpgx_blocks_multi", "jpgx_stripe",
-    "jpgx_device_count", "jpgx_version",
+    "jpgx_device_count", "jpgx_version", "jpgx_chroma_blocks",
 ]
 COMPAT_EXPORTS = [
     "jpgx_new_block", "jpgx_get_value_block", "jpgx_set_value_block", "jpgx_copy_block",
@@ -97,6 +98,8 @@ def _load() -> ctypes.CDLL:
     L.jpgx_stripe.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
     L.jpgx_stripe.restype = None
     L.jpgx_device_count.argtypes = []
+    L.jpgx_chroma_blocks.argtypes = [i, i, i, i, ctypes.c_uint]
+    L.jpgx_chroma_blocks.restype = sz
     L.jpgx_version.restype = ctypes.c_char_p
     return L
 
@@ -215,15 +218,30 @@ def gen_tie_gpu(d_dst, width: int, height: int, stream=None) -> None:
            "jpgx_gen_tie_gpu")
 
 
+def chroma_blocks(width: int, row_begin: int, row_end: int, sample_ratio: int = 0,
+                  flags: int = 0) -> int:
+    """Chroma blocks per channel of a stripe (== luma blocks unless FLAG_SUBSAMPLE)."""
+    return int(lib.jpgx_chroma_blocks(width, row_begin, row_end, sample_ratio, flags))
+
+
+def split_sub(out, nb: int, nbc: int):
+    """(Y [nb][64], CbCr [2][nbc][64]) views of one frame's FLAG_SUBSAMPLE output."""
+    return out[:nb], out[nb:nb + 2 * nbc].reshape(2, nbc, 64)
+
+
 def encode_blocks(rgb, quality: int, sample_ratio: int = 0, underflow: bytes | None = None,
                   flags: int = 0, device=None):
     """Convenience: one image (H,W,3 uint8 torch tensor on a GPU, or numpy on the host) ->
-    int16 [3][nb][64].  Device tensors stay on the device; numpy goes through jpgx_blocks."""
+    int16 [3][nb][64] (with FLAG_SUBSAMPLE: [nb + 2 nbc][64], see split_sub).  Device tensors
+    stay on the device; numpy goes through jpgx_blocks."""
+    H, W = int(rgb.shape[0]), int(rgb.shape[1])
+    nb = (H // 8) * (W // 8)
+    nbc = chroma_blocks(W, 0, H // 8, sample_ratio, flags)
+    shape = (nb + 2 * nbc, 64) if flags & FLAG_SUBSAMPLE else (3, nb, 64)
     if isinstance(rgb, np.ndarray):
         rgb = np.ascontiguousarray(rgb, np.uint8)
-        H, W = rgb.shape[:2]
         p = default_params(W, H, quality, sample_ratio, underflow, flags)
-        out = np.empty((3, (H // 8) * (W // 8), 64), np.int16)
+        out = np.empty(shape, np.int16)
         dev = 0 if device is None else int(device)
         _check(lib.jpgx_blocks(rgb.ctypes.data, W, H, W * 3, ctypes.byref(p), out.ctypes.data,
                                dev), "jpgx_blocks")
@@ -233,7 +251,8 @@ def encode_blocks(rgb, quality: int, sample_ratio: int = 0, underflow: bytes | N
     p = default_params(W, H, quality, sample_ratio, underflow, flags)
     _check(validate(W, H, p), "jpgx_validate")
     fr = frames(W, H)
-    out = torch.empty((3, (H // 8) * (W // 8), 64), dtype=torch.int16, device=rgb.device)
+    fr.out_frame_stride = shape[0] * 64 if flags & FLAG_SUBSAMPLE else 3 * nb * 64
+    out = torch.empty(shape, dtype=torch.int16, device=rgb.device)
     ws = torch.empty(workspace_size(fr), dtype=torch.uint8, device=rgb.device)
     blocks_gpu(fr, p, rgb.contiguous(), out, ws)
     return out
@@ -245,7 +264,9 @@ def encode_blocks_multi(rgb: np.ndarray, quality: int, ngpus: int, sample_ratio:
     rgb = np.ascontiguousarray(rgb, np.uint8)
     H, W = rgb.shape[:2]
     p = default_params(W, H, quality, sample_ratio, underflow, flags)
-    out = np.empty((3, (H // 8) * (W // 8), 64), np.int16)
+    nb = (H // 8) * (W // 8)
+    nbc = chroma_blocks(W, 0, H // 8, sample_ratio, flags)
+    out = np.empty((nb + 2 * nbc, 64) if flags & FLAG_SUBSAMPLE else (3, nb, 64), np.int16)
     _check(lib.jpgx_blocks_multi(rgb.ctypes.data, W, H, W * 3, ctypes.byref(p), out.ctypes.data,
                                  ngpus), "jpgx_blocks_multi")
     return out

@@ -201,6 +201,73 @@ int cpuref_blocks_rows(const uint8_t *rgb, int W, int H, size_t pitch, int quali
     return 0;
 }
 
+/* ---- true chroma subsampling (extension; the reference's stubs print only) ------------- */
+/* Level-shifted chroma of one pixel, the reference's double arithmetic (preprocess.c:161-162,
+ * 186-188). */
+static double chroma_ls(int ch, const uint8_t *p)
+{
+    const int r = p[0], g = p[1], b = p[2];
+    if (ch == 1) {
+        const double cb = 128 - (0.168736 * r - 0.331264 * g + 0.5 * b);
+        return cb - 128;
+    }
+    const double cr = 128 + (0.5 * r - 0.418688 * g - 0.081312 * b);
+    return cr - 128;
+}
+
+/* Chroma sample (X, Y) of the subsampled plane: the level-shifted values (Notes: "level shift
+ * before chroma subsample") averaged as (p0 + p1) * 0.5 over the horizontal pair (4:2:2) or
+ * ((p00 + p01) + (p10 + p11)) * 0.25 over the 2x2 quad (4:2:0), in double. */
+double cpuref_chroma_sample(const uint8_t *rgb, size_t pitch, int sample_ratio, int ch, long X,
+                            long Y)
+{
+    if (sample_ratio == 1) {
+        const uint8_t *p = rgb + (size_t)Y * pitch + (size_t)(2 * X) * 3;
+        return (chroma_ls(ch, p) + chroma_ls(ch, p + 3)) * 0.5;
+    }
+    const uint8_t *p = rgb + (size_t)(2 * Y) * pitch + (size_t)(2 * X) * 3;
+    const uint8_t *q = p + pitch;
+    return ((chroma_ls(ch, p) + chroma_ls(ch, p + 3)) + (chroma_ls(ch, q) + chroma_ls(ch, q + 3))) *
+           0.25;
+}
+
+int cpuref_chroma_sub_rows(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
+                           int sample_ratio, int mode, int nthreads, int crow_begin,
+                           int crow_end, int16_t *out)
+{
+    if (sample_ratio != 1 && sample_ratio != 2) return -3;
+    int err = validate(W, H, quality, sample_ratio);
+    if (err) return err;
+    const int Wc = W / 2, Hc = sample_ratio == 2 ? H / 2 : H;
+    if (crow_begin < 0 || crow_end > Hc / 8 || crow_begin > crow_end) return -1;
+    int qt[8][8];
+    cpuref_scale_table(cpuref_q_chr, quality, qt);
+    cos_init();
+    const long bpr = Wc / 8;
+    const long nb_out = (long)(crow_end - crow_begin) * bpr;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 64) if (nthreads != 1)
+#endif
+    for (long i = 0; i < nb_out; i++) {
+        const long by = crow_begin + i / bpr, bx = i % bpr;
+        for (int ch = 1; ch <= 2; ch++) {
+            double X[64];
+            for (int y = 0; y < 8; y++)
+                for (int x = 0; x < 8; x++)
+                    X[y * 8 + x] = cpuref_chroma_sample(rgb, pitch, sample_ratio, ch, 8 * bx + x,
+                                                        8 * by + y);
+            int16_t *o = out + ((long)(ch - 1) * nb_out + i) * 64;
+            for (int u = 0; u < 8; u++)
+                for (int v = 0; v < 8; v++) {
+                    const double F = dct_coef(X, u, v, mode);
+                    o[cpuref_scan_order[v][u]] = (int16_t)(int)round(F / qt[u][v]);
+                }
+        }
+    }
+    return 0;
+}
+
 int cpuref_blocks(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
                   int sample_ratio, const uint8_t underflow[3][8], int mode, int nthreads,
                   int16_t *out)

@@ -72,6 +72,22 @@ int cpuref_blocks(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
                   int sample_ratio, const uint8_t underflow[3][8], int mode, int nthreads,
                   int16_t *out);
 
+/*
+ * True chroma subsampling (EXTENSION: the reference's subsample_422/420, downsample.c:24-32,
+ * only print; this restatement DEFINES the semantics, parity with the reference is unpinned).
+ * Chroma samples are the level-shifted Cb/Cr of preprocess.c:161-162 in double, averaged over
+ * the horizontal pixel pair (sample_ratio 1, 4:2:2) or the 2x2 quad (2, 4:2:0) as
+ * cpuref_chroma_sample states; the (W/2) x H or (W/2) x (H/2) planes are tiled in raster order
+ * with the standard tiling (the x0 = -8 quirk belongs to the 4:4:4 convert_blocks only); DCT,
+ * transposed chroma quantisation and zig-zag as for 4:4:4.  out: int16 [2][nbc][64] (Cb, Cr)
+ * for chroma block-rows [crow_begin, crow_end).
+ */
+double cpuref_chroma_sample(const uint8_t *rgb, size_t pitch, int sample_ratio, int ch, long X,
+                            long Y);
+int cpuref_chroma_sub_rows(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
+                           int sample_ratio, int mode, int nthreads, int crow_begin,
+                           int crow_end, int16_t *out);
+
 /* dpcm.c:6-21 on one channel's [nb][64] int array (in place, alternating recurrence). */
 void cpuref_dpcm_i32(int32_t *zz, long nb);
 

@@ -52,6 +52,14 @@ def lib() -> ctypes.CDLL:
         L.cpuref_scale_table.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_int)]
         L.cpuref_dpcm_i32.argtypes = [ctypes.POINTER(ctypes.c_int32), ctypes.c_long]
+        L.cpuref_chroma_sub_rows.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_int16)]
+        L.cpuref_chroma_sub_rows.restype = ctypes.c_int
+        L.cpuref_chroma_sample.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_long, ctypes.c_long]
+        L.cpuref_chroma_sample.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -102,6 +110,23 @@ def blocks(rgb: np.ndarray, quality: int, sample_ratio: int = 0, underflow=None,
                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)))
     if rc != 0:
         raise ValueError(f"cpuref_blocks_rows failed: {rc}")
+    return out
+
+
+def chroma_sub(rgb: np.ndarray, quality: int, sample_ratio: int, mode: int = MODE_TABLE,
+               nthreads: int = 0, crows: tuple[int, int] | None = None) -> np.ndarray:
+    """int16 [2][nbc][64]: true 4:2:2 (sample_ratio 1) / 4:2:0 (2) Cb, Cr blocks (EXTENSION,
+    semantics defined by cpu_ref.h, parity with the reference unpinned)."""
+    H, W = rgb.shape[0], rgb.shape[1]
+    rgb = np.ascontiguousarray(rgb)
+    Hc = H // 2 if sample_ratio == 2 else H
+    r0, r1 = crows if crows is not None else (0, Hc // 8)
+    nbc = max(r1 - r0, 0) * (W // 16)
+    out = np.empty((2, nbc, 64), np.int16)
+    rc = lib().cpuref_chroma_sub_rows(_u8(rgb), W, H, W * 3, quality, sample_ratio, mode, nthreads,
+                                      r0, r1, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)))
+    if rc != 0:
+        raise ValueError(f"cpuref_chroma_sub_rows failed: {rc}")
     return out
 
 
