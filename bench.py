@@ -119,14 +119,15 @@ def measured_traffic():
     return None, None
 
 
-def rank_plan(W, H, frames_per_gpu, world, rank, jpgx):
+def rank_plan(W, H, frames_per_gpu, world, rank, jpgx, unit=1):
     """What rank `rank` of `world` holds: its block-row stripe [r0, r1) of every frame of the
     global batch (weak scaling: frames_per_gpu * world frames), the one-pixel-row halo above a
     stripe that does not start at row 0 (the x0 = -8 quirk reads it), and the splitmix seed
     that makes the rank's bytes equal to the same rows of the global frame (byte k of a frame
     is mix(seed + (k+1)*C), so starting at byte k0 is seed + k0*C)."""
     B = frames_per_gpu * world
-    r0, r1 = jpgx.stripe(H // 8, world, rank)
+    r0, r1 = jpgx.stripe(H // 8 // unit, world, rank)     # unit 2: true 4:2:0 MCU rows
+    r0, r1 = r0 * unit, r1 * unit
     halo = 1 if r0 > 0 else 0
     row_bytes = W * 3
     rows_px = (r1 - r0) * 8 + halo
@@ -160,6 +161,9 @@ def main():
     ap.add_argument("--sample-ratio", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--subsample", action="store_true",
+                    help="true 4:2:2 / 4:2:0 chroma (JPGX_FLAG_SUBSAMPLE, an extension; needs "
+                         "--sample-ratio 1 or 2): not the headline metric")
     ap.add_argument("--event-every", type=int, default=4,
                     help="record kernel-timing events on every k-th timed step")
     args = ap.parse_args()
@@ -180,7 +184,11 @@ def main():
     N = world
 
     W, H, q = args.width, args.height, args.quality
-    plan = rank_plan(W, H, args.frames_per_gpu, N, rank, jpgx)
+    flags = jpgx.FLAG_SUBSAMPLE if args.subsample else 0
+    if args.subsample and args.sample_ratio not in (1, 2):
+        raise SystemExit("--subsample needs --sample-ratio 1 or 2")
+    unit = 2 if args.subsample and args.sample_ratio == 2 else 1
+    plan = rank_plan(W, H, args.frames_per_gpu, N, rank, jpgx, unit)
     B, r0, r1, halo = plan["B"], plan["r0"], plan["r1"], plan["halo"]
     row_bytes, fstride, nb = plan["row_bytes"], plan["fstride"], plan["nb"]
 
@@ -188,11 +196,14 @@ def main():
     d_in = torch.empty(B * fstride, dtype=torch.uint8, device=dev)
     for f in range(B):
         jpgx.gen_splitmix_gpu(d_in[f * fstride:(f + 1) * fstride], plan["seeds"][f])
-    d_out = torch.empty((B, 3, nb, 64), dtype=torch.int16, device=dev)
+    nbc = jpgx.chroma_blocks(W, r0, r1, args.sample_ratio, flags)
+    per = nb + 2 * nbc                                   # blocks per frame stripe output
+    bytes_per_px = 3 + 2 * per / max(nb, 1)              # 9 for 4:4:4; 7 / 6 true 4:2:2 / 4:2:0
+    d_out = torch.empty((B, per, 64), dtype=torch.int16, device=dev)
     fr = jpgx.frames(W, H, nframes=B, rows=(r0, r1), in_pitch=row_bytes, in_frame_stride=fstride,
-                     out_frame_stride=3 * nb * 64)
+                     out_frame_stride=per * 64)
     d_ws = torch.empty(jpgx.workspace_size(fr), dtype=torch.uint8, device=dev)
-    params = jpgx.default_params(W, H, q, args.sample_ratio)
+    params = jpgx.default_params(W, H, q, args.sample_ratio, flags=flags)
     rgb_ptr = d_in.data_ptr() + halo * row_bytes
     torch.cuda.synchronize()
 
@@ -235,31 +246,36 @@ def main():
     px_total = B * W * H * args.steps                 # all ranks
     value = px_total / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
-    achieved = BYTES_PER_PX * px_rank_step / (xform_ms * 1e-3) / 1e9
+    achieved = bytes_per_px * px_rank_step / (xform_ms * 1e-3) / 1e9
 
     if rank == 0:
-        t_ratio, t_src = measured_traffic()
+        t_ratio, t_src = measured_traffic() if not args.subsample else (None, None)
         cpu = None
         if N == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(W, H, q, args.cpu_seconds, jpgx)
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "Mpixels/s", "n_gpus": N,
+            "metric": METRIC if not args.subsample else
+                      f"Mpixels/sec RGB->quantised-coeff, true {'4:2:2' if args.sample_ratio == 1 else '4:2:0'} "
+                      f"q={q} (extension, not the headline)",
+            "value": round(value, 1), "unit": "Mpixels/s", "n_gpus": N,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (splitmix64 RGB frames generated in HBM)",
             "config": {"workload": f"{args.frames_per_gpu} x {W}x{H} RGB frames per GPU, "
-                                   f"4:4:4, q={q}, block-row stripes",
+                                   f"{['4:4:4', 'true 4:2:2', 'true 4:2:0'][args.sample_ratio] if args.subsample else '4:4:4'}"
+                                   f", q={q}, block-row stripes",
                        "global_batch_frames": B, "width": W, "height": H, "quality": q,
                        "sample_ratio": args.sample_ratio, "parallelism": f"stripes{N}",
                        "exact_pass_ms_per_step": round(fix_ms, 4),
                        "kernel_event_samples": len(evs)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": (round(t_ratio * BYTES_PER_PX * px_rank_step)
+                         "traffic": (round(t_ratio * bytes_per_px * px_rank_step)
                                      if t_ratio else None),
                          "traffic_source": t_src,
-                         "kernel": "k_xform", "kernel_ms": round(xform_ms, 4),
-                         "bytes_per_launch": BYTES_PER_PX * px_rank_step},
+                         "kernel": "k_xform" if not args.subsample else "k_xform(Y)+k_chroma",
+                         "kernel_ms": round(xform_ms, 4),
+                         "bytes_per_launch": bytes_per_px * px_rank_step},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

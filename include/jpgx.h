@@ -132,6 +132,20 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
                        int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream,
                        void *event_between);
 
+/* Entropy-stage statistics on the device: over one image's coefficients
+ * d_coef = Y [nb_y][64] | Cb [nb_c][64] | Cr [nb_c][64] (what jpgx_blocks_gpu writes; nb_c =
+ * nb_y unless JPGX_FLAG_SUBSAMPLE), the reference's in-place DC recurrence (src/dpcm.c:6-21)
+ * into d_dc[nb_y + 2 nb_c] (int32), and huffman_encode's frequency pass (src/huffman.c:23-44,
+ * 182-235; construct_huffman_table excluded) into d_hist[4][257] (uint32: lum_DC, lum_AC,
+ * chrom_DC, chrom_AC; freq[256] = 1 as initialize_huffman reserves it; AC symbols keep the
+ * reference's `run | size`).  carry (host, may be NULL = image start): per channel the last
+ * dpcm'd DC of the blocks before these (jpgx_dpcm_dc semantics), for stripes.  Workspace:
+ * jpgx_entropy_workspace_size() bytes, 8-byte aligned.  Asynchronous on `stream`. */
+size_t jpgx_entropy_workspace_size(size_t nb_y, size_t nb_c);
+int jpgx_entropy_stats_gpu(const int16_t *d_coef, size_t nb_y, size_t nb_c, const int32_t *carry,
+                           int32_t *d_dc, uint32_t *d_hist, void *d_workspace,
+                           size_t workspace_bytes, void *stream);
+
 /* Synthetic frames, generated directly in device memory (SURVEY.md 8c generator G: byte k
  * of the buffer = splitmix64(seed + (k+1)*0x9E3779B97F4A7C15) >> 56). */
 int jpgx_gen_splitmix_gpu(uint8_t *d_dst, size_t nbytes, uint64_t seed, void *stream);

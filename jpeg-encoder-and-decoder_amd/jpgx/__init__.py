@@ -38,7 +38,8 @@ EXPORTS = [
     "jpgx_guard_band", "jpgx_workspace_size", "jpgx_blocks_gpu", "jpgx_blocks_gpu_ev",
     "jpgx_gen_splitmix_gpu",
     "jpgx_gen_tie_gpu", "jpgx_blocks", "jpgx_blocks_multi", "jpgx_stripe",
-    "jpgx_device_count", "jpgx_version", "jpgx_chroma_blocks",
+    "jpgx_device_count", "jpgx_version", "jpgx_chroma_blocks", "jpgx_entropy_workspace_size",
+    "jpgx_entropy_stats_gpu",
 ]
 COMPAT_EXPORTS = [
     "jpgx_new_block", "jpgx_get_value_block", "jpgx_set_value_block", "jpgx_copy_block",
@@ -100,6 +101,9 @@ def _load() -> ctypes.CDLL:
     L.jpgx_device_count.argtypes = []
     L.jpgx_chroma_blocks.argtypes = [i, i, i, i, ctypes.c_uint]
     L.jpgx_chroma_blocks.restype = sz
+    L.jpgx_entropy_workspace_size.argtypes = [sz, sz]
+    L.jpgx_entropy_workspace_size.restype = sz
+    L.jpgx_entropy_stats_gpu.argtypes = [vp, sz, sz, vp, vp, vp, vp, sz, vp]
     L.jpgx_version.restype = ctypes.c_char_p
     return L
 
@@ -222,6 +226,25 @@ def chroma_blocks(width: int, row_begin: int, row_end: int, sample_ratio: int = 
                   flags: int = 0) -> int:
     """Chroma blocks per channel of a stripe (== luma blocks unless FLAG_SUBSAMPLE)."""
     return int(lib.jpgx_chroma_blocks(width, row_begin, row_end, sample_ratio, flags))
+
+
+def entropy_stats_gpu(d_coef, nb_y: int, nb_c: int, carry=None, stream=None):
+    """(dc int32 [nb_y + 2 nb_c], hist uint32 [4][257]) device tensors: the reference's dpcm and
+    huffman_encode frequency pass over d_coef (torch int16 tensor, Y|Cb|Cr blocks)."""
+    import torch
+    dev = d_coef.device
+    dc = torch.empty(nb_y + 2 * nb_c, dtype=torch.int32, device=dev)
+    hist = torch.empty((4, 257), dtype=torch.int32, device=dev)
+    ws = torch.empty(max(int(lib.jpgx_entropy_workspace_size(nb_y, nb_c)), 8), dtype=torch.uint8,
+                     device=dev)
+    cy = None
+    if carry is not None:
+        cy = (ctypes.c_int32 * 3)(*[int(x) for x in carry])
+    _check(lib.jpgx_entropy_stats_gpu(d_coef.data_ptr(), nb_y, nb_c,
+                                      ctypes.cast(cy, ctypes.c_void_p) if cy is not None else None,
+                                      dc.data_ptr(), hist.data_ptr(), ws.data_ptr(), ws.numel(),
+                                      _stream_ptr(stream)), "jpgx_entropy_stats_gpu")
+    return dc, hist
 
 
 def split_sub(out, nb: int, nbc: int):

@@ -268,6 +268,68 @@ int cpuref_chroma_sub_rows(const uint8_t *rgb, int W, int H, size_t pitch, int q
     return 0;
 }
 
+/* ---- entropy-stage statistics (dpcm.c:6-21, huffman.c:23-44,182-235) ------------------- */
+static int get_class(int value)             /* huffman.c:226-235 */
+{
+    int c = 0;
+    value = abs(value);
+    while (value > 0) {
+        value >>= 1;
+        c++;
+    }
+    return c;
+}
+
+static void freq_ac(int32_t *freq, const int *zz)   /* huffman.c:187-222, '|' quirk kept */
+{
+    int last = 0, zeros = 0;
+    for (int i = 63; i > 0; i--)
+        if (zz[i] != 0) {
+            last = i;
+            break;
+        }
+    for (int i = 1; i < 64; i++) {
+        if (i == last + 1) {
+            freq[0x00]++;                        /* EOB */
+            break;
+        }
+        if (zz[i] == 0) {
+            if (++zeros == 16) {
+                freq[0xF0]++;                    /* ZRL */
+                zeros = 0;
+            }
+        } else {
+            freq[zeros | get_class(zz[i])]++;    /* the reference ORs, not (run << 4) */
+            zeros = 0;
+        }
+    }
+}
+
+void cpuref_entropy_stats(const int16_t *coef, long nb_y, long nb_c, int32_t *dc,
+                          int32_t hist[4][257])
+{
+    for (int t = 0; t < 4; t++) {                /* initialize_huffman, huffman.c:52-75 */
+        for (int k = 0; k < 256; k++) hist[t][k] = 0;
+        hist[t][256] = 1;
+    }
+    long off = 0;
+    for (int ch = 0; ch < 3; ch++) {
+        const long nb = ch == 0 ? nb_y : nb_c;
+        int prev = 0;
+        for (long i = 0; i < nb; i++) {
+            int zz[64];
+            for (int k = 0; k < 64; k++) zz[k] = coef[(off + i) * 64 + k];
+            const int d = i == 0 ? zz[0] : zz[0] - prev;     /* dpcm.c:10-20, in place */
+            prev = d;
+            zz[0] = d;
+            dc[off + i] = d;
+            hist[ch == 0 ? 0 : 2][get_class(d)]++;           /* calculate_freq_block_DC */
+            freq_ac(hist[ch == 0 ? 1 : 3], zz);               /* calculate_freq_block_AC */
+        }
+        off += nb;
+    }
+}
+
 int cpuref_blocks(const uint8_t *rgb, int W, int H, size_t pitch, int quality,
                   int sample_ratio, const uint8_t underflow[3][8], int mode, int nthreads,
                   int16_t *out)

@@ -88,6 +88,18 @@ int cpuref_chroma_sub_rows(const uint8_t *rgb, int W, int H, size_t pitch, int q
                            int sample_ratio, int mode, int nthreads, int crow_begin,
                            int crow_end, int16_t *out);
 
+/*
+ * Entropy-stage statistics of one image: coef = Y [nb_y][64] | Cb [nb_c][64] | Cr [nb_c][64]
+ * (zig-zag int16, the hot path's output).  dc[nb_y + 2 nb_c] = every block's DC after the
+ * reference's in-place dpcm recurrence (dpcm.c:10-20); hist = the four freq[257] tables
+ * lum_DC | lum_AC | chrom_DC | chrom_AC exactly as huffman_encode fills them before it calls
+ * construct_huffman_table (huffman.c:23-44, 52-75, 182-235: freq[256] = 1 reserved, DC by
+ * class of the dpcm'd value, AC run/size symbols with the reference's `run | size` (not
+ * run << 4 | size), ZRL 0xF0, EOB 0x00 unless the last coefficient is non-zero).
+ */
+void cpuref_entropy_stats(const int16_t *coef, long nb_y, long nb_c, int32_t *dc,
+                          int32_t hist[4][257]);
+
 /* dpcm.c:6-21 on one channel's [nb][64] int array (in place, alternating recurrence). */
 void cpuref_dpcm_i32(int32_t *zz, long nb);
 

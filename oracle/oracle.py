@@ -60,6 +60,10 @@ def lib() -> ctypes.CDLL:
         L.cpuref_chroma_sample.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_long, ctypes.c_long]
         L.cpuref_chroma_sample.restype = ctypes.c_double
+        L.cpuref_entropy_stats.argtypes = [ctypes.POINTER(ctypes.c_int16), ctypes.c_long,
+                                           ctypes.c_long, ctypes.POINTER(ctypes.c_int32),
+                                           ctypes.POINTER(ctypes.c_int32)]
+        L.cpuref_entropy_stats.restype = None
         _lib = L
     return _lib
 
@@ -128,6 +132,20 @@ def chroma_sub(rgb: np.ndarray, quality: int, sample_ratio: int, mode: int = MOD
     if rc != 0:
         raise ValueError(f"cpuref_chroma_sub_rows failed: {rc}")
     return out
+
+
+def entropy_stats(coef: np.ndarray, nb_y: int | None = None, nb_c: int | None = None):
+    """(dc int32 [nb_y + 2 nb_c], hist int32 [4][257]) of huffman.c's frequency pass over
+    the dpcm'd blocks (cpu_ref.h).  coef: [3][nb][64] or a flat [nb_y + 2 nb_c][64]."""
+    c = np.ascontiguousarray(coef, np.int16).reshape(-1, 64)
+    if nb_y is None:
+        nb_y = nb_c = c.shape[0] // 3
+    dc = np.empty(nb_y + 2 * nb_c, np.int32)
+    hist = np.empty((4, 257), np.int32)
+    lib().cpuref_entropy_stats(c.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)), nb_y, nb_c,
+                               dc.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                               hist.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return dc, hist
 
 
 def bmp_decode(data: bytes) -> np.ndarray:

@@ -1,0 +1,139 @@
+"""Entropy-stage statistics: the reference's DC recurrence (src/dpcm.c:6-21)
+and huffman_encode's frequency pass (src/huffman.c:23-44, 182-235).  The oracle restatement is
+pinned against the REAL reference's frequency tables (tests/golden/entropy_stats.json, made by
+tests/golden/make_entropy_golden.py from the compiled reference); the GPU kernels
+(jpgx_entropy_stats_gpu) must match the oracle exactly (integer work)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import jpgx
+import oracle as O
+from conftest import GOLDEN
+
+
+def _cases():
+    return json.load(open(os.path.join(GOLDEN, "entropy_stats.json")))["cases"]
+
+
+def _rgb(case):
+    if "image" in case:
+        return O.bmp_decode(open(os.path.join(GOLDEN, "images", f"{case['image']}.bmp"), "rb").read())
+    return O.gen_splitmix(case["seed"], case["W"], case["H"]) if case["kind"] == "G" else O.gen_tie(case["W"], case["H"])
+
+
+def _underflow(case, golden):
+    if "image" in case:
+        return golden["images"][case["image"]]["underflow"]
+    for ent in golden["synthetic"]:
+        if (ent["kind"], ent["W"], ent["H"], ent["seed"]) == (case.get("kind"), case.get("W"),
+                                                               case.get("H"), case.get("seed")):
+            return ent["underflow"]
+    return None
+
+
+def test_oracle_matches_reference_frequency_tables(golden):
+    for case in _cases():
+        if case.get("W", 0) * case.get("H", 0) > 512 * 512:
+            continue                                  # the 1080p case runs on the GPU test
+        coef = O.blocks(_rgb(case), case["q"], underflow=_underflow(case, golden))
+        dc, hist = O.entropy_stats(coef)
+        assert np.array_equal(hist, np.array(case["hist"], np.int32)), case.get("image", case.get("kind"))
+        assert hashlib.sha256(dc.astype("<i4").tobytes()).hexdigest() == case["dc_sha256"]
+
+
+def test_histogram_quirks_by_construction():
+    """Hand-made blocks: EOB only when the last AC is zero, ZRL per 16 zeros, run|size."""
+    coef = np.zeros((3, 3, 64), np.int16)
+    coef[0, 0, 0] = 5                                 # DC class 3
+    coef[0, 0, 1] = 1                                 # (0 | 1), then EOB
+    coef[0, 1, 0] = 5                                 # dpcm: 5 - 5 = 0 -> class 0
+    coef[0, 1, 20] = -3                               # 19 zeros: ZRL, then (3 | 2) = 3, EOB
+    coef[0, 2, 63] = 7                                # last AC non-zero: no EOB; 62 zeros:
+    dc, hist = O.entropy_stats(coef)                  # 3 ZRL, then (14 | 3) = 15
+    assert list(dc[:3]) == [5, 0, 0]
+    assert hist[0, 3] == 1 and hist[0, 0] == 2 and hist[0, 256] == 1
+    assert hist[1, 0x00] == 2 + 0 and hist[1, 0xF0] == 1 + 3
+    assert hist[1, 1] == 1 and hist[1, 3] == 1 and hist[1, 15] == 1
+
+
+def test_host_dpcm_matches_oracle():
+    rgb = O.gen_splitmix(9, 128, 64)
+    coef = O.blocks(rgb, 75)
+    dc, _ = O.entropy_stats(coef)
+    nb = coef.shape[1]
+    got = np.empty(3 * nb, np.int32)
+    import ctypes
+    f = jpgx.lib.jpgx_dpcm_dc
+    f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    carry = (ctypes.c_int32 * 3)(0, 0, 0)
+    assert f(coef.ctypes.data, nb, ctypes.cast(carry, ctypes.c_void_p), got.ctypes.data) == 0
+    assert np.array_equal(got, dc)
+
+
+def _gpu_stats(coef, nb_y, nb_c, cuda, carry=None):
+    import torch
+    d = torch.from_numpy(np.ascontiguousarray(coef.reshape(-1, 64))).to(cuda)
+    dc, hist = jpgx.entropy_stats_gpu(d, nb_y, nb_c, carry)
+    return dc.cpu().numpy(), hist.cpu().numpy()
+
+
+@pytest.mark.gpu
+def test_gpu_stats_golden(golden, cuda):
+    for case in _cases():
+        coef = jpgx.encode_blocks(__import__("torch").from_numpy(_rgb(case)).to(cuda), case["q"],
+                                  underflow=_underflow(case, golden)).cpu().numpy()
+        nb = coef.shape[1]
+        dc, hist = _gpu_stats(coef, nb, nb, cuda)
+        assert np.array_equal(hist, np.array(case["hist"], np.int32)), case.get("image", case.get("kind"))
+        assert hashlib.sha256(dc.astype("<i4").tobytes()).hexdigest() == case["dc_sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,q", [(8, 8, 50), (40, 16, 90), (1920, 1080, 75), (3840, 2160, 90)])
+def test_gpu_stats_vs_oracle(cuda, W, H, q):
+    rgb = O.gen_splitmix(W + q, W, H)
+    coef = jpgx.encode_blocks(__import__("torch").from_numpy(rgb).to(cuda), q).cpu().numpy()
+    nb = coef.shape[1]
+    dc, hist = _gpu_stats(coef, nb, nb, cuda)
+    rdc, rhist = O.entropy_stats(coef)
+    assert np.array_equal(dc, rdc)
+    assert np.array_equal(hist, rhist)
+
+
+@pytest.mark.gpu
+def test_gpu_stats_stripes_with_carry(cuda):
+    """Two stripes with the first one's last DCs carried in: the second stripe's dc equals the
+    whole image's; its histogram plus the first's (minus one reserved count) equals the whole."""
+    rgb = O.gen_splitmix(77, 640, 480)
+    coef = O.blocks(rgb, 90)
+    nb = coef.shape[1]
+    dc_all, hist_all = O.entropy_stats(coef)
+    s = (480 // 8 // 2) * (640 // 8)
+    a, b = coef[:, :s], coef[:, s:]
+    dca, ha = _gpu_stats(a, s, s, cuda)
+    carry = [int(dca[c * s + s - 1]) for c in range(3)]
+    dcb, hb = _gpu_stats(b, nb - s, nb - s, cuda, carry)
+    want_b = np.concatenate([dc_all[c * nb + s:(c + 1) * nb] for c in range(3)])
+    assert np.array_equal(dcb, want_b)
+    tot = ha.astype(np.int64) + hb
+    tot[:, 256] -= 1
+    assert np.array_equal(tot, hist_all)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sr", [1, 2])
+def test_gpu_stats_subsampled_layout(cuda, sr):
+    import torch
+    W, H = 256, 128
+    rgb = O.gen_splitmix(5, W, H)
+    out = jpgx.encode_blocks(torch.from_numpy(rgb).to(cuda), 75, sr, flags=jpgx.FLAG_SUBSAMPLE)
+    nb = (H // 8) * (W // 8)
+    nbc = jpgx.chroma_blocks(W, 0, H // 8, sr, jpgx.FLAG_SUBSAMPLE)
+    dc, hist = jpgx.entropy_stats_gpu(out, nb, nbc)
+    rdc, rhist = O.entropy_stats(out.cpu().numpy(), nb, nbc)
+    assert np.array_equal(dc.cpu().numpy(), rdc)
+    assert np.array_equal(hist.cpu().numpy(), rhist)
