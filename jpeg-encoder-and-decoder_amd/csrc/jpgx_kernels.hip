@@ -434,11 +434,13 @@ __device__ __forceinline__ void store_and_queue(const int CH, const jx_xform_arg
 #pragma unroll
         for (int j = 0; j < 8; j++) jx_store(dst + (unsigned)j * 64u + lane, unit[j]);
     } else {                                   /* tile crosses a frame end or the last tile */
+        /* units past the end hold block total-1's coefficients (inactive lanes computed the
+         * clamped block): they are written there again, identical bytes, so every path issues
+         * the same 8 stores (which the vmcnt accounting of JX_PREFETCH 2 relies on) */
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            const unsigned e = (unsigned)j * 64u + lane, bb = b0 + (e >> 3);
-            if (bb < total)
-                jx_store((u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8), stage_unit(W, e));
+            const unsigned e = (unsigned)j * 64u + lane, bb = std::min(b0 + (e >> 3), total - 1u);
+            jx_store((u32x4 *)coef_ptr(g, bb, CH, (int)(e & 7) * 8), stage_unit(W, e));
         }
     }
     /* some lane has a coefficient inside the guard band (about 40% of the channel-tiles of
@@ -1017,7 +1019,9 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
     const unsigned ntiles = (total + 63u) / 64u;
     const unsigned lane = threadIdx.x & 63u;
     const unsigned nwaves = gridDim.x * (JX_WG / 64);
-    unsigned t = blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6);
+    /* wave-uniform (readfirstlane: the compiler cannot see that threadIdx.x >> 6 is), so the
+     * tile loop and its branches are scalar */
+    unsigned t = __builtin_amdgcn_readfirstlane(blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6));
     const unsigned wave = t;
     if (t >= ntiles) {                             /* whole wave: nothing to queue */
         if (!JX_DBG_NO_EXACT && lane < 3) a.fix.count[lane * a.fix.nwaves + wave] = 0;
@@ -1033,6 +1037,10 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
     }
 #if JX_PREFETCH == 2
     __builtin_amdgcn_s_waitcnt(0xF70);              /* vmcnt(0): same state as the back edge */
+#pragma unroll
+    for (int y = 0; y < 8; y++)
+#pragma unroll
+        for (int k = 0; k < 6; k++) asm volatile("" : "+v"(raw[y][k]));
 #endif
 #endif
     for (; t < ntiles; t += nwaves) {
@@ -1140,6 +1148,12 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
          * them: vmcnt counts loads and stores in order, and without this explicit count the
          * wait at the loop head is vmcnt(0), which also drains those stores every tile */
         __builtin_amdgcn_s_waitcnt(0xF78);          /* vmcnt(8), expcnt/lgkmcnt: no wait */
+        /* re-define raw here: at the loop head it then comes from this (already waited) point
+         * on both paths, not from loads the wait analysis would drain the stores for */
+#pragma unroll
+        for (int y = 0; y < 8; y++)
+#pragma unroll
+            for (int k = 0; k < 6; k++) asm volatile("" : "+v"(raw[y][k]));
 #endif
 #endif
 #if JX_FUSED_FIX
@@ -1289,7 +1303,9 @@ __global__ __launch_bounds__(JX_WG, 3) void k_chroma(const jx_xform_args a)
     const unsigned ntiles = (total + 63u) / 64u;
     const unsigned lane = threadIdx.x & 63u;
     const unsigned nwaves = gridDim.x * (JX_WG / 64);
-    unsigned t = blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6);
+    /* wave-uniform (readfirstlane: the compiler cannot see that threadIdx.x >> 6 is), so the
+     * tile loop and its branches are scalar */
+    unsigned t = __builtin_amdgcn_readfirstlane(blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6));
     if (t >= ntiles) return;
     WaveLds &W = s_wave[threadIdx.x >> 6];
     Queue Q{{0, 0, 0}, {0u, 0u, 0u}};
@@ -1517,7 +1533,9 @@ __global__ __launch_bounds__(JX_WG, JX_K2_WPE) void k_xform2(const jx_xform_args
     const unsigned ntiles = (total + 31u) / 32u;
     const unsigned lane = threadIdx.x & 63u, h = lane >> 5, bl = lane & 31u;
     const unsigned nwaves = gridDim.x * (JX_WG / 64);
-    unsigned t = blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6);
+    /* wave-uniform (readfirstlane: the compiler cannot see that threadIdx.x >> 6 is), so the
+     * tile loop and its branches are scalar */
+    unsigned t = __builtin_amdgcn_readfirstlane(blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6));
     if (t >= ntiles) return;
     WaveLds2 &W = s_wave[threadIdx.x >> 6];
     int qn[3] = {0, 0, 0};
