@@ -43,6 +43,8 @@ struct jx_limtab {
     float limcol[3][8];     /* [ch][u]: min over v (one limit per column, JX_FLAG_MODE 3)  */
     float lsq[3][4][8][2];  /* packed path: a float <= lim^2 (or -1 where lim < 0), pair
                                order as jx_qtab.wp: flag when d*d - lsq >= 0                */
+    float lsqn[3][8][8];    /* [ch][u][v]: a float <= lim^2 (-1 where lim < 0): the packed
+                               band test d*d - lsqn >= 0 of JX_FLAG_MODE 4                  */
     float limh[3][4][8];    /* two-lane kernel: [ch][k][v] = min(lim(k,v), lim(4+k,v)), one
                                band for the two half-waves (columns k and 4+k)             */
 };

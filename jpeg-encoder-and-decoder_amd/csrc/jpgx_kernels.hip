@@ -148,6 +148,7 @@ __constant__ jx_limtab g_limsub[2][2][JX_MAXQ + 1];
 constexpr double kAlpha0 = JX_ALPHA0;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 #ifndef JX_NT_STORE     /* coefficient stores with the nontemporal bit (streamed, never re-read) */
@@ -473,7 +474,7 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
     const jx_limtab &band = a.sub ? g_limsub[a.sub - 1][fe][a.quality] : g_lim[fe][a.quality];
     /* wave mask of lanes with a coefficient of this channel inside the guard band */
     uint64_t seen = 0;
-#if JX_FLAG_MODE == 1 || JX_FLAG_MODE == 3
+#if JX_FLAG_MODE == 1 || JX_FLAG_MODE == 3 || JX_FLAG_MODE == 4
     float flagacc = -1.0f, epair = 0.0f, colmax = 0.0f;
     (void)epair;
     (void)colmax;
@@ -490,7 +491,7 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
 #pragma unroll
     for (int v = 0; v < 8; v++) {
         wc[v] = tab.w[CH][0][v];
-        lc[v] = band.lim[CH][0][v];
+        lc[v] = JX_FLAG_MODE == 4 ? band.lsqn[CH][0][v] : band.lim[CH][0][v];
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
@@ -499,16 +500,38 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
 #pragma unroll
         for (int v = 0; v < 8; v++) {
             wn[v] = JX_TPF && u < 7 ? tab.w[CH][u + 1][v] : 0.0f;
-            ln[v] = JX_TPF && u < 7 ? band.lim[CH][u + 1][v] : 0.0f;
+            ln[v] = JX_TPF && u < 7 ? (JX_FLAG_MODE == 4 ? band.lsqn[CH][u + 1][v]
+                                                         : band.lim[CH][u + 1][v])
+                                    : 0.0f;
             if (!JX_TPF) {
                 wc[v] = tab.w[CH][u][v];
-                lc[v] = band.lim[CH][u][v];
+                lc[v] = JX_FLAG_MODE == 4 ? band.lsqn[CH][u][v] : band.lim[CH][u][v];
             }
         }
         float col[8], F[8];
 #pragma unroll
         for (int y = 0; y < 8; y++) col[y] = T[y][u];
         jx_fdct8<FOps>(col, F);
+#if JX_FLAG_MODE == 4
+        /* quantiser and band test two coefficients (v, v+1) per v_pk_*_f32: tm, rint and d are
+         * lane for lane quant_coef's values; the test d*d - lsq >= 0 (lsq <= lim^2) flags every
+         * coefficient |d| >= lim flags, into one running max per lane (no compare, no SALU) */
+#pragma unroll
+        for (int v = 0; v < 8; v += 2) {
+            const f2 Fp = f2{F[v], F[v + 1]}, wp = f2{wc[v], wc[v + 1]};
+            const f2 M2 = f2{kMagic, kMagic};
+            const f2 tm = __builtin_elementwise_fma(Fp, wp, M2);
+            ((uint16_t *)W.stage)[lane * 66 + zz_of(v, u)] = (uint16_t)__float_as_uint(tm.x);
+            ((uint16_t *)W.stage)[lane * 66 + zz_of(v + 1, u)] = (uint16_t)__float_as_uint(tm.y);
+            if (!JX_DBG_NO_EXACT) {
+                const f2 rr = tm - M2;
+                const f2 d = __builtin_elementwise_fma(Fp, wp, -rr);
+                const f2 e = __builtin_elementwise_fma(d, d, -f2{lc[v], lc[v + 1]});
+                flagacc = __builtin_fmaxf(flagacc, __builtin_fmaxf(e.x, e.y));
+            }
+        }
+        if (false)
+#endif
 #pragma unroll
         for (int v = 0; v < 8; v++) {
             float tm, d;
@@ -592,7 +615,7 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
 #ifdef JX_DBG_NO_STAGE
     W.stage[lane] = dbg_acc;
 #endif
-#if JX_FLAG_MODE == 1 || JX_FLAG_MODE == 3
+#if JX_FLAG_MODE == 1 || JX_FLAG_MODE == 3 || JX_FLAG_MODE == 4
     seen = __ballot(flagacc >= 0.0f);
 #elif JX_FLAG_MODE == 2
     seen = __ballot(flagany != 0u);
@@ -623,8 +646,6 @@ __device__ __forceinline__ void xform_cols(const int CH, float (&T)[8][8], const
 #else
 #define JX_SB_Q() ((void)0)
 #endif
-
-typedef float f2 __attribute__((ext_vector_type(2)));
 
 struct DevPair {
     typedef f2 V;
@@ -1775,6 +1796,16 @@ constexpr int kMaxDev = 64;
 std::once_flag g_tab_once[kMaxDev];
 int g_tab_rc[kMaxDev];
 
+/* a float <= lim^2 (exactly representable squares of floats fit in a double); -1 for lim < 0 */
+float lim_square_down(float lim)
+{
+    if (!(lim > 0.0f)) return -1.0f;
+    const double l2 = (double)lim * (double)lim;
+    float s = (float)l2;
+    if ((double)s > l2) s = nextafterf(s, 0.0f);
+    return s;
+}
+
 int tables_for_current_device()
 {
     int dev = 0;
@@ -1801,6 +1832,12 @@ int tables_for_current_device()
                     band[q].limcol[ch][u] = m;
                     band[JX_MAXQ + 1 + q].limcol[ch][u] = -1.0f;
                 }
+            for (int ch = 0; ch < 3; ch++)
+                for (int u = 0; u < 8; u++)
+                    for (int v = 0; v < 8; v++) {
+                        band[q].lsqn[ch][u][v] = lim_square_down(band[q].lim[ch][u][v]);
+                        band[JX_MAXQ + 1 + q].lsqn[ch][u][v] = -1.0f;
+                    }
             for (int ch = 0; ch < 3; ch++)
                 for (int k = 0; k < 4; k++)
                     for (int v = 0; v < 8; v++) {
@@ -1841,6 +1878,8 @@ int tables_for_current_device()
                         for (int v = 0; v < 8; v++) {
                             bn.lim[ch][u][v] = lim[ch][v * 8 + u];
                             bf.lim[ch][u][v] = -1.0f;
+                            bn.lsqn[ch][u][v] = lim_square_down(lim[ch][v * 8 + u]);
+                            bf.lsqn[ch][u][v] = -1.0f;
                         }
             }
         g_tab_rc[dev] = hip_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_qtab), host.data(),
