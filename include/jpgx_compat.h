@@ -159,6 +159,17 @@ size_t jpgx_jfif_bound(int width, int height);
 int jpgx_write_jfif(const int16_t *coef, int width, int height, int quality, uint8_t *out,
                     size_t cap, size_t *len);
 
+/* The same for coef = Y [nb][64] | Cb [nbc][64] | Cr [nbc][64] with sample_ratio 1 (true 4:2:2,
+ * Y sampled 2x1, MCU = 2 Y + Cb + Cr) or 2 (true 4:2:0, 2x2, MCU = 4 Y + Cb + Cr), the layout
+ * JPGX_FLAG_SUBSAMPLE produces; sample_ratio 0 is jpgx_write_jfif. */
+int jpgx_write_jfif_sub(const int16_t *coef, int width, int height, int quality,
+                        int sample_ratio, uint8_t *out, size_t cap, size_t *len);
+
+/* encode_bmp_to_jpeg with flags: JPGX_FLAG_SUBSAMPLE and sample_ratio 1/2 write a truly
+ * subsampled JFIF (extension); otherwise exactly jpgx_encode_bmp_to_jpeg.  GPU `device`. */
+int jpgx_encode_bmp_to_jpeg_ex(const char *input, const char *output, int quality,
+                               int sample_ratio, unsigned flags, int device);
+
 /* The reference's public entry point (src/headers/jpg_encode.h:85): BMP in, JPEG file out --
  * the block transform on GPU 0, then jpgx_write_jfif.  Returns 0 or a JPGX_E* code. */
 int jpgx_encode_bmp_to_jpeg(const char *input, const char *output, int quality,

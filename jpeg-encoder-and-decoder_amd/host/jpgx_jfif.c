@@ -141,12 +141,54 @@ size_t jpgx_jfif_bound(int width, int height)
     return 1024 + blocks * 2 * (13 + 63 * 26 + 7) / 8;
 }
 
+/* one block's Huffman-coded data (T.81 F.1.2): DC difference against *pred, AC run/size */
+static void encode_block(Out *o, const int16_t *z, int *pred, const HuffCodes *dc,
+                         const HuffCodes *ac)
+{
+    unsigned extra;
+    int diff = z[0] - *pred;                       /* true DC prediction */
+    if (diff > 2047) diff = 2047;                  /* (never reached: |DC| <= 1364) */
+    if (diff < -2047) diff = -2047;
+    *pred = z[0];
+    const int s = category(diff, &extra);
+    put_bits(o, dc->code[s], dc->len[s]);
+    put_bits(o, extra, s);
+    int run = 0;
+    for (int k = 1; k < 64; k++) {
+        int v = z[k];
+        if (v > 1023) v = 1023;
+        if (v < -1023) v = -1023;
+        if (v == 0) {
+            run++;
+            continue;
+        }
+        while (run > 15) {                         /* ZRL */
+            put_bits(o, ac->code[0xf0], ac->len[0xf0]);
+            run -= 16;
+        }
+        const int sa = category(v, &extra);
+        const int sym = run << 4 | sa;
+        put_bits(o, ac->code[sym], ac->len[sym]);
+        put_bits(o, extra, sa);
+        run = 0;
+    }
+    if (run) put_bits(o, ac->code[0x00], ac->len[0x00]);   /* EOB */
+}
+
 int jpgx_write_jfif(const int16_t *coef, int width, int height, int quality, uint8_t *out,
                     size_t cap, size_t *len)
 {
+    return jpgx_write_jfif_sub(coef, width, height, quality, 0, out, cap, len);
+}
+
+int jpgx_write_jfif_sub(const int16_t *coef, int width, int height, int quality,
+                        int sample_ratio, uint8_t *out, size_t cap, size_t *len)
+{
     if (!coef || !out || width <= 0 || height <= 0 || width % 8 || height % 8 ||
-        width > 65535 || height > 65535)
+        width > 65535 || height > 65535 || sample_ratio < 0 || sample_ratio > 2)
         return JPGX_EARG;
+    const int hs = sample_ratio ? 2 : 1, vs = sample_ratio == 2 ? 2 : 1;   /* Y sampling */
+    if (width % (8 * hs) || height % (8 * vs)) return JPGX_EGEOMETRY;
     int qs[2][8][8];
     if (jpgx_scale_table(0, quality, qs[0]) || jpgx_scale_table(1, quality, qs[1]))
         return JPGX_EQUALITY;
@@ -183,7 +225,7 @@ int jpgx_write_jfif(const int16_t *coef, int width, int height, int quality, uin
     put_byte(&o, 3);
     for (int c = 0; c < 3; c++) {
         put_byte(&o, (uint8_t)(c + 1));
-        put_byte(&o, 0x11);                                /* 4:4:4 */
+        put_byte(&o, (uint8_t)(c ? 0x11 : (hs << 4 | vs)));   /* 0x11, 0x21 or 0x22 */
         put_byte(&o, (uint8_t)(c ? 1 : 0));
     }
     put_dht(&o, 0x00, kDcLumBits, kDcVals);
@@ -206,45 +248,59 @@ int jpgx_write_jfif(const int16_t *coef, int width, int height, int quality, uin
     build_codes(kDcChrBits, kDcVals, &dc[1]);
     build_codes(kAcLumBits, kAcLumVals, &ac[0]);
     build_codes(kAcChrBits, kAcChrVals, &ac[1]);
-    const size_t nb = (size_t)(width / 8) * (height / 8);
+    const size_t bpr = (size_t)(width / 8), nb = bpr * (height / 8);
+    const size_t cpr = bpr / hs, nbc = cpr * (height / 8 / vs);  /* chroma planes' blocks */
     int pred[3] = {0, 0, 0};
-    for (size_t i = 0; i < nb; i++)                        /* MCU = one block per component */
-        for (int c = 0; c < 3; c++) {
-            const int16_t *z = coef + ((size_t)c * nb + i) * 64;
-            const int t = c ? 1 : 0;
-            unsigned extra;
-            int diff = z[0] - pred[c];                     /* true DC prediction */
-            if (diff > 2047) diff = 2047;                  /* (never reached: |DC| <= 1364) */
-            if (diff < -2047) diff = -2047;
-            pred[c] = z[0];
-            const int s = category(diff, &extra);
-            put_bits(&o, dc[t].code[s], dc[t].len[s]);
-            put_bits(&o, extra, s);
-            int run = 0;
-            for (int k = 1; k < 64; k++) {
-                int v = z[k];
-                if (v > 1023) v = 1023;
-                if (v < -1023) v = -1023;
-                if (v == 0) {
-                    run++;
-                    continue;
+    /* MCU: hs x vs luma blocks (raster within the MCU), then Cb, then Cr (T.81 A.2.3) */
+    for (size_t my = 0; my < (size_t)(height / 8 / vs); my++)
+        for (size_t mx = 0; mx < cpr; mx++) {
+            for (int dy = 0; dy < vs; dy++)
+                for (int dx = 0; dx < hs; dx++) {
+                    const size_t yb = (my * vs + dy) * bpr + mx * hs + dx;
+                    encode_block(&o, coef + yb * 64, &pred[0], &dc[0], &ac[0]);
                 }
-                while (run > 15) {                         /* ZRL */
-                    put_bits(&o, ac[t].code[0xf0], ac[t].len[0xf0]);
-                    run -= 16;
-                }
-                const int sa = category(v, &extra);
-                const int sym = run << 4 | sa;
-                put_bits(&o, ac[t].code[sym], ac[t].len[sym]);
-                put_bits(&o, extra, sa);
-                run = 0;
-            }
-            if (run) put_bits(&o, ac[t].code[0x00], ac[t].len[0x00]);   /* EOB */
+            const size_t cb = my * cpr + mx;
+            encode_block(&o, coef + (nb + cb) * 64, &pred[1], &dc[1], &ac[1]);
+            encode_block(&o, coef + (nb + nbc + cb) * 64, &pred[2], &dc[1], &ac[1]);
         }
     flush_bits(&o);
     put_u16(&o, 0xffd9);                                   /* EOI */
     if (len) *len = o.n;
     return o.overflow ? JPGX_EARG : JPGX_OK;
+}
+
+int jpgx_encode_bmp_to_jpeg_ex(const char *input, const char *output, int quality,
+                               int sample_ratio, unsigned flags, int device)
+{
+    if (!input || !output) return JPGX_EARG;
+    if (!(flags & JPGX_FLAG_SUBSAMPLE) || sample_ratio == 0)
+        return jpgx_encode_bmp_to_jpeg(input, output, quality, sample_ratio);
+    int W = 0, H = 0;
+    uint8_t *rgb = NULL;
+    size_t fsize = 0;
+    int rc = jpgx_bmp_read(input, &rgb, &W, &H, &fsize);
+    if (rc) return rc;
+    jpgx_params p;
+    jpgx_default_params(&p, W, H, quality, sample_ratio);
+    p.flags = flags;
+    const size_t nb = (size_t)(W / 8) * (H / 8);
+    const size_t nbc = jpgx_chroma_blocks(W, 0, H / 8, sample_ratio, flags);
+    int16_t *coef = (int16_t *)malloc((nb + 2 * nbc) * 64 * sizeof(int16_t));
+    const size_t cap = jpgx_jfif_bound(W, H);
+    uint8_t *buf = (uint8_t *)malloc(cap);
+    size_t len = 0;
+    rc = (coef && buf) ? JPGX_OK : JPGX_EARG;
+    if (!rc) rc = jpgx_blocks(rgb, W, H, (size_t)W * 3, &p, coef, device);
+    if (!rc) rc = jpgx_write_jfif_sub(coef, W, H, quality, sample_ratio, buf, cap, &len);
+    if (!rc) {
+        FILE *f = fopen(output, "wb");
+        if (!f || fwrite(buf, 1, len, f) != len) rc = JPGX_EARG;
+        if (f && fclose(f)) rc = JPGX_EARG;
+    }
+    jpgx_free(rgb);
+    free(coef);
+    free(buf);
+    return rc;
 }
 
 int jpgx_encode_bmp_to_jpeg(const char *input, const char *output, int quality,

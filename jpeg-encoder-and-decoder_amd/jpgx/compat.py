@@ -232,6 +232,27 @@ def write_jfif(coef: np.ndarray, width: int, height: int, quality: int) -> bytes
     return bytes(buf[:n.value])
 
 
+def write_jfif_sub(coef: np.ndarray, width: int, height: int, quality: int,
+                   sample_ratio: int) -> bytes:
+    """Y|Cb|Cr blocks of the JPGX_FLAG_SUBSAMPLE layout -> 4:2:2 / 4:2:0 JFIF bytes."""
+    coef = np.ascontiguousarray(coef, np.int16)
+    cap = lib.jpgx_jfif_bound(width, height)
+    buf = (ctypes.c_uint8 * cap)()
+    n = ctypes.c_size_t()
+    _check(lib.jpgx_write_jfif_sub(ctypes.c_void_p(coef.ctypes.data), width, height, quality,
+                                   sample_ratio, ctypes.cast(buf, ctypes.c_void_p),
+                                   ctypes.c_size_t(cap), ctypes.byref(n)),
+           "jpgx_write_jfif_sub")
+    return bytes(buf[:n.value])
+
+
+def encode_bmp_to_jpeg_ex(src: str, dst: str, quality: int, sample_ratio: int, flags: int,
+                          device: int = 0) -> None:
+    _check(lib.jpgx_encode_bmp_to_jpeg_ex(src.encode(), dst.encode(), quality, sample_ratio,
+                                          ctypes.c_uint(flags), device),
+           "jpgx_encode_bmp_to_jpeg_ex")
+
+
 def encode_bmp_to_jpeg(src: str, dst: str, quality: int, sample_ratio: int = 0) -> None:
     _check(lib.jpgx_encode_bmp_to_jpeg(src.encode(), dst.encode(), quality, sample_ratio),
            "jpgx_encode_bmp_to_jpeg")

@@ -1,6 +1,7 @@
 """Minimal baseline-JPEG entropy decoder (test helper): parses the markers jpgx_write_jfif
 emits (SOF0, DQT, DHT, one interleaved SOS, no restart markers) and returns the quantised
-zig-zag coefficients [ncomp][nblocks][64] and the DQT tables -- an independent check of the
+zig-zag coefficients [ncomp][nblocks][64] (a list [Y, Cb, Cr] for 4:2:2 / 4:2:0) and the
+DQT tables -- an independent check of the
 writer, written from ITU-T T.81 (Annex C canonical codes, F.2.2 decoding, F.1.2.3 stuffing)."""
 import numpy as np
 
@@ -84,36 +85,52 @@ def decode(data: bytes):
             assert seg[0] == 8
             H, W = _u16(seg, 1), _u16(seg, 3)
             comps = [(seg[6 + 3 * k], seg[7 + 3 * k], seg[8 + 3 * k]) for k in range(seg[5])]
-            assert all(c[1] == 0x11 for c in comps), "4:4:4 only"
+            assert all(c[1] == 0x11 for c in comps[1:]), "chroma must be sampled 1x1"
         elif m == 0xDA:
             ns = seg[0]
             sel = [(seg[1 + 2 * k], seg[2 + 2 * k]) for k in range(ns)]
             i += 2 + ln
             break
         i += 2 + ln
-    nb = (W // 8) * (H // 8)
-    out = np.zeros((len(sel), nb, 64), np.int32)
+    hs, vs = comps[0][1] >> 4, comps[0][1] & 15       # luma sampling (1,1) (2,1) (2,2)
+    bpr = W // 8
+    nb = bpr * (H // 8)
+    cpr, crows = bpr // hs, H // 8 // vs
+    nbc = cpr * crows
+    out = [np.zeros((nb, 64), np.int32)] + [np.zeros((nbc, 64), np.int32) for _ in sel[1:]]
     br = _Bits(b[i:])
     pred = [0] * len(sel)
-    for blk in range(nb):
-        for c, (_, tables) in enumerate(sel):
-            dc_t, ac_t = dht[tables >> 4], dht[0x10 | (tables & 15)]
-            s = _decode_sym(br, dc_t)
-            pred[c] += _extend(br.bits(s), s)
-            out[c, blk, 0] = pred[c]
-            k = 1
-            while k < 64:
-                rs = _decode_sym(br, ac_t)
-                r, s = rs >> 4, rs & 15
-                if s == 0:
-                    if r == 15:
-                        k += 16
-                        continue
-                    break                                  # EOB
-                k += r
-                out[c, blk, k] = _extend(br.bits(s), s)
-                k += 1
+
+    def block(c, tables, dst):
+        dc_t, ac_t = dht[tables >> 4], dht[0x10 | (tables & 15)]
+        s = _decode_sym(br, dc_t)
+        pred[c] += _extend(br.bits(s), s)
+        dst[0] = pred[c]
+        k = 1
+        while k < 64:
+            rs = _decode_sym(br, ac_t)
+            r, s = rs >> 4, rs & 15
+            if s == 0:
+                if r == 15:
+                    k += 16
+                    continue
+                break                                      # EOB
+            k += r
+            dst[k] = _extend(br.bits(s), s)
+            k += 1
+
+    for my in range(crows):                            # MCUs (T.81 A.2.3)
+        for mx in range(cpr):
+            for c, (_, tables) in enumerate(sel):
+                if c == 0:
+                    for dy in range(vs):
+                        for dx in range(hs):
+                            block(0, tables, out[0][(my * vs + dy) * bpr + mx * hs + dx])
+                else:
+                    block(c, tables, out[c][my * cpr + mx])
+    if hs == vs == 1:
+        out = np.stack(out)
     rest = br.d[br.i:]
     assert rest[-2:] == b"\xff\xd9", "no EOI after the scan"
     return {"width": W, "height": H, "coef": out, "dqt": dqt,
-            "qsel": [c[2] for c in comps]}
+            "qsel": [c[2] for c in comps], "sampling": (hs, vs)}

@@ -148,3 +148,57 @@ def test_gpu_subsample_stripes_and_batch(cuda, sr):
     got = out.cpu().numpy()
     for f in range(F):
         assert np.array_equal(got[f], want[f]), f"frame {f}"
+
+
+@pytest.mark.parametrize("sr", [1, 2])
+@pytest.mark.parametrize("q", [50, 90])
+def test_jfif_subsampled_roundtrip(sr, q):
+    """jpgx_write_jfif_sub on the oracle's Y + subsampled chroma: the independent decoder
+    (tests/jfif_decode.py, MCU interleave of T.81 A.2.3) returns the same coefficients."""
+    from jpgx import compat as C
+    from jfif_decode import decode
+    W, H = 96, 64
+    rgb = O.gen_splitmix(21 + sr, W, H)
+    y, c = O.blocks(rgb, q, sr)[0], O.chroma_sub(rgb, q, sr)
+    data = C.write_jfif_sub(np.concatenate([y, c.reshape(-1, 64)]), W, H, q, sr)
+    d = decode(data)
+    assert d["sampling"] == ((2, 1) if sr == 1 else (2, 2))
+    assert np.array_equal(d["coef"][0], y)
+    assert np.array_equal(d["coef"][1], c[0]) and np.array_equal(d["coef"][2], c[1])
+
+
+@pytest.mark.parametrize("sr", [1, 2])
+def test_jfif_subsampled_decodes_with_pil(sr):
+    """libjpeg (PIL) decodes the subsampled file; on a smooth frame its image is close to the
+    decode of the 4:4:4 file of the same pipeline (same Cb sign quirk in both)."""
+    import io
+    Image = pytest.importorskip("PIL.Image")
+    from jpgx import compat as C
+    W, H = 128, 64
+    yy, xx = np.mgrid[0:H, 0:W]
+    rgb = np.stack([(xx * 2) % 256, (yy * 4) % 256, ((xx + yy) * 1.5) % 256], -1).astype(np.uint8)
+    full = O.blocks(rgb, 90)
+    y, c = O.blocks(rgb, 90, sr)[0], O.chroma_sub(rgb, 90, sr)
+    a = np.asarray(Image.open(io.BytesIO(C.write_jfif(full, W, H, 90))).convert("RGB"), float)
+    img = Image.open(io.BytesIO(C.write_jfif_sub(np.concatenate([y, c.reshape(-1, 64)]), W, H, 90, sr)))
+    assert img.size == (W, H)
+    b = np.asarray(img.convert("RGB"), float)
+    psnr = 10 * np.log10(255 ** 2 / np.mean((a - b) ** 2))
+    assert psnr > 30, psnr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sr", [1, 2])
+def test_gpu_encode_bmp_to_jpeg_subsampled(tmp_path, cuda, sr):
+    """BMP in, truly subsampled JPEG out (jpgx_encode_bmp_to_jpeg_ex on the GPU)."""
+    from jpgx import compat as C
+    from jfif_decode import decode
+    W, H = 256, 128
+    rgb = O.gen_splitmix(31, W, H)
+    src, dst = str(tmp_path / "in.bmp"), str(tmp_path / "out.jpg")
+    O.write_bmp(src, rgb)
+    C.encode_bmp_to_jpeg_ex(src, dst, 75, sr, jpgx.FLAG_SUBSAMPLE)
+    d = decode(open(dst, "rb").read())
+    assert np.array_equal(d["coef"][0], O.blocks(rgb, 75, sr)[0])
+    c = O.chroma_sub(rgb, 75, sr)
+    assert np.array_equal(d["coef"][1], c[0]) and np.array_equal(d["coef"][2], c[1])
