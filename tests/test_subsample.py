@@ -202,3 +202,20 @@ def test_gpu_encode_bmp_to_jpeg_subsampled(tmp_path, cuda, sr):
     assert np.array_equal(d["coef"][0], O.blocks(rgb, 75, sr)[0])
     c = O.chroma_sub(rgb, 75, sr)
     assert np.array_equal(d["coef"][1], c[0]) and np.array_equal(d["coef"][2], c[1])
+
+
+def test_subsample_argument_errors():
+    """Validation happens before any device work: no GPU needed."""
+    S = jpgx.FLAG_SUBSAMPLE
+    W, H = 64, 64
+    fake = 1 << 20                                   # never dereferenced
+    p = jpgx.default_params(W, H, 75, 0, flags=S)
+    fr = jpgx.frames(W, H)
+    rc = jpgx.lib.jpgx_blocks_gpu(__import__("ctypes").byref(fr), __import__("ctypes").byref(p),
+                                  fake, fake, fake, 0, None)
+    assert rc == jpgx.ESAMPLE                       # the flag needs sample_ratio 1 or 2
+    p = jpgx.default_params(W, H, 75, 2, flags=S)
+    fr = jpgx.frames(W, H, rows=(1, 4))
+    rc = jpgx.lib.jpgx_blocks_gpu(__import__("ctypes").byref(fr), __import__("ctypes").byref(p),
+                                  fake, fake, fake, 0, None)
+    assert rc == jpgx.EARG                          # 4:2:0 stripes start on even block rows
