@@ -51,6 +51,15 @@ struct jx_limtab {
 
 #define JX_MAXQ 97
 
+/* k_mx (csrc/jpgx_mx.hip) per-quality tables: lane n = 8c + u of the MFMA result holds the
+ * scales and guard band of coefficients (c, u, v = 0..7) */
+struct jx_mxtab {
+    float w[32][8];         /* 1/4 a(u) a(v) k(v) / Q[u][v] (row transform uses exact cosines);
+                               columns 24..31 are MFMA padding: w 0                          */
+    float lim[32][8];       /* rigorous guard band of the k_mx arithmetic (padding: 3e38)     */
+    int16_t q[2][64];       /* scaled tables, q[t][u*8+v] = Qs[u][v] (src/quantise.c:58)       */
+};
+
 /* Device workspace: per k_xform wave and channel, the blocks with a coefficient inside the
  * guard band (no atomics: every wave owns a region), consumed by k_fix. */
 struct jx_fixlist {
@@ -68,6 +77,8 @@ struct jx_xform_args {
     int force_exact;        /* JPGX_FLAG_FORCE_EXACT: flag every coefficient              */
     int luma_only;          /* k_xform: channel 0 only (chroma from k_chroma)             */
     int sub;                /* k_chroma: 1 = true 4:2:2, 2 = true 4:2:0                   */
+    unsigned *rec_pg;       /* k_mx: flagged pair-group records (workspace), [pair-groups]  */
+    uint64_t *rec_sv;       /*       and their lane masks [pair-groups][2][8]               */
 };
 
 
@@ -81,6 +92,13 @@ int jx_plan_tables_mode(int quality, int sub, float w[3][64], float lim[3][64], 
 void jx_under_dwords(const uint8_t under[3][8], uint32_t out[6]);
 /* packed-pair vs scalar transform, bit for bit (host; returns the mismatch count) */
 long long jx_selftest_pk(long long nblocks, unsigned long long seed);
+/* k_mx: tables and f16 B operands (host plan), launch (device side) */
+int jx_plan_tables_mx(int quality, float w[24][8], float lim[24][8], int16_t q[2][64]);
+int jx_mx_operands(uint16_t ops[6][64][8]);
+long long jx_selftest_mx(long long nblocks, unsigned long long seed, int quality,
+                         long long *flagged, double *ratio);
+int jx_launch_mx(const struct jx_xform_args *xa, void *ws, size_t ws_bytes, void *stream);
+size_t jx_mx_workspace(size_t nb, int nframes);
 #ifdef __cplusplus
 }
 #endif

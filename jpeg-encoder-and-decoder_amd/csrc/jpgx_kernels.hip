@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -1918,6 +1919,14 @@ int resident_waves()
     return g_resident_waves[dev];
 }
 
+/* the 4:4:4 transform kernel: k_xform (all-VALU), or k_mx (matrix-core row pass,
+ * csrc/jpgx_mx.hip) with JPGX_KERNEL=mx -- bit-exact, measured slower so far */
+bool mx_selected()
+{
+    const char *e = getenv("JPGX_KERNEL");
+    return e && strcmp(e, "mx") == 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1938,7 +1947,10 @@ size_t jpgx_workspace_size(const jpgx_frames *fr)
     /* per k_xform wave (at most tiles + 3 of them) and channel: a count, and room for 64
      * items per tile the wave walks (waves x ceil(tiles / waves) < 2 x tiles + 3) */
     const size_t counts = (3 * (ntiles + 3) * sizeof(unsigned) + 255) & ~(size_t)255;
-    return JX_WS_HEADER + counts + 3 * (2 * ntiles + 3) * 64 * sizeof(uint32_t);
+    const size_t xform = JX_WS_HEADER + counts + 3 * (2 * ntiles + 3) * 64 * sizeof(uint32_t);
+    /* k_mx: a flag-record slot per pair-group of 8 blocks */
+    return std::max(xform, jx_mx_workspace((size_t)(fr->row_end - fr->row_begin) * (fr->width / 8),
+                                           fr->nframes));
 }
 
 int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
@@ -1998,6 +2010,13 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     xa.force_exact = (p->flags & JPGX_FLAG_FORCE_EXACT) ? 1 : 0;
     hipStream_t s = (hipStream_t)stream;
     xa.luma_only = sub ? 1 : 0;
+    if (!sub && mx_selected()) {
+        /* k_mx: colour + row DCT on the matrix cores, exact pass inside (csrc/jpgx_mx.hip) */
+        rc = jx_launch_mx(&xa, d_workspace, workspace_bytes, stream);
+        if (rc) return rc;
+        if (event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
+        return rc;
+    }
     if (JX_K2 && !sub) {
         /* two lanes per block: 32-block tiles, persistent grid, exact pass inside */
         const size_t nt2 = (total + 31) / 32;

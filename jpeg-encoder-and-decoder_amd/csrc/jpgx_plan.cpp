@@ -358,3 +358,236 @@ extern "C" long long jx_selftest_pk(long long nblocks, unsigned long long seed)
 extern "C" {
 
 }  /* extern "C" */
+
+/* ---- k_mx: colour conversion + row DCT as one f16 MFMA product --------------------------
+ *
+ * k_mx multiplies each pixel row, 24 bytes b_k (k = 3x + p, plane p of pixel x) shifted to
+ * s_k = b_k - 128 (exact in f16), by B[k][n] = a[c][p] cos((2x+1)u pi/16), n = 8c + u, with
+ * the bias row k = 24 (input 1.0) carrying 8 * (128 sum_p a[c][p] + shift_c) for u = 0 (the
+ * level shift, preprocess.c:160-162,186-188; the true cosines of u > 0 sum to 0).  B is
+ * split into three f16 parts:
+ *   Bh  B rounded to a multiple of 2^-11 (|B| < 1: 11 bits, an f16; bias: its f16),
+ *   Bl  f16(B - Bh),  Bm  f16(B - Bh - Bl).
+ * acc_h = sum_k s_k Bh_k is EXACT whatever the order of the MFMA's additions: every product
+ * and every partial sum is a multiple of 2^-11 below 2^13 in magnitude (24 bits).  acc_l =
+ * sum_k s_k (Bl_k + Bm_k) is below 1 in magnitude; its additions (at most 70) are charged one
+ * ulp each.  R = fl(acc_h + acc_l) then enters the column pass (jx_fdct8, FOps) as usual.
+ */
+static const double kMxA[3][3] = {{0.299, 0.587, 0.114},
+                                  {-0.168736, 0.331264, -0.5},
+                                  {0.5, -0.418688, -0.081312}};
+
+/* round to the nearest f16 (ties to even); bit pattern in *bits */
+static long double f16_round(long double x, uint16_t *bits)
+{
+    if (x == 0) {
+        *bits = 0;
+        return 0;
+    }
+    const int e = ilogbl(x);
+    const int qe = std::max(e - 10, -24);
+    const long double v = rintl(ldexpl(x, -qe)) * ldexpl(1.0L, qe);
+    const long double av = fabsl(v);
+    uint16_t s = v < 0 ? 0x8000 : 0;
+    const int ev = ilogbl(av);
+    if (ev < -14) {
+        s |= (uint16_t)llrintl(ldexpl(av, 24));
+    } else {
+        const long long mant = llrintl(ldexpl(av, 10 - ev)) - 1024;
+        s |= (uint16_t)(((ev + 15) << 10) | mant);
+    }
+    *bits = s;
+    return v;
+}
+
+/* exact B[k][n] (k < 24: matrix, k = 24: bias row, else 0; n < 24) */
+static long double mx_exact(int k, int n)
+{
+    if (n >= 24) return 0;
+    const int c = n / 8, u = n % 8;
+    const long double pi = 3.141592653589793238462643383279502884L;
+    if (k < 24) {
+        const int x = k / 3, p = k % 3;
+        return (long double)kMxA[c][p] * cosl((2 * x + 1) * u * pi / 16);
+    }
+    if (k == 24 && u == 0) {
+        const long double sa = (long double)kMxA[c][0] + kMxA[c][1] + kMxA[c][2];
+        return 8.0L * (128.0L * sa - (c == 0 ? 128.0L : 0.0L));
+    }
+    return 0;
+}
+
+struct MxSplit {
+    long double h[32][32], l[32][32], m[32][32];
+    uint16_t bh[32][32], bl[32][32], bm[32][32];
+};
+
+static int mx_split(MxSplit &S)
+{
+    for (int k = 0; k < 32; k++)
+        for (int n = 0; n < 32; n++) {
+            const long double B = mx_exact(k, n);
+            long double hv;
+            if (k < 24) {
+                hv = rintl(ldexpl(B, 11)) / 2048.0L;
+                f16_round(hv, &S.bh[k][n]);
+            } else {
+                hv = f16_round(B, &S.bh[k][n]);
+            }
+            if (ldexpl(hv, 11) != rintl(ldexpl(hv, 11))) return JPGX_EARG;
+            S.h[k][n] = hv;
+            S.l[k][n] = f16_round(B - hv, &S.bl[k][n]);
+            S.m[k][n] = f16_round(B - hv - S.l[k][n], &S.bm[k][n]);
+        }
+    for (int n = 0; n < 24; n++) {              /* acc_h exactness: partial sums < 2^13 */
+        long double sh = fabsl(S.h[24][n]);
+        for (int k = 0; k < 24; k++) sh += 128.0L * fabsl(S.h[k][n]);
+        if (sh >= 8192.0L) return JPGX_EARG;
+    }
+    return JPGX_OK;
+}
+
+extern "C" int jx_mx_operands(uint16_t ops[6][64][8])
+{
+    static MxSplit S;
+    const int rc = mx_split(S);
+    if (rc) return rc;
+    /* operand i = 2 * part + kstep; lane l holds B[16 kstep + 8 (l >> 5) + j][l & 31] */
+    for (int part = 0; part < 3; part++)
+        for (int ks = 0; ks < 2; ks++)
+            for (int l = 0; l < 64; l++)
+                for (int j = 0; j < 8; j++) {
+                    const int k = 16 * ks + 8 * (l >> 5) + j, n = l & 31;
+                    ops[2 * part + ks][l][j] =
+                        part == 0 ? S.bh[k][n] : (part == 1 ? S.bl[k][n] : S.bm[k][n]);
+                }
+    return JPGX_OK;
+}
+
+/* Interval + error bound of R (the column pass input) for column n = 8c + u. */
+static Bnd mx_row_bound(const MxSplit &S, int n)
+{
+    long double loh = S.h[24][n], hih = S.h[24][n];
+    long double lol = S.l[24][n] + S.m[24][n], hil = lol;
+    long double sl = fabsl(S.l[24][n]) + fabsl(S.m[24][n]);
+    long double rep = fabsl(mx_exact(24, n) - S.h[24][n] - S.l[24][n] - S.m[24][n]);
+    for (int k = 0; k < 24; k++) {
+        const long double bh = S.h[k][n], bo = S.l[k][n] + S.m[k][n];
+        loh += std::min(-128.0L * bh, 127.0L * bh);
+        hih += std::max(-128.0L * bh, 127.0L * bh);
+        lol += std::min(-128.0L * bo, 127.0L * bo);
+        hil += std::max(-128.0L * bo, 127.0L * bo);
+        sl += 128.0L * (fabsl(S.l[k][n]) + fabsl(S.m[k][n]));
+        rep += 128.0L * fabsl(mx_exact(k, n) - S.h[k][n] - S.l[k][n] - S.m[k][n]);
+    }
+    const double el = (double)(70.0L * sl * 0x1p-23L + rep);
+    return BoundOps::add(Bnd{(double)loh, (double)hih, 0.0},
+                         Bnd{(double)lol - el, (double)hil + el, el});
+}
+
+extern "C" int jx_plan_tables_mx(int quality, float w[24][8], float lim[24][8], int16_t q[2][64])
+{
+    int qs[2][8][8];
+    int rc = jpgx_scale_table(0, quality, qs[0]);
+    if (rc) return rc;
+    jpgx_scale_table(1, quality, qs[1]);
+    for (int t = 0; t < 2; t++)
+        for (int u = 0; u < 8; u++)
+            for (int v = 0; v < 8; v++) q[t][u * 8 + v] = (int16_t)qs[t][u][v];
+    static MxSplit S;
+    rc = mx_split(S);
+    if (rc) return rc;
+    const long double a0 = 1.0L / sqrtl(2.0L);
+    for (int n = 0; n < 24; n++) {
+        const int c = n / 8, u = n % 8, t = c == 0 ? 0 : 1;
+        const Bnd R = mx_row_bound(S, n);
+        Bnd col[8], out[8];
+        for (int y = 0; y < 8; y++) col[y] = R;
+        jx_fdct8<BoundOps>(col, out);
+        for (int v = 0; v < 8; v++) {
+            const long double au = u == 0 ? a0 : 1.0L, av = v == 0 ? a0 : 1.0L;
+            const long double ws = 0.25L * au * av * dct_kfactor(v) / (long double)qs[t][u][v];
+            const float wf = (float)ws;
+            const Bnd &b = out[v];
+            const double mF = BoundOps::mag(b) + b.E;
+            double et = b.E * (double)wf + mF * (double)fabsl((long double)wf - ws) + 0x1p-25;
+            et = et * 1.01 + 1e-7;
+            w[n][v] = wf;
+            lim[n][v] = (float)(0.5 - et);
+        }
+    }
+    return JPGX_OK;
+}
+
+/* Host emulation of k_mx's fast path on random blocks (acc_h exact, acc_l summed in fp32,
+ * R = fl(acc_h + acc_l), then the kernel's FOps column pass and quantiser): counts the
+ * coefficients whose unflagged fp32 result differs from round(exact quotient) (must be 0)
+ * and the flagged ones.  ratio[0] = max |fp32 quotient - exact| / (0.5 - lim). */
+extern "C" long long jx_selftest_mx(long long nblocks, unsigned long long seed, int quality,
+                                    long long *flagged, double *ratio)
+{
+    static MxSplit S;
+    if (mx_split(S)) return -1;
+    float w[24][8], lim[24][8];
+    int16_t q[2][64];
+    if (jx_plan_tables_mx(quality, w, lim, q)) return -1;
+    const long double pi = 3.141592653589793238462643383279502884L;
+    const long double a0 = 1.0L / sqrtl(2.0L);
+    uint64_t s = seed;
+    long long bad = 0, nfl = 0;
+    double worst = 0;
+    for (long long bk = 0; bk < nblocks; bk++) {
+        int px[8][24];
+        for (int y = 0; y < 8; y++)
+            for (int k = 0; k < 24; k++) {
+                s = s * 6364136223846793005ULL + 1442695040888963407ULL;
+                px[y][k] = (int)(s >> 56);
+                if ((bk & 3) == 1) px[y][k] = px[0][k % 3];      /* flat blocks too */
+            }
+        for (int n = 0; n < 24; n++) {
+            const int c = n / 8, u = n % 8;
+            float R[8];
+            for (int y = 0; y < 8; y++) {
+                long double ah = S.h[24][n];
+                float al = (float)(S.l[24][n] + S.m[24][n]);
+                for (int k = 0; k < 24; k++) {
+                    const int sv = px[y][k] - 128;
+                    ah += sv * S.h[k][n];
+                    al = al + (float)(sv * S.l[k][n]);
+                    al = al + (float)(sv * S.m[k][n]);
+                }
+                R[y] = (float)ah + al;
+            }
+            float F[8];
+            jx_fdct8<FOps>(R, F);
+            for (int v = 0; v < 8; v++) {
+                /* exact: 1/4 a(u) a(v) sum_x sum_y X c_u(x) c_v(y) / Q, X from double colours */
+                long double sum = 0;
+                for (int y = 0; y < 8; y++)
+                    for (int x = 0; x < 8; x++) {
+                        long double X = (long double)kMxA[c][0] * px[y][3 * x] +
+                                        (long double)kMxA[c][1] * px[y][3 * x + 1] +
+                                        (long double)kMxA[c][2] * px[y][3 * x + 2];
+                        X += c == 0 ? -128.0L : 0.0L;
+                        sum += X * cosl((2 * x + 1) * u * pi / 16) * cosl((2 * y + 1) * v * pi / 16);
+                    }
+                const long double au = u == 0 ? a0 : 1.0L, av = v == 0 ? a0 : 1.0L;
+                const long double qx = 0.25L * au * av * sum / q[c == 0 ? 0 : 1][u * 8 + v];
+                const float tm = fmaf(F[v], w[n][v], 12582912.0f);
+                const float rr = tm - 12582912.0f;
+                const float d = fmaf(F[v], w[n][v], -rr);
+                const double qf = (double)F[v] * (double)w[n][v];
+                const double band = 0.5 - (double)lim[n][v];
+                worst = std::max(worst, (double)fabsl((long double)qf - qx) / band);
+                if (fabsf(d) >= lim[n][v]) {
+                    nfl++;
+                    continue;
+                }
+                if ((long double)rr != roundl(qx)) bad++;
+            }
+        }
+    }
+    if (flagged) *flagged = nfl;
+    if (ratio) *ratio = worst;
+    return bad;
+}

@@ -12,6 +12,15 @@ from conftest import GOLDEN, coef_sha
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["xform", "mx"])
+def kernel(request, monkeypatch):
+    """Every parity test runs on both 4:4:4 kernels: k_xform (all-VALU, the default) and k_mx
+    (colour + row DCT on the matrix cores, csrc/jpgx_mx.hip), selected per call by the
+    library through JPGX_KERNEL."""
+    monkeypatch.setenv("JPGX_KERNEL", request.param)
+    return request.param
+
+
 def _dev(a, cuda):
     import torch
     return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)

@@ -101,14 +101,35 @@ def test_kernel_cos_table_is_glibc():
 
 
 def test_workspace_size():
-    # header + per-wave counts + per-wave lists with room for every block of its tiles
-    def expect(nblocks):
+    # k_xform: header + per-wave counts + per-wave lists with room for every block of its
+    # tiles; k_mx: a 132-byte flag record per pair-group of 8 blocks (+256); the larger
+    def expect(nblocks, nframes=1):
         tiles = (nblocks + 63) // 64
-        return 256 + (3 * (tiles + 3) * 4 + 255) // 256 * 256 + 3 * (2 * tiles + 3) * 256
+        xform = 256 + (3 * (tiles + 3) * 4 + 255) // 256 * 256 + 3 * (2 * tiles + 3) * 256
+        mx = ((nblocks // nframes + 7) // 8) * nframes * 132 + 256
+        return max(xform, mx)
     nb = (3840 // 8) * (2160 // 8) * 8
-    assert jpgx.workspace_size(jpgx.frames(3840, 2160, nframes=8)) == expect(nb)
+    assert jpgx.workspace_size(jpgx.frames(3840, 2160, nframes=8)) == expect(nb, 8)
     assert jpgx.workspace_size(jpgx.frames(64, 64, rows=(2, 5))) == expect(3 * 8)
+    assert jpgx.workspace_size(jpgx.frames(8, 8, nframes=1000)) == expect(1000, 1000)
     assert jpgx.workspace_size(jpgx.frames(64, 64, rows=(3, 3))) == 0
+
+
+@pytest.mark.parametrize("q", [10, 50, 75, 90, 97])
+def test_mx_guard_band_holds_on_emulated_arithmetic(q):
+    """k_mx's guard band (jpgx_plan.cpp jx_plan_tables_mx) on a host emulation of its fast
+    path (acc_h exact, acc_l summed in fp32, R = fl(acc_h + acc_l), the FOps column pass and
+    quantiser): no unflagged coefficient may round differently from the exact quotient, and
+    the observed error must stay well inside the band."""
+    import ctypes
+    f = jpgx.lib.jx_selftest_mx
+    f.restype = ctypes.c_longlong
+    f.argtypes = [ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_int,
+                  ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
+    flagged, ratio = ctypes.c_longlong(), ctypes.c_double()
+    assert f(600, 77 + q, q, ctypes.byref(flagged), ctypes.byref(ratio)) == 0
+    assert ratio.value < 0.6
+    assert flagged.value < 600 * 192 // 100          # well under 1% flagged
 
 
 def test_packed_transform_matches_scalar_bit_for_bit():

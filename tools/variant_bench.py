@@ -42,6 +42,9 @@ print(json.dumps({"hash": h, "ms": sorted(ts)}))
 
 def run(lib):
     env = dict(os.environ, JPGX_LIB=lib)
+    if "#" in lib:                         # the default library with JPGX_KERNEL=<kernel>
+        lib, kern = lib.split("#")
+        env.update(JPGX_LIB=lib, JPGX_KERNEL=kern)
     r = subprocess.run([sys.executable, "-c", CHILD % {"repo": REPO}], env=env, capture_output=True,
                        text=True, timeout=300)
     if r.returncode:
@@ -52,7 +55,10 @@ def run(lib):
 def main():
     names = sys.argv[1:] or sorted(os.path.basename(p)[8:-3] for p in glob.glob(f"{VAR}/libjpgx_*.so"))
     libs = {"default": os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "lib", "libjpgx.so")}
-    libs.update({n: f"{VAR}/libjpgx_{n}.so" for n in names if n != "default"})
+    libs.update({n: f"{VAR}/libjpgx_{n}.so" for n in names if n not in ("default", "xform", "mx")})
+    for k in ("xform", "mx"):
+        if k in names:
+            libs[k] = libs["default"] + "#" + k
     res = {}
     for rnd in range(2):                      # interleaved rounds
         for n, lib in libs.items():
