@@ -55,7 +55,7 @@ def run(lib):
 def main():
     names = sys.argv[1:] or sorted(os.path.basename(p)[8:-3] for p in glob.glob(f"{VAR}/libjpgx_*.so"))
     libs = {"default": os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "lib", "libjpgx.so")}
-    libs.update({n: f"{VAR}/libjpgx_{n}.so" for n in names if n not in ("default", "xform", "mx")})
+    libs.update({n: f"{VAR}/libjpgx_{n}.so" + ("#mx" if n.startswith("mx") else "") for n in names if n not in ("default", "xform", "mx")})
     for k in ("xform", "mx"):
         if k in names:
             libs[k] = libs["default"] + "#" + k
