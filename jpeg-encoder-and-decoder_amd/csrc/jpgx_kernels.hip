@@ -91,6 +91,10 @@ constexpr float kMagic = 12582912.0f; /* 1.5 * 2^23: x + kMagic rounds x to an i
 #ifndef JX_QUEUE_ITEMS
 #define JX_QUEUE_ITEMS 128
 #endif
+#ifndef JX_FIX_STAGGER  /* 1: one mid-run exact pass per wave at a wave-dependent tile; 2: one
+                           before the wave's last tile (plus the end-of-kernel pass)          */
+#define JX_FIX_STAGGER 0
+#endif
 #ifndef JX_FUSED_FIX    /* k_xform runs the exact pass itself, 8 queued blocks at a time: 1 after its
                            last tile, 2 also at each tile start, under the pixel loads;
                            0: a second kernel (k_fix) does it */
@@ -1051,6 +1055,11 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
     }
     WaveLds &W = s_wave[threadIdx.x >> 6];
     Queue Q{{0, 0, 0}, {0u, 0u, 0u}};
+    unsigned iter = 0;                             /* tiles done by this wave (uniform) */
+    const unsigned tpw = (ntiles + nwaves - 1) / nwaves;
+    const unsigned stagger_at = tpw > 2 ? wave % (tpw - 1) : 0u;
+    (void)stagger_at;
+    (void)iter;
     uint32_t raw[8][6];
 #if JX_PREFETCH || JX_RELOAD
     {
@@ -1183,7 +1192,17 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
             /* only when a queue could overflow (rare): the rest waits for the kernel's end */
             while (Q.n[0] > kItems - 64 || Q.n[1] > kItems - 64 || Q.n[2] > kItems - 64)
                 fix_queued(W, Q.n, a, lane);
+#if JX_FIX_STAGGER == 1
+            /* one mid-run drain per wave, at a wave-dependent tile: the waves' exact passes
+             * overlap the others' streaming instead of all landing at the end */
+            if (iter == stagger_at)
+                while (Q.n[0] + Q.n[1] + Q.n[2] > 0) fix_queued(W, Q.n, a, lane);
+#elif JX_FIX_STAGGER == 2
+            if (t + 2 * nwaves >= ntiles)        /* before the wave's last tile */
+                while (Q.n[0] + Q.n[1] + Q.n[2] > 0) fix_queued(W, Q.n, a, lane);
+#endif
         }
+        iter++;
 #else
         /* keep room for the next tile's 64 possible items per channel */
         if (!JX_DBG_NO_EXACT) {
@@ -1205,6 +1224,9 @@ __global__ __launch_bounds__(JX_WG, JX_WPE) void k_xform(const jx_xform_args a)
     }
 #if JX_FUSED_FIX
     if (!JX_DBG_NO_EXACT) {
+#ifdef JX_DBG_NO_FIXPASS  /* timing experiments only: band test and queueing, no exact pass */
+        Q.n[0] = Q.n[1] = Q.n[2] = 0;
+#endif
         while (Q.n[0] + Q.n[1] + Q.n[2] > 0) fix_queued(W, Q.n, a, lane);
     }
     (void)wave;
