@@ -14,7 +14,8 @@
  * holds all eight pixel rows of blocks 2h and 2h+1 for its column n = 8c + u:
  *     A[m][k]  = b_k - 128 of the pixel row (k = 3x + p; exact in f16), k = 24 the bias 1.0
  *     B[k][n]  = a[c][p] cos((2x+1)u pi/16), B[24][n] = the level-shift bias (jpgx_plan.cpp)
- *     R[m][n]  = (A Bh) + fl(A Bl + A Bm)       (acc_h exact: jpgx_plan.cpp explains why)
+ *     R[m][n]  = (A Bh) + 2^-12 fl(A Bl + A Bm) (acc_h exact: jpgx_plan.cpp explains why;
+ *                                                the lo parts are stored scaled by 2^12)
  * i.e. the colour-converted, level-shifted row transform of all three channels in 6 MFMAs
  * per 4 blocks.  Each lane then runs the column DCT (jx_fdct8, the FOps code the guard band
  * is derived from) of its column for two blocks, quantises with the per-lane (c,u) scales,
@@ -287,7 +288,9 @@ __device__ __forceinline__ void mx_rows(mx_h8 A0, mx_h8 A1, const mx_h8 (&B)[6],
     al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B[5], al, 0, 0, 0);
 #pragma unroll
     for (int y = 0; y < 8; y++)
-        R[y] = mx_f2{ah[2 * y], ah[2 * y + 1]} + mx_f2{al[2 * y], al[2 * y + 1]};
+        R[y] = __builtin_elementwise_fma(mx_f2{al[2 * y], al[2 * y + 1]},
+                                         mx_f2{0x1p-12f, 0x1p-12f},
+                                         mx_f2{ah[2 * y], ah[2 * y + 1]});
 }
 
 /* v_pk_*_f32 pairs: two blocks' columns in lock-step, lane by lane the FOps sequence */

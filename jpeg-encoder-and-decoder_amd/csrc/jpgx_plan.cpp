@@ -367,11 +367,12 @@ extern "C" {
  * level shift, preprocess.c:160-162,186-188; the true cosines of u > 0 sum to 0).  B is
  * split into three f16 parts:
  *   Bh  B rounded to a multiple of 2^-11 (|B| < 1: 11 bits, an f16; bias: its f16),
- *   Bl  f16(B - Bh),  Bm  f16(B - Bh - Bl).
+ *   Bl  f16(2^12 (B - Bh)),  Bm  f16(2^12 (B - Bh) - Bl)   (scaled: normal f16 numbers).
  * acc_h = sum_k s_k Bh_k is EXACT whatever the order of the MFMA's additions: every product
  * and every partial sum is a multiple of 2^-11 below 2^13 in magnitude (24 bits).  acc_l =
- * sum_k s_k (Bl_k + Bm_k) is below 1 in magnitude; its additions (at most 70) are charged one
- * ulp each.  R = fl(acc_h + acc_l) then enters the column pass (jx_fdct8, FOps) as usual.
+ * sum_k s_k (Bl_k + Bm_k) 2^-12 is below 1 in magnitude; its additions (at most 70) are charged
+ * one ulp each.  R = fl(acc_h + 2^-12 acc_l) (one fma) then enters the column pass (jx_fdct8,
+ * FOps) as usual.
  */
 static const double kMxA[3][3] = {{0.299, 0.587, 0.114},
                                   {-0.168736, 0.331264, -0.5},
@@ -436,8 +437,13 @@ static int mx_split(MxSplit &S)
             }
             if (ldexpl(hv, 11) != rintl(ldexpl(hv, 11))) return JPGX_EARG;
             S.h[k][n] = hv;
-            S.l[k][n] = f16_round(B - hv, &S.bl[k][n]);
-            S.m[k][n] = f16_round(B - hv - S.l[k][n], &S.bm[k][n]);
+            /* the lo parts are stored scaled by 2^12 (normal f16 numbers, not subnormals that
+             * would flush the third part to 0); k_mx takes R = acc_h + 2^-12 acc_l, exact
+             * scaling.  S.l / S.m hold the unscaled values. */
+            const long double ls = f16_round(ldexpl(B - hv, 12), &S.bl[k][n]);
+            const long double ms = f16_round(ldexpl(B - hv, 12) - ls, &S.bm[k][n]);
+            S.l[k][n] = ldexpl(ls, -12);
+            S.m[k][n] = ldexpl(ms, -12);
         }
     for (int n = 0; n < 24; n++) {              /* acc_h exactness: partial sums < 2^13 */
         long double sh = fabsl(S.h[24][n]);

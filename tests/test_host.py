@@ -118,7 +118,7 @@ def test_workspace_size():
 @pytest.mark.parametrize("q", [10, 50, 75, 90, 97])
 def test_mx_guard_band_holds_on_emulated_arithmetic(q):
     """k_mx's guard band (jpgx_plan.cpp jx_plan_tables_mx) on a host emulation of its fast
-    path (acc_h exact, acc_l summed in fp32, R = fl(acc_h + acc_l), the FOps column pass and
+    path (acc_h exact, acc_l summed in fp32, R = fl(acc_h + 2^-12 acc_l), the FOps column pass and
     quantiser): no unflagged coefficient may round differently from the exact quotient, and
     the observed error must stay well inside the band."""
     import ctypes
@@ -130,6 +130,41 @@ def test_mx_guard_band_holds_on_emulated_arithmetic(q):
     assert f(600, 77 + q, q, ctypes.byref(flagged), ctypes.byref(ratio)) == 0
     assert ratio.value < 0.6
     assert flagged.value < 600 * 192 // 100          # well under 1% flagged
+
+
+def test_mx_operands_make_the_hi_product_exact():
+    """k_mx's B operands (jpgx_plan.cpp jx_mx_operands): the hi part is a multiple of 2^-11 whose
+    products with b - 128 sum below 2^13 in every column (so the MFMA's hi accumulation is exact
+    in fp32 whatever its internal order), and hi + lo + lo2 reconstruct the colour x cosine
+    matrix (and the level-shift bias row) to 2^-30 (the lo parts are stored scaled by 2^12, so
+    the third part is a normal f16 rather than a flushed subnormal)."""
+    import ctypes
+    import math
+    ops = np.zeros((6, 64, 8), np.uint16)
+    f = jpgx.lib.jx_mx_operands
+    f.restype = ctypes.c_int
+    assert f(ops.ctypes.data_as(ctypes.c_void_p)) == 0
+    parts = ops.view(np.float16).astype(np.float64)            # [part*2 + kstep][lane][j]
+    B = np.zeros((3, 32, 32))
+    for part in range(3):
+        for ks in range(2):
+            for lane in range(64):
+                for j in range(8):
+                    B[part, 16 * ks + 8 * (lane >> 5) + j, lane & 31] = parts[2 * part + ks, lane, j]
+    hi, lo, lo2 = B[0], B[1] * 2.0 ** -12, B[2] * 2.0 ** -12      # lo parts stored x 2^12
+    assert np.all(hi * 2048 == np.round(hi * 2048))
+    assert np.all(128 * np.abs(hi[:24]).sum(axis=0) + np.abs(hi[24]) < 8192)
+    a = [(0.299, 0.587, 0.114), (-0.168736, 0.331264, -0.5), (0.5, -0.418688, -0.081312)]
+    for c in range(3):
+        for u in range(8):
+            n = 8 * c + u
+            for x in range(8):
+                for p in range(3):
+                    want = a[c][p] * math.cos((2 * x + 1) * u * math.pi / 16)
+                    assert abs(hi[3 * x + p, n] + lo[3 * x + p, n] + lo2[3 * x + p, n] - want) < 2 ** -30
+            bias = 8 * (128 * sum(a[c]) - (128 if c == 0 else 0)) if u == 0 else 0.0
+            assert abs(hi[24, n] + lo[24, n] + lo2[24, n] - bias) < 2 ** -30 * 512
+    assert not np.any(B[:, 25:, :]) and not np.any(B[:, :, 24:])
 
 
 def test_packed_transform_matches_scalar_bit_for_bit():
