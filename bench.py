@@ -161,10 +161,16 @@ def main():
     ap.add_argument("--sample-ratio", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel", choices=["xform", "mx"], default=None,
+                    help="4:4:4 transform kernel (sets JPGX_KERNEL): k_xform (default) or k_mx, "
+                         "the matrix-core row pass (DESIGN.md 4.6)")
     ap.add_argument("--subsample", action="store_true",
                     help="true 4:2:2 / 4:2:0 chroma (JPGX_FLAG_SUBSAMPLE, an extension; needs "
                          "--sample-ratio 1 or 2): not the headline metric")
     args = ap.parse_args()
+    if args.kernel:
+        os.environ["JPGX_KERNEL"] = args.kernel
+    kname = "k_mx" if os.environ.get("JPGX_KERNEL") == "mx" else "k_xform"
 
     import torch
     import torch.distributed as dist
@@ -238,7 +244,8 @@ def main():
     achieved = bytes_per_px * px_rank_step / (xform_ms * 1e-3) / 1e9
 
     if rank == 0:
-        t_ratio, t_src = measured_traffic() if not args.subsample else (None, None)
+        t_ratio, t_src = (measured_traffic() if not args.subsample and kname == "k_xform"
+                          else (None, None))
         cpu = None
         if N == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(W, H, q, args.cpu_seconds, jpgx)
@@ -261,7 +268,7 @@ def main():
                          "traffic": (round(t_ratio * bytes_per_px * px_rank_step)
                                      if t_ratio else None),
                          "traffic_source": t_src,
-                         "kernel": "k_xform" if not args.subsample else "k_xform(Y)+k_chroma",
+                         "kernel": kname if not args.subsample else "k_xform(Y)+k_chroma",
                          "kernel_ms": round(xform_ms, 4),
                          "bytes_per_launch": bytes_per_px * px_rank_step},
             "cpu_baseline": cpu,
