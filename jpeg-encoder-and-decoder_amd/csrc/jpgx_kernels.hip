@@ -44,8 +44,9 @@ namespace {
 #ifndef JX_PREFETCH
 #define JX_PREFETCH 0   /* input prefetch mode, see k_xform */
 #endif
-#ifndef JX_TPF          /* 1: quantiser tables of the next column loaded one column ahead */
-#define JX_TPF 1
+#ifndef JX_TPF          /* 1: quantiser tables of the next column loaded one column ahead
+                           (0 measured 1-2% faster, tools/variant_bench.py, 6 interleaved rounds) */
+#define JX_TPF 0
 #endif
 #ifndef JX_CHLOOP       /* 1: the three channels run one rolled copy of the channel body */
 #define JX_CHLOOP 0
@@ -57,8 +58,9 @@ namespace {
 #ifndef JX_RELOAD_COL   /* column of the column pass at which the next loads are issued  */
 #define JX_RELOAD_COL 4
 #endif
-#ifndef JX_ROW_SB       /* scheduling fence between the row DCTs of a channel          */
-#define JX_ROW_SB 1
+#ifndef JX_ROW_SB       /* scheduling fence between the row DCTs of a channel
+                           (0 measured 1-2% faster together with JX_TPF 0)             */
+#define JX_ROW_SB 0
 #endif
 #ifndef JX_COL_SB       /* scheduling fence between the column DCTs of a channel       */
 #define JX_COL_SB 1

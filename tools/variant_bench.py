@@ -60,7 +60,7 @@ def main():
         if k in names:
             libs[k] = libs["default"] + "#" + k
     res = {}
-    for rnd in range(2):                      # interleaved rounds
+    for rnd in range(int(os.environ.get("VB_ROUNDS", "2"))):   # interleaved rounds
         for n, lib in libs.items():
             r = run(lib)
             res.setdefault(n, []).append(r)
