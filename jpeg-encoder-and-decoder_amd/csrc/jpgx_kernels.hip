@@ -1972,9 +1972,7 @@ size_t jpgx_workspace_size(const jpgx_frames *fr)
      * items per tile the wave walks (waves x ceil(tiles / waves) < 2 x tiles + 3) */
     const size_t counts = (3 * (ntiles + 3) * sizeof(unsigned) + 255) & ~(size_t)255;
     const size_t xform = JX_WS_HEADER + counts + 3 * (2 * ntiles + 3) * 64 * sizeof(uint32_t);
-    /* k_mx: a flag-record slot per pair-group of 8 blocks */
-    return std::max(xform, jx_mx_workspace((size_t)(fr->row_end - fr->row_begin) * (fr->width / 8),
-                                           fr->nframes));
+    return xform;
 }
 
 int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
@@ -2036,7 +2034,7 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     xa.luma_only = sub ? 1 : 0;
     if (!sub && mx_selected()) {
         /* k_mx: colour + row DCT on the matrix cores, exact pass inside (csrc/jpgx_mx.hip) */
-        rc = jx_launch_mx(&xa, d_workspace, workspace_bytes, stream);
+        rc = jx_launch_mx(&xa, stream);
         if (rc) return rc;
         if (event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
         return rc;

@@ -1,34 +1,42 @@
 /*
  * jpgx_mx.hip -- k_mx, the gfx950 block-transform kernel with the colour conversion and the
  * row DCT on the matrix cores (v_mfma_f32_32x32x16_f16), the column DCT, quantiser, guard
- * band and zig-zag in VALU.
+ * band and zig-zag in VALU, and the exact-order fp64 pass for guard-band coefficients inside
+ * the same waves.
  *
  * Reference path: preprocess.c:160-162,186-188 (colour + level shift) -> dct.c:36-59 ->
  * quantise.c:52-72 (transposed divisor, round()) -> zig_zag.c:48-58; output = the three
  * JpgData.zig_zag_* arrays, [frame][Y|Cb|Cr][nb][64] int16.
  *
- * Mapping.  A wave takes a "pair-group" of 8 consecutive blocks of one frame, as two MFMA
- * groups of 4 blocks.  MFMA row m (0..31) of a group is pixel row y of block blk with
- * m = 8i + 4hh + j -> blk = 2hh + (i >> 1), y = 4(i & 1) + j, so that in the 32x32 result
- * (column n on the lane, rows (r & 3) + 8(r >> 2) + 4(lane >> 5) in register r) lane half h
- * holds all eight pixel rows of blocks 2h and 2h+1 for its column n = 8c + u:
- *     A[m][k]  = b_k - 128 of the pixel row (k = 3x + p; exact in f16), k = 24 the bias 1.0
- *     B[k][n]  = a[c][p] cos((2x+1)u pi/16), B[24][n] = the level-shift bias (jpgx_plan.cpp)
- *     R[m][n]  = (A Bh) + 2^-12 fl(A Bl + A Bm) (acc_h exact: jpgx_plan.cpp explains why;
- *                                                the lo parts are stored scaled by 2^12)
- * i.e. the colour-converted, level-shifted row transform of all three channels in 6 MFMAs
- * per 4 blocks.  Each lane then runs the column DCT (jx_fdct8, the FOps code the guard band
- * is derived from) of its column for two blocks, quantises with the per-lane (c,u) scales,
- * tests the guard band (v_cmp into an SGPR mask), and writes each int16 to the wave's LDS
- * stage at its zig-zag position.  The 8 blocks x 3 channels x 128 B leave as three 1-KiB
- * nontemporal stores (64 lanes x 16 B, contiguous per channel).
+ * Work unit.  Each wave walks a contiguous range of "steps" of 8 consecutive blocks
+ * (launch-global block index, frames concatenated); a step is two MFMA groups of 4 blocks.
+ * Per group, lane l loads ONE 16-byte piece: pixel row y of block blk (the A-operand row
+ * m = l & 31 of the group) at byte offset 8 hA, hA = l >> 5 (jpgx_plan.cpp: K layout), issued
+ * a step ahead.  MFMA row m = 8i + 4hh + j <-> block blk = 2hh + (i >> 1)... precisely:
+ *     i = (m & 3) + 4 (m >> 3),  blk = 2 ((m >> 2) & 1) + (i & 1),  y = i >> 1,
+ * so that in the 32x32 result (column n = lane & 31 = 8c + u, rows (r & 3) + 8 (r >> 2) +
+ * 4 (lane >> 5) in register r) lane half h holds all 8 pixel rows of blocks 2h, 2h + 1 as the
+ * aligned register pairs (2y, 2y + 1):
+ *     A[m][k]  = b_k - 128 (exact in f16; bytes -> f16 by v_perm + v_pk_add_f16),
+ *                the bias slot A = 1.0 (k-step 1, lane half 0, element 0)
+ *     R[m][n]  = (A Bh) + 2^-12 (A Bl [+ A Bm])    (acc_h exact: jpgx_plan.cpp)
+ * = the colour-converted, level-shifted row transform of all three channels, 2 * JX_MX_PARTS
+ * MFMAs per 4 blocks.  Each lane then runs the column DCT of its column for its two blocks in
+ * lock-step (jx_fdct8 over v_pk_* pairs: lane by lane the FOps code the guard band is derived
+ * for), quantises with the per-lane (c,u) scales (tm = F w + 1.5 2^23: the low 16 bits are the
+ * rounded int16), writes each int16 to the wave's LDS stage at its zig-zag position, and folds
+ * the guard-band test d^2 - lim^2 >= 0 (d = F w - rint, exact) into one running max.  After each
+ * step, the 8 blocks x 3 channels x 128 B leave as three 1-KiB nontemporal stores.
  *
- * Exactness (as k_xform): coefficients inside the rigorous guard band
- * (jx_plan_tables_mx) are recorded per block-channel as 64-bit masks, turned into tasks in
- * an LDS queue after the pair-group's stores, and recomputed in the reference's fp64
- * operation order (8 lanes per coefficient: lane x forms (X(x,y) c_u[x]) c_v[y] for y = 0..7,
- * the 64-term sum runs x-outer / y-inner through the 8 lanes in turn) when the queue fills
- * and at the end of the wave's work.
+ * Exactness.  A group whose running max says "some coefficient inside the
+ * band" (rare: wave-uniform branch) re-tests its coefficients, copies the flagged blocks'
+ * pixel rows (already in registers) into an LDS slot and queues one task per flagged
+ * coefficient.  A full queue, and the end of the wave's range, run the exact pass: eight tasks
+ * at a time, eight lanes each -- lane x forms (X(x,y) c_u[x]) c_v[y] in fp64 for y = 0..7
+ * with X in the reference's double colour arithmetic, the 64-term sum runs x-outer / y-inner
+ * (dct.c:46-50) through lanes x = 0..7 in turn, then F = ((1/4 a(u)) a(v)) s and round(F / Q)
+ * with the transposed divisor.  The exact value patches the LDS stage if its block belongs to
+ * the step being built, else global memory (after the wave's earlier stores have landed).
  */
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -51,61 +59,63 @@ typedef _Float16 mx_h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 mx_h2 __attribute__((ext_vector_type(2)));
 typedef float mx_f16 __attribute__((ext_vector_type(16)));
 typedef uint32_t mx_u4 __attribute__((ext_vector_type(4)));
-typedef uint32_t mx_u2 __attribute__((ext_vector_type(2)));
 typedef float mx_f2 __attribute__((ext_vector_type(2)));
 
-constexpr float kMagic = 12582912.0f;   /* 1.5 * 2^23 */
-constexpr int kMxCap = 256;             /* exact tasks queued per wave                     */
-#ifndef JX_MX_DBG_NORARE         /* measurement only: no exact pass (NOT bit-exact) */
-#define JX_MX_DBG_NORARE 0
-#endif
-#ifndef JX_MX_RARE               /* inlining of the rare paths (exact pass, flag masks)  */
-#define JX_MX_RARE __forceinline__
-#endif
-#ifndef JX_MX_DBG_NODRAIN        /* measurement only: band test, no exact pass (NOT bit-exact) */
-#define JX_MX_DBG_NODRAIN 0
-#endif
-#ifndef JX_MX_DRAIN              /* the exact pass: out of line (its registers would
-                                    otherwise count against the tile loop's)            */
-#define JX_MX_DRAIN __forceinline__
-#endif
+constexpr float kMagic = 12582912.0f;   /* 1.5 * 2^23: x + kMagic rounds x to an integer   */
+constexpr int kParts = JX_MX_PARTS;
+constexpr int kSlots = 10;              /* LDS pixel slots (one block each) for exact tasks */
+constexpr int kRecs = 4;                /* flagged-group records per wave                   */
 #ifndef JX_MX_WPE
-#define JX_MX_WPE 3                     /* waves per SIMD the register allocation targets  */
+#define JX_MX_WPE 4                     /* waves per SIMD the register allocation targets  */
 #endif
 
-__device__ jx_mxtab g_mxtab[JX_MAXQ + 1];
-__device__ mx_u4 g_mxB[6][64];          /* B operands: (part, kstep) x lane, 8 f16 each     */
-__device__ uint32_t g_mxzo[64][8];      /* LDS stage offset of (lane, v): column n = 8c + u,
-                                           lane half h (blocks 2h, 2h + 1)                 */
+/* LDS stage: channel c at mx_stage_base(c), 8 blocks x 128 B each, blocks in step order,
+ * zig-zag order inside a block.  The bases put the three channels' 16-bit zig-zag writes of one
+ * instruction on different banks (bank = dword % 32: shifts 0, 4, 16 dwords; at most 3-way,
+ * about 2-way on average over the 8 rows v) and keep every 16-byte store chunk aligned.  The
+ * MFMA's padding columns 24..31 compute Y's columns again (jx_mx_operands), so those lanes
+ * write the very values lanes 0..7 write to the same addresses: no dummy area, no exec mask. */
+__host__ __device__ constexpr unsigned mx_stage_base(unsigned c)
+{
+    return 1152u * c + 16u * (c + 2u * (c >> 1));
+}
+constexpr unsigned kStageBytes = mx_stage_base(2) + 1024;
+
+struct MxLds {
+    uint8_t stage[kStageBytes];
+    mx_u4 in[2][2][64];                 /* [step & 1][group][lane]: the A-operand pieces, landed
+                                           by LDS-DMA one step ahead                         */
+    uint8_t pix[kSlots][8][24];         /* exact tasks: the flagged blocks' 8 pixel rows    */
+    uint16_t rbits[kRecs][64];          /* flagged-group record: per lane, bit 2v + j = its
+                                           coefficient (u, v) of block 2h + j is in the band */
+    uint32_t rblk[kRecs];               /* the group's first launch-global block            */
+    uint8_t rslot[kRecs][4];            /* pixel slot of each of its 4 blocks               */
+    uint32_t tblk[8];                   /* one exact batch: launch-global block             */
+    uint16_t tcode[8];                  /*                  slot << 9 | c << 6 | v << 3 | u  */
+};
+static_assert(kStageBytes % 16 == 0, "LDS-DMA pieces must stay 16-byte aligned");
+
+__device__ mx_u4 g_mxB[2 * kParts][64];          /* B operands: (part, kstep) x lane      */
+__device__ jx_mxtab g_mxtab[2][JX_MAXQ + 1];     /* [force][quality]                      */
 __constant__ double kMxCos[8][8] = JX_COS_INIT;
 __constant__ int kMxScan[8][8] = JX_SCAN_ORDER_INIT;
 constexpr double kMxAlpha0 = JX_ALPHA0;
+/* per channel the reference's colour constants as the exact pass uses them: t = (k0 r + k1 g)
+ * + k2 b (the signs of its subtractions folded into k1, k2: a - b*k == a + b*(-k) exactly),
+ * then (A + S t) - 128 with (A, S) = (0, 1) Y, (128, -1) Cb, (128, 1) Cr */
+__constant__ double kMxQuarterAlpha[8] = {0.25 * JX_ALPHA0, 0.25, 0.25, 0.25, 0.25, 0.25, 0.25, 0.25};
+__constant__ double kMxAlpha[8] = {JX_ALPHA0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0};
+__constant__ double kMxColour[3][5] = {{0.299, 0.587, 0.114, 0.0, 1.0},
+                                       {0.168736, -0.331264, 0.5, 128.0, -1.0},
+                                       {0.5, -0.418688, -0.081312, 128.0, 1.0}};
 
-struct MxLds {
-    uint8_t stage[4096];                /* [c][8 blocks][64] int16; c = 3: unused columns  */
-    uint32_t tblk[kMxCap];              /* queued tasks: launch-global block               */
-    uint16_t tcode[kMxCap];             /*               ch << 6 | v << 3 | u              */
-};
-
-/* four pixel bytes -> two f16 (b - 128): bytes as 0x64bb = 1024 + b, minus 1152 (exact) */
-__device__ __forceinline__ mx_h2 mx_bytes2(uint32_t d, uint32_t sel)
-{
-    const uint32_t v = __builtin_amdgcn_perm(0x64646464u, d, sel);
-    return __builtin_bit_cast(mx_h2, v) - (mx_h2){(_Float16)1152.0f, (_Float16)1152.0f};
-}
-
-__device__ __forceinline__ mx_h8 mx_cvt8(mx_u2 b)
-{
-    const mx_h2 p0 = mx_bytes2(b.x, 0x04010400u), p1 = mx_bytes2(b.x, 0x04030402u);
-    const mx_h2 p2 = mx_bytes2(b.y, 0x04010400u), p3 = mx_bytes2(b.y, 0x04030402u);
-    return (mx_h8){p0[0], p0[1], p1[0], p1[1], p2[0], p2[1], p3[0], p3[1]};
-}
-
+/* Order this wave's LDS accesses across lanes: a wave's LDS instructions execute in program
+ * order, so only the compiler must be kept from moving memory operations across this point
+ * (no fence: a wavefront-scope fence makes the compiler drain the vector memory counter). */
 __device__ __forceinline__ void mx_wave_sync()
 {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    asm volatile("" ::: "memory");
 }
 
 __device__ __forceinline__ int mx_rank(uint64_t m)
@@ -114,178 +124,298 @@ __device__ __forceinline__ int mx_rank(uint64_t m)
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-/* The launch geometry as plain values (kernel-argument fields copied out: references into
- * the argument struct, or indexed reads of its arrays, make the compiler copy it to scratch) */
+/* The lane id, recomputed where it is used by the rare paths: an opaque (volatile) value
+ * cannot be hoisted, so the rare paths' lane-derived constants do not occupy registers
+ * across the tile loop. */
+__device__ __forceinline__ unsigned mx_lane()
+{
+    unsigned l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+/* four pixel bytes of dword d -> two f16 b - 128: perm makes 0x64bb (= 1024 + b) from each
+ * byte (K = 0x64646481: byte 5 is 0x64, byte 4 is 0x81 = 129, which the bias selector of
+ * lane half 0 picks to make 1153 - 1152 = 1.0), then one packed subtraction, exact. */
+__device__ __forceinline__ uint32_t mx_cvt2(uint32_t K, uint32_t d, uint32_t sel)
+{
+    const mx_h2 v = __builtin_bit_cast(mx_h2, __builtin_amdgcn_perm(K, d, sel)) -
+                    (mx_h2){(_Float16)1152.0f, (_Float16)1152.0f};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+/* The launch geometry as plain values (references into the kernel-argument struct, or indexed
+ * reads of its arrays, make the compiler copy it to scratch) */
 struct MxG {
     const uint8_t *rgb;
     int16_t *out;
     long long pitch, fstride, ofstride;
-    unsigned bpr, nb;
-    int row0, quality;
-    uint32_t u0, u1, u2, u3, u4, u5;   /* the underflow pixel row (jx_geom.under) */
+    unsigned bpr, nb, total;
+    int row0, quality, force;
+    uint32_t u[6];                      /* the underflow pixel row (jx_geom.under) */
 };
 
-__device__ __forceinline__ MxG mx_geom(const jx_xform_args &a)
-{
-    MxG G;
-    G.rgb = a.g.rgb;
-    G.out = a.g.out;
-    G.pitch = a.g.in_pitch;
-    G.fstride = a.g.in_fstride;
-    G.ofstride = a.g.out_fstride;
-    G.bpr = (unsigned)a.g.bpr;
-    G.nb = (unsigned)a.g.nb;
-    G.row0 = a.g.row0;
-    G.quality = a.quality;
-    G.u0 = a.g.under[0];
-    G.u1 = a.g.under[1];
-    G.u2 = a.g.under[2];
-    G.u3 = a.g.under[3];
-    G.u4 = a.g.under[4];
-    G.u5 = a.g.under[5];
-    return G;
-}
+typedef const mx_u4 __attribute__((address_space(1))) *mx_gp;   /* global (not flat) loads */
 
 /*
- * Pixel row pointer of block (frame f, row r, column c), pixel row y, with the reference's
- * addressing: blockToCoords (preprocess.c:199-211) gives x0 = -8 for the last block of a
- * block-row, i.e. pixel row 8r+y-1, columns W-8..W-1; at frame block-row 0, y = 0 those are
- * the bytes in front of the planes (g.under; *under = true, the pointer is then unused).
+ * Address of the 16 bytes of pixel row y of block b (launch-global, clamped into range) at
+ * offset 8 hA, with the reference's addressing: blockToCoords (preprocess.c:199-211) gives
+ * x0 = -8 for the last block of a block-row, i.e. pixel row 8r+y-1, columns W-8..W-1; at frame
+ * block-row 0, y = 0 those are the bytes in front of the planes (the underflow row): *under is
+ * set and the address points at a readable row (the value is replaced at its use).
  */
-__device__ __forceinline__ const uint8_t *mx_row(MxG g, unsigned f, unsigned r,
-                                                 unsigned c, unsigned y, bool *under)
+__device__ __forceinline__ const uint8_t *mx_addr_general(const MxG &g, unsigned b, unsigned y,
+                                                         unsigned hA, bool *under)
 {
+    b = b < g.total ? b : g.total - 1u;
+    const unsigned f = b / g.nb, bi = b - f * g.nb;
+    const unsigned r = bi / g.bpr, c = bi - r * g.bpr;
     const bool last = c == g.bpr - 1u;
     *under = last && y == 0 && g.row0 + (int)r == 0;
-    const long long pr = 8ll * r + y - (last ? 1 : 0);
-    return g.rgb + (long long)f * g.fstride + (*under ? 0 : pr * g.pitch) + 24ll * c;
+    const long long pr = *under ? 0 : 8ll * r + y - (last ? 1 : 0);
+    return g.rgb + (long long)f * g.fstride + pr * g.pitch + 24ll * c + 8 * hA;
+}
+
+/* position of a step's first block: frame f, block bi in the frame, block-row r, column c */
+struct MxPos {
+    unsigned f, bi, r, c;
+};
+
+__device__ __forceinline__ void mx_advance(MxPos &p, const MxG &g)
+{
+    p.bi += 8u;
+    p.c += 8u;
+    while (p.c >= g.bpr) {
+        p.c -= g.bpr;
+        p.r++;
+    }
+    while (p.bi >= g.nb) {          /* next frame (frames smaller than a step: several) */
+        p.bi -= g.nb;
+        p.f++;
+        p.r = p.bi / g.bpr;
+        p.c = p.bi - p.r * g.bpr;
+    }
+}
+
+/* the step's 8 blocks lie in one block-row of one frame, none is the row's last block, and
+ * all are in range: the fast (one-add) load and store addressing applies */
+__device__ __forceinline__ bool mx_simple(const MxPos &p, const MxG &g, unsigned b0)
+{
+    return p.c + 8u < g.bpr && b0 + 8u <= g.total;
+}
+
+/* The two group loads of the step at position P (first block b0), by LDS-DMA into dst[q]
+ * (lane l's 16 bytes land at dst[q][l]): one global_load_lds_dwordx4 per group on every path
+ * (the general path only computes other addresses; bit q of the return value marks a lane
+ * whose group-q piece is the underflow row, replaced at its use). */
+__device__ __forceinline__ uint32_t mx_issue(const MxG &g, const MxPos &P, unsigned b0,
+                                             bool simple, uint32_t laneoff, mx_u4 (*dst)[64])
+{
+    const uint8_t *p[2];
+    uint32_t un = 0;
+    if (simple) {
+        const uint8_t *base = g.rgb + (long long)P.f * g.fstride + 8ll * P.r * g.pitch +
+                              24ll * P.c + laneoff;
+        p[0] = base;
+        p[1] = base + 96;
+    } else {
+        const unsigned lane = mx_lane(), m = lane & 31u, hA = lane >> 5;
+        const unsigned iA = (m & 3u) + 4u * (m >> 3);
+        const unsigned blkA = 2u * ((m >> 2) & 1u) + (iA & 1u), yA = iA >> 1;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            bool uq;
+            p[q] = mx_addr_general(g, b0 + 4u * q + blkA, yA, hA, &uq);
+            un |= (uq ? 1u : 0u) << q;
+        }
+    }
+#ifdef JX_MX_DBG_NOLOAD        /* timing experiments only: no pixel loads (pieces set once) */
+    if (un != 0xdeadbeefu) {
+        const unsigned l = mx_lane();
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const uint32_t h = (l * 2654435761u) ^ (q * 0x9e3779b9u) ^ b0;
+            dst[q][l] = mx_u4{h, h * 747796405u + 1u, h ^ 0x5bd1e995u, h * 3u + 7u};
+        }
+        return un;
+    }
+#endif
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)p[q],
+                                         (__attribute__((address_space(3))) void *)&dst[q][0],
+                                         16, 0, 0);
+    return un;
 }
 
 /*
- * Exact pass over the wave's queued tasks (after its stores: s_waitcnt vmcnt(0)), 8 at a
- * time, 8 lanes each: lane x of task i forms the products (X(x,y) c_u[x]) c_v[y], y = 0..7
- * (dct.c:48-50, exact_pixel in double), and the sum runs x-outer / y-inner (dct.c:46-47)
- * through lanes x = 0..7 in turn; then F = ((1/4 a(u)) a(v)) s (dct.c:54) and round(F / Q)
- * with the transposed divisor (quantise.c:58).
+ * One exact batch of n <= 8 tasks (L.tblk / L.tcode), eight lanes each: lane x of task i forms
+ * the products (X(x,y) c_u[x]) c_v[y], y = 0..7 (dct.c:48-50, X in the reference's double
+ * colour arithmetic, preprocess.c:160-162,186-188), and the sum runs x-outer / y-inner
+ * (dct.c:46-47) through lanes x = 0..7 in turn; F = ((1/4 a(u)) a(v)) s (dct.c:54) and
+ * round(F / Q) with the transposed divisor (quantise.c:58).  Blocks >= step_b0 (the step whose
+ * stage is being built) patch the stage; the others global memory (the caller has waited for
+ * the wave's stores).
  */
-__device__ JX_MX_DRAIN void mx_drain(MxLds &L, int nq, MxG g, unsigned lane)
+__device__ __forceinline__ void mx_batch(MxLds &L, int nt, const MxG &g, unsigned step_b0)
 {
-    const jx_mxtab &T = g_mxtab[g.quality];
+    const unsigned lane = mx_lane();
+    const jx_mxtab &T = g_mxtab[0][g.quality];
     const unsigned i = lane >> 3, x = lane & 7u;
-    uint32_t(*px)[8][6] = reinterpret_cast<uint32_t(*)[8][6]>(L.stage);  /* [task][row][dword] */
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool live = (int)i < nt;
+    const unsigned blk = L.tblk[live ? i : 0u];
+    const unsigned code = L.tcode[live ? i : 0u];
+    const int slot = (int)(code >> 9), ch = (int)((code >> 6) & 7u), v = (int)((code >> 3) & 7u),
+              u = (int)(code & 7u);
+    const double cu = kMxCos[u][x];
+    const double k0c = kMxColour[ch][0], k1c = kMxColour[ch][1], k2c = kMxColour[ch][2];
+    const double Ac = kMxColour[ch][3], Sc = kMxColour[ch][4];
+    double prod[8];
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+        const uint8_t *px = &L.pix[slot][y][3 * x];
+        const double rr = (double)px[0], gg = (double)px[1], bb = (double)px[2];
+        const double tt = (k0c * rr + k1c * gg) + k2c * bb;
+        const double X = (Ac + Sc * tt) - 128.0;
+        prod[y] = X * cu * kMxCos[v][y];
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int xx = 0; xx < 8; xx++) {
+        if ((int)x == xx) {
+#pragma unroll
+            for (int y = 0; y < 8; y++) sum += prod[y];
+        }
+        sum = __shfl(sum, (int)((lane & ~7u) | (unsigned)xx), 64);
+    }
+    if (live && x == 0) {
+        /* ((0.25 * a(u)) * a(v)) * s, dct.c:54 (0.25 * a(u) is exact in the table) */
+        const double F = kMxQuarterAlpha[u] * kMxAlpha[v] * sum;
+        const int q = T.q[ch == 0 ? 0 : 1][u * 8 + v];
+        const int16_t val = (int16_t)(int)round(F / (double)q);
+        const int z = kMxScan[v][u];
+        if (blk >= step_b0) {
+            *(int16_t *)(L.stage + mx_stage_base((unsigned)ch) + (blk - step_b0) * 128u + 2u * z) = val;
+        } else {
+            const unsigned f = blk / g.nb, bi = blk - f * g.nb;
+            g.out[(long long)f * g.ofstride + ((long long)ch * g.nb + bi) * 64 + z] = val;
+        }
+    }
+    mx_wave_sync();                                    /* batch buffer reused */
+}
+
+/* Exact pass over every recorded flagged group: tasks eight at a time (the records are
+ * expanded lane by lane, lowest bit first). */
+__device__ __forceinline__ void mx_drain(MxLds &L, int nrec, const MxG &g, unsigned step_b0)
+{
+    const unsigned lane = mx_lane();
+#ifdef JX_MX_EXPERIMENT_NODRAIN
+    return;
+#endif
+    const unsigned n = lane & 31u, h = lane >> 5, c = n >> 3, u = n & 7u;
+    __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0): the wave's stores landed */
     mx_wave_sync();
-    for (int t0 = 0; t0 < nq; t0 += 8) {
-        const int t = t0 + (int)i;
-        const bool live = t < nq;
-        const unsigned blk = L.tblk[live ? t : t0];
-        const unsigned code = L.tcode[live ? t : t0];
-        const int ch = (int)(code >> 6), v = (int)((code >> 3) & 7u), u = (int)(code & 7u);
-        const unsigned nb = g.nb, f = blk / nb, bi = blk - f * nb;
-        const unsigned r = bi / g.bpr, c = bi - r * g.bpr;
-        {   /* lane x of task i stages pixel row x of the task's block */
-            bool under;
-            const uint8_t *p = mx_row(g, f, r, c, x, &under);
-            const mx_u2 *pw = (const mx_u2 *)__builtin_assume_aligned(p, 8);
-            const mx_u2 d0 = pw[0], d1 = pw[1], d2 = pw[2];
-            px[i][x][0] = under ? g.u0 : d0.x;
-            px[i][x][1] = under ? g.u1 : d0.y;
-            px[i][x][2] = under ? g.u2 : d1.x;
-            px[i][x][3] = under ? g.u3 : d1.y;
-            px[i][x][4] = under ? g.u4 : d2.x;
-            px[i][x][5] = under ? g.u5 : d2.y;
-        }
-        mx_wave_sync();
-        /* lane x: the 8 products of pixel column x */
-        const int k0 = (int)(3 * x) >> 2, sh = (int)(3 * x) & 3, k1 = k0 + 1 < 6 ? k0 + 1 : 5;
-        const double cu = kMxCos[u][x];
-        /* mx_exact_pixel with the channel's constants selected once: t = (k0 r + k1 g) + k2 b
-         * (the signs of the reference's subtractions folded into k1, k2: a - b*k == a + b*(-k)
-         * exactly), then (A + S t) - 128 with (A, S) = (0, 1) Y, (128, -1) Cb, (128, 1) Cr */
-        const double k0c = ch == 0 ? 0.299 : (ch == 1 ? 0.168736 : 0.5);
-        const double k1c = ch == 0 ? 0.587 : (ch == 1 ? -0.331264 : -0.418688);
-        const double k2c = ch == 0 ? 0.114 : (ch == 1 ? 0.5 : -0.081312);
-        const double Ac = ch == 0 ? 0.0 : 128.0, Sc = ch == 1 ? -1.0 : 1.0;
-        double prod[8];
-#pragma unroll
-        for (int y = 0; y < 8; y++) {
-            const uint64_t w = (uint64_t)px[i][y][k0] | ((uint64_t)px[i][y][k1] << 32);
-            const uint32_t p3 = (uint32_t)(w >> (8 * sh));
-            const double rr = (double)(p3 & 0xffu), gg = (double)((p3 >> 8) & 0xffu),
-                         bb = (double)((p3 >> 16) & 0xffu);
-            const double t = (k0c * rr + k1c * gg) + k2c * bb;
-            const double X = (Ac + Sc * t) - 128.0;
-            prod[y] = X * cu * kMxCos[v][y];
-        }
-        double s = 0.0;
-#pragma unroll
-        for (int xx = 0; xx < 8; xx++) {
-            if ((int)x == xx) {
-#pragma unroll
-                for (int y = 0; y < 8; y++) s += prod[y];
+    int nt = 0;
+    for (int r = 0; r < nrec; r++) {
+        uint32_t bits = L.rbits[r][lane];
+        const unsigned gb0 = L.rblk[r];
+        for (;;) {
+            const uint64_t act = __ballot(bits != 0);
+            if (!act) break;
+            const int room = 8 - nt, rk = mx_rank(act);
+            if (bits != 0 && rk < room) {
+                const int k = __builtin_ctz(bits);
+                bits &= bits - 1u;
+                const unsigned v = (unsigned)k >> 1, blk = 2u * h + ((unsigned)k & 1u);
+                L.tblk[nt + rk] = gb0 + blk;
+                L.tcode[nt + rk] = (uint16_t)((unsigned)L.rslot[r][blk] << 9 | c << 6 | v << 3 | u);
             }
-            s = __shfl(s, (int)((lane & ~7u) | (unsigned)xx), 64);
+            nt += std::min((int)__popcll(act), room);
+            mx_wave_sync();
+            if (nt == 8) {
+                mx_batch(L, 8, g, step_b0);
+                nt = 0;
+            }
         }
-        if (live && x == 0) {
-            const double F = 0.25 * (u == 0 ? kMxAlpha0 : 1.0) * (v == 0 ? kMxAlpha0 : 1.0) * s;
-            const int q = T.q[ch == 0 ? 0 : 1][u * 8 + v];
-            g.out[(long long)f * g.ofstride + ((long long)ch * nb + bi) * 64 + kMxScan[v][u]] =
-                (int16_t)(int)round(F / (double)q);
-        }
-        mx_wave_sync();                                    /* px reused by the next chunk */
     }
+    if (nt) mx_batch(L, nt, g, step_b0);
+    /* nothing of the exact pass stays in flight: the tile loop's wait accounting (and the
+     * compiler's, which would otherwise drain the counter at every reuse of these registers)
+     * starts clean */
+    __builtin_amdgcn_s_waitcnt(0xF70);
 }
 
-/* The pair-group's flagged coefficients as per-lane task bits: lane t < 24 <-> block
- * bl = t / 3 of the pair-group, channel c = t % 3, bit 8v + u for coefficient (u, v).
- * L.seenv[q][v] holds the lanes (h, n = 8c + u) of group q that flagged row v in either of
- * their two blocks 2h, 2h + 1: both blocks get the task. */
-__device__ __forceinline__ uint64_t mx_task_bits(const uint64_t *seenv, unsigned lane,
-                                                 unsigned seenq, unsigned nvalid)
+/*
+ * Rare path of one group (some lane's running max says a coefficient is inside the band):
+ * re-test every coefficient (the fast path's arithmetic exactly) and record the flagged ones
+ * with the flagged blocks' pixel rows (already in registers) copied to LDS slots; the caller
+ * guarantees room for one record and four slots.
+ */
+__device__ __forceinline__ void mx_record(MxLds &L, int &nrec, int &nslot, const mx_f2 (&F)[8],
+                                          const float (&w)[8], const float (&lsq)[8], mx_u4 ld,
+                                          unsigned gb0)
 {
-    uint64_t M = 0;
-    const unsigned bl = lane / 3u, c = lane - 3u * bl, q = bl >> 2, hh = (bl >> 1) & 1u;
-    if (lane < 24 && bl < nvalid && ((seenq >> q) & 1u)) {
+    const unsigned lane = mx_lane();
+    const unsigned n = lane & 31u;
+    const unsigned m = lane & 31u, hA = lane >> 5;
+    const unsigned iA = (m & 3u) + 4u * (m >> 3);
+    const unsigned blkA = 2u * ((m >> 2) & 1u) + (iA & 1u), yA = iA >> 1;
+    uint32_t bits = 0;
 #pragma unroll
-        for (int v = 0; v < 8; v++)
-            M |= ((seenv[8 * q + v] >> (32u * hh + 8u * c)) & 0xffull) << (8 * v);
+    for (int v = 7; v >= 0; v--) {
+        const float t0 = __builtin_fmaf(F[v].x, w[v], kMagic);
+        const float t1 = __builtin_fmaf(F[v].y, w[v], kMagic);
+        const float d0 = __builtin_fmaf(F[v].x, w[v], -(t0 - kMagic));
+        const float d1 = __builtin_fmaf(F[v].y, w[v], -(t1 - kMagic));
+        const float e0 = __builtin_fmaf(d0, d0, -lsq[v]);
+        const float e1 = __builtin_fmaf(d1, d1, -lsq[v]);
+        bits = (bits << 2) | (e1 >= 0.0f ? 2u : 0u) | (e0 >= 0.0f ? 1u : 0u);
     }
-    return M;
+    if (n >= 24) bits = 0;
+    /* flagged blocks of the group: bit (2h + j) */
+    const uint64_t m0 = __ballot((bits & 0x5555u) != 0), m1 = __ballot((bits & 0xaaaau) != 0);
+    const unsigned blkmask = ((uint32_t)m0 ? 1u : 0u) | ((uint32_t)m1 ? 2u : 0u) |
+                             ((m0 >> 32) ? 4u : 0u) | ((m1 >> 32) ? 8u : 0u);
+    if (!blkmask) return;
+    const int r = nrec;
+    L.rbits[r][lane] = (uint16_t)bits;
+    if (lane == 0) L.rblk[r] = gb0;
+    if (lane < 4) {
+        const bool fl = (blkmask >> lane) & 1u;
+        L.rslot[r][lane] = fl ? (uint8_t)(nslot + __builtin_popcount(blkmask & ((1u << lane) - 1u))) : 0;
+    }
+    if ((blkmask >> blkA) & 1u) {
+        const int sl = nslot + __builtin_popcount(blkmask & ((1u << blkA) - 1u));
+        uint8_t *row = &L.pix[sl][yA][8 * hA];
+        *(uint32_t *)(row + 0) = ld.x;
+        *(uint32_t *)(row + 4) = ld.y;
+        *(uint32_t *)(row + 8) = ld.z;
+        *(uint32_t *)(row + 12) = ld.w;
+    }
+    nrec++;
+    nslot += __builtin_popcount(blkmask);
 }
 
-/* Move task bits M (blocks blk0 + lane / 3) into the LDS queue while it has room; the bits
- * that did not fit stay in M.  Returns the new queue length. */
-__device__ __forceinline__ int mx_enqueue(MxLds &L, int nq, uint64_t &M, unsigned blk0,
-                                          unsigned lane)
+/* Colour conversion + row DCT of one group of 4 blocks through the matrix cores: R[y] =
+ * (block 2h, block 2h + 1) at pixel row y for this lane's column n. */
+__device__ __forceinline__ void mx_rows(mx_u4 ld, uint32_t K, uint32_t selb, const mx_h8 (&B)[2 * kParts],
+                                        mx_f2 (&R)[8])
 {
-    const unsigned bl = lane / 3u, c = lane - 3u * bl;
-    for (;;) {
-        const uint64_t act = __ballot(M != 0);
-        if (!act || nq == kMxCap) break;
-        const int room = kMxCap - nq, rk = mx_rank(act);
-        if (M != 0 && rk < room) {
-            const int k = __builtin_ctzll(M);
-            M &= M - 1;
-            L.tblk[nq + rk] = blk0 + bl;
-            L.tcode[nq + rk] = (uint16_t)(c << 6 | k);
-        }
-        nq += std::min((int)__popcll(act), room);
-    }
-    return nq;
-}
-
-/* Rows of one 4-block group through the matrix cores.  Register r of the 32x32 result holds
- * block 2h + (r & 1), pixel row r >> 1 of column n = lane & 31 (the A-row mapping in k_mx),
- * so R[y] = (block 2h, block 2h + 1) at pixel row y is an aligned register pair. */
-__device__ __forceinline__ void mx_rows(mx_h8 A0, mx_h8 A1, const mx_h8 (&B)[6], mx_f2 (&R)[8])
-{
-    mx_f16 ah = {}, al = {};
-    ah = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B[0], ah, 0, 0, 0);
+    const uint32_t s0 = 0x05010500u, s1 = 0x05030502u;
+    const mx_u4 a0 = {mx_cvt2(K, ld.x, s0), mx_cvt2(K, ld.x, s1), mx_cvt2(K, ld.y, s0),
+                      mx_cvt2(K, ld.y, s1)};
+    const mx_u4 a1 = {mx_cvt2(K, ld.z, selb), mx_cvt2(K, ld.z, s1), mx_cvt2(K, ld.w, s0),
+                      mx_cvt2(K, ld.w, s1)};
+    const mx_h8 A0 = __builtin_bit_cast(mx_h8, a0), A1 = __builtin_bit_cast(mx_h8, a1);
+    const mx_f16 zero = {};
+    mx_f16 ah = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B[0], zero, 0, 0, 0);
+    mx_f16 al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B[2], zero, 0, 0, 0);
     ah = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B[1], ah, 0, 0, 0);
-    al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B[2], al, 0, 0, 0);
     al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B[3], al, 0, 0, 0);
-    al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B[4], al, 0, 0, 0);
-    al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B[5], al, 0, 0, 0);
+    if (kParts == 3) {
+        al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B[4 % (2 * kParts)], al, 0, 0, 0);
+        al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B[5 % (2 * kParts)], al, 0, 0, 0);
+    }
 #pragma unroll
     for (int y = 0; y < 8; y++)
         R[y] = __builtin_elementwise_fma(mx_f2{al[2 * y], al[2 * y + 1]},
@@ -308,196 +438,172 @@ struct MxPair {
 __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
 {
     __shared__ MxLds s_lds[4];
-    const MxG g = mx_geom(a);
+    MxG g;
+    g.rgb = a.g.rgb;
+    g.out = a.g.out;
+    g.pitch = a.g.in_pitch;
+    g.fstride = a.g.in_fstride;
+    g.ofstride = a.g.out_fstride;
+    g.bpr = (unsigned)a.g.bpr;
+    g.nb = (unsigned)a.g.nb;
+    g.total = (unsigned)a.g.nb * (unsigned)a.g.nframes;
+    g.row0 = a.g.row0;
+    g.quality = a.quality;
+    g.force = a.force_exact;
+#pragma unroll
+    for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+
     const unsigned lane = threadIdx.x & 63u;
     MxLds &L = s_lds[threadIdx.x >> 6];
-    const unsigned nb = g.nb, bpr = g.bpr;
-    const unsigned pgf = (nb + 7u) / 8u, npg = pgf * (unsigned)a.g.nframes;
-    const bool force = a.force_exact != 0;
-    /* each wave walks a contiguous range of pair-groups (incremental addressing, no division
-     * per pair-group) */
+    /* each wave walks a contiguous range of steps */
+    const unsigned nsteps = (g.total + 7u) / 8u;
     const unsigned nw = gridDim.x * 4u;
     const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    const unsigned pg_end = (unsigned)(((unsigned long long)npg * (wv + 1)) / nw);
-    unsigned pg = (unsigned)(((unsigned long long)npg * wv) / nw);
-    if (pg >= pg_end) return;
-    /* position of pair-group pg: frame f, pair-group pgi in it, first block b0 = (r0, c0) */
-    unsigned f = pg / pgf, pgi = pg - f * pgf;
-    unsigned r0 = (8u * pgi) / bpr, c0 = 8u * pgi - r0 * bpr;
+    const unsigned s_end = (unsigned)(((unsigned long long)nsteps * (wv + 1)) / nw);
+    unsigned s = (unsigned)(((unsigned long long)nsteps * wv) / nw);
+    if (s >= s_end) return;
 
-    /* A-operand row of this lane (both groups): register r = (m & 3) + 4 (m >> 3) of lane
-     * half (m >> 2) & 1 of the result is block 2((m >> 2) & 1) + (r & 1), pixel row r >> 1 */
-    const unsigned h = lane >> 5, m = lane & 31u;
-    const unsigned rA = (m & 3u) + 4u * (m >> 3);
-    const unsigned blkA = 2u * ((m >> 2) & 1u) + (rA & 1u), yA = rA >> 1;
-    const long long laneoff = (long long)yA * g.pitch + 24 * blkA;   /* within the group */
-    const unsigned n = lane & 31u;
-    const unsigned last_b = nb - 1u, last_r = last_b / bpr, last_c = last_b - last_r * bpr;
-    const uint32_t ua0 = h ? g.u2 : g.u0, ua1 = h ? g.u3 : g.u1;
+    /* A-operand row of this lane (both groups): block blkA of the group, pixel row yA */
+    const unsigned hA = lane >> 5, m = lane & 31u;
+    const unsigned iA = (m & 3u) + 4u * (m >> 3);
+    const unsigned blkA = 2u * ((m >> 2) & 1u) + (iA & 1u), yA = iA >> 1;
+    const uint32_t laneoff = (uint32_t)(yA * (unsigned)g.pitch + 24u * blkA + 8u * hA);
+    const uint32_t K = 0x64646481u;
+    const uint32_t selb = hA ? 0x05010500u : 0x05010504u;
 
-    /* The lane's 8-byte loads (bytes 8h.., and 16..23) of both groups of the pair-group at
-     * (F, R0, C0, B0).  Pair-groups inside one block-row, clear of its last block, take one
-     * add per load; the others (row wrap, the x0 = -8 quirk, underflow, frame tail) the
-     * general per-lane path. */
-    mx_u2 LdA[2][2], LdB[2][2];
-#define MX_LOAD(Ld, F, R0, C0, B0)                                                          \
-    do {                                                                                    \
-        if ((C0) + 8u < bpr) {                                                              \
-            const uint8_t *base = g.rgb + (long long)(F) * g.fstride +                      \
-                                  (long long)(8u * (R0)) * g.pitch + 24ll * (C0) + laneoff; \
-            _Pragma("unroll") for (int q = 0; q < 2; q++) {                                 \
-                const mx_u2 *pw = (const mx_u2 *)__builtin_assume_aligned(base + 96 * q, 8); \
-                (Ld)[q][0] = pw[h];                                                         \
-                (Ld)[q][1] = pw[2];                                                         \
-            }                                                                               \
-        } else {                                                                            \
-            _Pragma("unroll") for (int q = 0; q < 2; q++) {                                 \
-                const unsigned off = 4u * (unsigned)q + blkA;                               \
-                unsigned c = (C0) + off, r = (R0);                                          \
-                while (c >= bpr) {                                                          \
-                    c -= bpr;                                                               \
-                    r++;                                                                    \
-                }                                                                           \
-                const bool tail = (B0) + off > last_b;                                      \
-                r = tail ? last_r : r;                                                      \
-                c = tail ? last_c : c;                                                      \
-                bool un;                                                                    \
-                const uint8_t *p8 = mx_row(g, (F), r, c, yA, &un);                          \
-                const mx_u2 *pw = (const mx_u2 *)__builtin_assume_aligned(p8, 8);           \
-                const mx_u2 l0 = pw[h], l1 = pw[2];                                         \
-                (Ld)[q][0] = un ? mx_u2{ua0, ua1} : l0;                                     \
-                (Ld)[q][1] = un ? mx_u2{g.u4, g.u5} : l1;                                   \
-            }                                                                               \
-        }                                                                                   \
-    } while (0)
-
-    /* flagged pair-groups: record k of this wave at slot pg_begin + k of the workspace
-     * (rec_pg = pair-group | seenq << 30, rec_sv = its 16 lane masks), exact pass after the
-     * tile loop, where none of its values are live */
-    const unsigned pg_begin = pg;
-    unsigned nrec = 0;
-    const jx_mxtab &T = g_mxtab[g.quality];
-    float w[8], lim[8];
+    /* output column n = 8c + u of this lane; C-layout lane half h = blocks 2h, 2h + 1 */
+    const unsigned n = lane & 31u, h = lane >> 5;
+    const unsigned cz = (n >> 3) % 3u, uz = n & 7u;     /* padding columns 24..31 = Y again */
+    const jx_mxtab &T = g_mxtab[g.force ? 1 : 0][g.quality];
+    float w[8], lsq[8];
     uint32_t zo[8];
 #pragma unroll
     for (int v = 0; v < 8; v++) {
         w[v] = T.w[n][v];
-        lim[v] = force && n < 24 ? -1.0f : T.lim[n][v];
-        zo[v] = g_mxzo[lane][v];
+        lsq[v] = T.lsq[n][v];
+        zo[v] = mx_stage_base(cz) + 256u * h + 2u * (unsigned)kMxScan[v][uz];
     }
-    mx_h8 B[6];
+    mx_h8 B[2 * kParts];
 #pragma unroll
-    for (int i = 0; i < 6; i++) B[i] = __builtin_bit_cast(mx_h8, g_mxB[i][lane]);
-    /* position of the pair-group after (F, P, R, C): scalar */
-#define MX_NEXT(F, P, R, C, FN, PN, RN, CN)                                                 \
-    do {                                                                                    \
-        FN = F;                                                                             \
-        PN = (P) + 1u;                                                                      \
-        RN = R;                                                                             \
-        CN = (C) + 8u;                                                                      \
-        if (PN == pgf) {                                                                    \
-            FN = (F) + 1u;                                                                  \
-            PN = 0;                                                                         \
-            RN = 0;                                                                         \
-            CN = 0;                                                                         \
-        } else {                                                                            \
-            while (CN >= bpr) {                                                             \
-                CN -= bpr;                                                                  \
-                RN++;                                                                       \
-            }                                                                               \
-        }                                                                                   \
-    } while (0)
-    /* One pair-group from the pixels in LC; the pixels of pair-group pg + 2 are loaded into
-     * LC as soon as its A operands are formed (two pair-groups in flight per wave). */
-#define MX_STEP(LC)                                                                         \
-    do {                                                                                    \
-        unsigned f2_, p2_, r2_, c2_;                                                        \
-        MX_NEXT(f1, p1, r1, c1, f2_, p2_, r2_, c2_);                                        \
-        const mx_h8 bias = (mx_h8){(_Float16)1.0f, 0, 0, 0, 0, 0, 0, 0};                    \
-        mx_h8 A[2][2];                                                                      \
-        _Pragma("unroll") for (int q = 0; q < 2; q++) {                                     \
-            A[q][0] = mx_cvt8(LC[q][0]);                                                    \
-            A[q][1] = h ? bias : mx_cvt8(LC[q][1]);                                         \
-        }                                                                                   \
-        if (pg + 2u < pg_end) MX_LOAD(LC, f2_, r2_, c2_, 8u * p2_);                          \
-        const unsigned b0 = 8u * pgi;                                                       \
-        const unsigned slot = pg_begin + nrec;                                              \
-        unsigned seenq = 0;                                                                 \
-        _Pragma("unroll") for (int q = 0; q < 2; q++) {                                     \
-            mx_f2 R[8], F[8];                                                               \
-            mx_rows(A[q][0], A[q][1], B, R);                                                \
-            jx_fdct8<PairOps<MxPair>>(R, F);                                                \
-            uint64_t sv[8];                                                                 \
-            _Pragma("unroll") for (int v = 0; v < 8; v++) {                                 \
-                const mx_f2 wv2 = mx_f2{w[v], w[v]}, M2 = mx_f2{kMagic, kMagic};            \
-                const mx_f2 tm = __builtin_elementwise_fma(F[v], wv2, M2);                  \
-                const mx_f2 rr = tm - M2;                                                   \
-                const mx_f2 d = __builtin_elementwise_fma(F[v], wv2, -rr);                  \
-                /* blocks 2h and 2h + 1 of group q: stage offsets (4q + 2h + b) * 128 */    \
-                *(uint16_t *)(L.stage + zo[v] + 512u * q) = (uint16_t)__float_as_uint(tm.x); \
-                *(uint16_t *)(L.stage + zo[v] + 512u * q + 128u) =                          \
-                    (uint16_t)__float_as_uint(tm.y);                                        \
-                const float e = __builtin_fmaxf(__builtin_fabsf(d.x), __builtin_fabsf(d.y)); \
-                sv[v] = __builtin_amdgcn_ballot_w64(e >= lim[v]);                           \
-            }                                                                               \
-            const uint64_t seen =                                                           \
-                ((sv[0] | sv[1]) | (sv[2] | sv[3])) | ((sv[4] | sv[5]) | (sv[6] | sv[7]));  \
-            if (!JX_MX_DBG_NORARE && seen) {   /* rare: record which lanes, per row v */    \
-                seenq |= 1u << q;                                                           \
-                if (lane == 0) {                                                            \
-                    uint64_t *rs = a.rec_sv + (size_t)slot * 16 + 8 * q;                    \
-                    _Pragma("unroll") for (int v = 0; v < 8; v++) rs[v] = sv[v];            \
-                }                                                                           \
-            }                                                                               \
-        }                                                                                   \
-        if (seenq) {                                                                        \
-            if (lane == 0) a.rec_pg[slot] = pg | seenq << 30;                               \
-            nrec++;                                                                         \
-        }                                                                                   \
-        mx_wave_sync();                                                                     \
-        /* stores: channel c's 8 blocks x 128 B are contiguous, 16 B per lane */            \
-        int16_t *ob = g.out + (long long)f * g.ofstride + (long long)b0 * 64 + lane * 8;    \
-        const bool st = b0 + (lane >> 3) < nb;                                              \
-        _Pragma("unroll") for (int c = 0; c < 3; c++) {                                     \
-            const mx_u4 val = *(const mx_u4 *)(L.stage + c * 1024 + lane * 16);             \
-            if (st) __builtin_nontemporal_store(val, (mx_u4 *)(ob + (long long)c * nb * 64)); \
-        }                                                                                   \
-        mx_wave_sync();                                                                     \
-        f = f1; pgi = p1; r0 = r1; c0 = c1;                                                 \
-        f1 = f2_; p1 = p2_; r1 = r2_; c1 = c2_;                                             \
-        pg++;                                                                               \
-    } while (0)
+    for (int i = 0; i < 2 * kParts; i++) B[i] = __builtin_bit_cast(mx_h8, g_mxB[i][lane]);
 
-    unsigned f1, p1, r1, c1;                 /* position of pair-group pg + 1 */
-    MX_NEXT(f, pgi, r0, c0, f1, p1, r1, c1);
-    MX_LOAD(LdA, f, r0, c0, 8u * pgi);
-    if (pg + 1u < pg_end) MX_LOAD(LdB, f1, r1, c1, 8u * p1);
-    while (pg < pg_end) {
-        MX_STEP(LdA);
-        if (pg >= pg_end) break;
-        MX_STEP(LdB);
+    int nrec = 0, nslot = 0;               /* flagged-group records, pixel slots in use */
+    MxPos P;
+    {
+        const unsigned b0 = 8u * s;
+        P.f = b0 / g.nb;
+        P.bi = b0 - P.f * g.nb;
+        P.r = P.bi / g.bpr;
+        P.c = P.bi - P.r * g.bpr;
     }
-#undef MX_STEP
-#undef MX_NEXT
-    if (JX_MX_DBG_NODRAIN || !nrec) return;
-    /* exact pass over the recorded pair-groups' flagged coefficients */
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int nq = 0;
-    for (unsigned k = 0; k < nrec; k++) {
-        const unsigned rec = a.rec_pg[pg_begin + k];
-        const unsigned p = rec & 0x3fffffffu, sq = rec >> 30;
-        const unsigned fr = p / pgf, bb0 = 8u * (p - fr * pgf);
-        uint64_t M = mx_task_bits(a.rec_sv + (size_t)(pg_begin + k) * 16, lane, sq,
-                                  std::min(8u, nb - bb0));
-        for (;;) {
-            nq = mx_enqueue(L, nq, M, fr * nb + bb0, lane);
-            if (__ballot(M != 0) == 0) break;
-            mx_drain(L, nq, g, lane);
-            nq = 0;
+    /* the loads of the wave's first step; every later step issues the next step's loads
+     * right after waiting for its own (vmcnt counts loads, LDS-DMA and stores in issue order:
+     * younger than this step's DMA are only the previous step's three stores) */
+    uint32_t un = mx_issue(g, P, 8u * s, mx_simple(P, g, 8u * s), laneoff, L.in[s & 1u]);
+    __builtin_amdgcn_s_waitcnt(0xF70);           /* vmcnt(0): tables, operands, first step */
+    bool first = true;
+    for (; s < s_end; s++) {
+        const unsigned b0 = 8u * s;
+        const MxPos PC = P;
+        if (!first) __builtin_amdgcn_s_waitcnt(0xF73);   /* vmcnt(3) */
+        first = false;
+        mx_wave_sync();
+        const uint32_t uc = un;
+        mx_advance(P, g);
+        if (s + 1u < s_end)
+            un = mx_issue(g, P, b0 + 8u, mx_simple(P, g, b0 + 8u), laneoff, L.in[(s + 1u) & 1u]);
+        const bool underrow = !mx_simple(PC, g, b0) && __ballot(uc != 0) != 0;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            mx_u4 ld = L.in[s & 1u][q][lane];
+            if (underrow && ((uc >> q) & 1u))       /* rare: the underflow row */
+                ld = hA ? mx_u4{g.u[2], g.u[3], g.u[4], g.u[5]} : mx_u4{g.u[0], g.u[1], g.u[2], g.u[3]};
+            mx_f2 R[8], F[8];
+#if defined(JX_MX_DBG_NOCOMPUTE)  /* timing experiments only: the stage writes, no transform */
+#pragma unroll
+            for (int v = 0; v < 8; v++) {
+                *(uint16_t *)(L.stage + zo[v] + 512u * q) = (uint16_t)(ld[v & 3] >> (v & 16));
+                *(uint16_t *)(L.stage + zo[v] + 512u * q + 128u) = (uint16_t)(ld[(v + 1) & 3]);
+            }
+            if (ld.x == 0xdeadbeefu)
+#endif
+            {
+#ifdef JX_MX_DBG_NOMFMA          /* timing experiments only: R by VALU from the bytes */
+#pragma unroll
+            for (int y = 0; y < 8; y++)
+                R[y] = mx_f2{(float)((ld[y & 3] >> (8 * (y >> 2))) & 0xffu) - 128.0f,
+                             (float)((ld[(y + 1) & 3] >> 8) & 0xffu) - 128.0f} * 7.0f;
+#else
+            mx_rows(ld, K, selb, B, R);
+#endif
+            jx_fdct8<PairOps<MxPair>>(R, F);
+            }
+            float emax = -1.0f;
+#if defined(JX_MX_DBG_NOCOMPUTE)
+            if (ld.x == 0xdeadbeefu)
+#endif
+#pragma unroll
+            for (int v = 0; v < 8; v++) {
+                /* quant_coef: tm = F w + 1.5 2^23 (low 16 bits = the rounded int16), d = F w -
+                 * rint (exact); band test d*d - lsq >= 0 folded into a running max */
+                const float t0 = __builtin_fmaf(F[v].x, w[v], kMagic);
+                const float t1 = __builtin_fmaf(F[v].y, w[v], kMagic);
+#ifndef JX_MX_DBG_NOSTAGE        /* timing experiments only: no zig-zag LDS writes */
+                *(uint16_t *)(L.stage + zo[v] + 512u * q) = (uint16_t)__float_as_uint(t0);
+                *(uint16_t *)(L.stage + zo[v] + 512u * q + 128u) = (uint16_t)__float_as_uint(t1);
+#else
+                emax += __uint_as_float(__float_as_uint(t0) ^ __float_as_uint(t1)) * 1e-30f;
+#endif
+                const float d0 = __builtin_fmaf(F[v].x, w[v], -(t0 - kMagic));
+                const float d1 = __builtin_fmaf(F[v].y, w[v], -(t1 - kMagic));
+                const float e0 = __builtin_fmaf(d0, d0, -lsq[v]);
+                const float e1 = __builtin_fmaf(d1, d1, -lsq[v]);
+                emax = __builtin_fmaxf(emax, __builtin_fmaxf(e0, e1));
+            }
+#ifdef JX_MX_DBG_NORARE           /* timing experiments only: no exact pass */
+            if (emax == 12345.0f)
+#else
+            if (__ballot(emax >= 0.0f))              /* rare: some coefficient in the band */
+#endif
+                mx_record(L, nrec, nslot, F, w, lsq, ld, b0 + 4u * q);
+            __builtin_amdgcn_sched_barrier(0);
         }
+        mx_wave_sync();
+        /* exact pass when the next step might not find room (rarely before the wave's end) */
+        if (nrec > kRecs - 2 || nslot > kSlots - 8) {
+            mx_drain(L, nrec, g, b0);
+            nrec = 0;
+            nslot = 0;
+        }
+        /* stores: channel c's 8 blocks x 128 B are contiguous, 16 B per lane; always three
+         * store instructions (the vmcnt(3) above counts on it) */
+#ifdef JX_MX_DBG_NOSTORE        /* timing experiments only: no coefficient stores */
+        if (b0 == 0xdeadbeefu)
+#endif
+        if (mx_simple(PC, g, b0)) {
+            int16_t *ob = g.out + (long long)PC.f * g.ofstride + (long long)PC.bi * 64 + lane * 8;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const mx_u4 val = *(const mx_u4 *)(L.stage + mx_stage_base(c) + lane * 16);
+                __builtin_nontemporal_store(val, (mx_u4 *)(ob + (long long)c * g.nb * 64));
+            }
+        } else {
+            /* lanes past the end rewrite the last block's chunk with its own bytes */
+            const unsigned lane = mx_lane();
+            const unsigned bl = b0 + (lane >> 3), b = bl < g.total ? bl : g.total - 1u;
+            const unsigned f = b / g.nb, bi = b - f * g.nb;
+            const unsigned src = bl < g.total ? lane : ((g.total - 1u - b0) << 3) | (lane & 7u);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const mx_u4 val = *(const mx_u4 *)(L.stage + mx_stage_base(c) + src * 16);
+                __builtin_nontemporal_store(
+                    val, (mx_u4 *)(g.out + (long long)f * g.ofstride +
+                                   ((long long)c * g.nb + bi) * 64 + (lane & 7u) * 8));
+            }
+        }
+        mx_wave_sync();
     }
-    if (nq) mx_drain(L, nq, g, lane);
-#undef MX_LOAD
+    if (nrec) mx_drain(L, nrec, g, 0xffffffffu);
 }
 
 int mx_rc(hipError_t e) { return e == hipSuccess ? JPGX_OK : JPGX_EHIP; }
@@ -507,33 +613,40 @@ std::once_flag g_mx_once[kMaxDev];
 int g_mx_rc[kMaxDev];
 int g_mx_waves[kMaxDev];
 
+/* a float <= lim^2 (-1 where lim < 0: every coefficient flagged) */
+float mx_lsq(float lim)
+{
+    if (!(lim > 0.0f)) return -1.0f;
+    const double l2 = (double)lim * (double)lim;
+    float s = (float)l2;
+    if ((double)s > l2) s = nextafterf(s, 0.0f);
+    return s;
+}
+
 int mx_tables_for_current_device(int *waves)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return JPGX_ENODEV;
     std::call_once(g_mx_once[dev], [dev]() {
-        std::vector<jx_mxtab> tab(JX_MAXQ + 1);
+        std::vector<jx_mxtab> tab(2 * (JX_MAXQ + 1));
         memset(tab.data(), 0, tab.size() * sizeof(jx_mxtab));
         int rc = JPGX_OK;
         for (int q = 1; q <= JX_MAXQ && !rc; q++) {
-            rc = jx_plan_tables_mx(q, tab[q].w, tab[q].lim, tab[q].q);
-            for (int n = 24; n < 32; n++)
-                for (int v = 0; v < 8; v++) {
-                    tab[q].w[n][v] = 0.0f;
-                    tab[q].lim[n][v] = 3.0e38f;
-                }
-        }
-        uint16_t ops[6][64][8];
-        if (!rc) rc = jx_mx_operands(ops);
-        static const int scan[8][8] = JX_SCAN_ORDER_INIT;
-        uint32_t zo[64][8];
-        for (int l = 0; l < 64; l++)
-            for (int v = 0; v < 8; v++) {   /* columns 24..31 (padding) write to stage[3] */
-                const int n = l & 31;
-                zo[l][v] = (uint32_t)((n >> 3) * 1024 + 256 * (l >> 5) +
-                                      2 * (n < 24 ? scan[v][n & 7] : v * 8 + (n & 7)));
+            float w[24][8], lim[24][8];
+            int16_t qq[2][64];
+            rc = jx_plan_tables_mx(q, w, lim, qq);
+            for (int f = 0; f < 2; f++) {
+                jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
+                memcpy(t.q, qq, sizeof qq);
+                for (int n = 0; n < 32; n++)        /* columns 24..31 repeat Y's 0..7 */
+                    for (int v = 0; v < 8; v++) {
+                        t.w[n][v] = w[n % 24][v];
+                        t.lsq[n][v] = f ? -1.0f : mx_lsq(lim[n % 24][v]);
+                    }
             }
-        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxzo), zo, sizeof zo));
+        }
+        uint16_t ops[2 * kParts][64][8];
+        if (!rc) rc = jx_mx_operands(ops);
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxtab), tab.data(),
                                               tab.size() * sizeof(jx_mxtab)));
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxB), ops, sizeof ops));
@@ -552,27 +665,16 @@ int mx_tables_for_current_device(int *waves)
 
 }  // namespace
 
-/* workspace bytes k_mx needs: a record slot per pair-group */
-extern "C" size_t jx_mx_workspace(size_t nb, int nframes)
-{
-    const size_t npg = (nb + 7) / 8 * (size_t)nframes;
-    return npg * (16 * sizeof(uint64_t) + sizeof(unsigned)) + 256;
-}
-
-/* k_mx over every frame of the stripe (4:4:4 / reference-parity output). */
-extern "C" int jx_launch_mx(const jx_xform_args *xa_in, void *ws, size_t ws_bytes, void *stream)
+/* k_mx over every frame of the stripe (4:4:4 / reference-parity output); no workspace. */
+extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)
 {
     int waves = 0;
     const int rc = mx_tables_for_current_device(&waves);
     if (rc) return rc;
-    jx_xform_args xa = *xa_in;
-    const size_t nb = (size_t)xa.g.nb, npg = (nb + 7) / 8 * (size_t)xa.g.nframes;
-    if (npg >= (1u << 30) || ws_bytes < jx_mx_workspace(nb, xa.g.nframes) || ((uintptr_t)ws & 15))
-        return JPGX_EWORKSPACE;
-    xa.rec_sv = (uint64_t *)ws;
-    xa.rec_pg = (unsigned *)((uint8_t *)ws + npg * 16 * sizeof(uint64_t));
-    const size_t w = std::min<size_t>(npg, (size_t)std::max(waves, 4));
+    const size_t total = (size_t)xa->g.nb * (size_t)xa->g.nframes;
+    const size_t nsteps = (total + 7) / 8;
+    const size_t w = std::min<size_t>(nsteps, (size_t)std::max(waves, 4));
     const unsigned grid = (unsigned)((w + 3) / 4);
-    hipLaunchKernelGGL(k_mx, dim3(grid), dim3(256), 0, (hipStream_t)stream, xa);
+    hipLaunchKernelGGL(k_mx, dim3(grid), dim3(256), 0, (hipStream_t)stream, *xa);
     return mx_rc(hipGetLastError());
 }

@@ -363,16 +363,22 @@ extern "C" {
  *
  * k_mx multiplies each pixel row, 24 bytes b_k (k = 3x + p, plane p of pixel x) shifted to
  * s_k = b_k - 128 (exact in f16), by B[k][n] = a[c][p] cos((2x+1)u pi/16), n = 8c + u, with
- * the bias row k = 24 (input 1.0) carrying 8 * (128 sum_p a[c][p] + shift_c) for u = 0 (the
- * level shift, preprocess.c:160-162,186-188; the true cosines of u > 0 sum to 0).  B is
- * split into three f16 parts:
+ * a bias row (input 1.0) carrying 8 * (128 sum_p a[c][p] + shift_c) for u = 0 (the level
+ * shift, preprocess.c:160-162,186-188; the true cosines of u > 0 sum to 0).  B is split into
+ * JX_MX_PARTS f16 parts:
  *   Bh  B rounded to a multiple of 2^-11 (|B| < 1: 11 bits, an f16; bias: its f16),
- *   Bl  f16(2^12 (B - Bh)),  Bm  f16(2^12 (B - Bh) - Bl)   (scaled: normal f16 numbers).
+ *   Bl  f16(2^12 (B - Bh)),  [Bm  f16(2^12 (B - Bh) - Bl)]   (scaled: normal f16 numbers).
  * acc_h = sum_k s_k Bh_k is EXACT whatever the order of the MFMA's additions: every product
  * and every partial sum is a multiple of 2^-11 below 2^13 in magnitude (24 bits).  acc_l =
- * sum_k s_k (Bl_k + Bm_k) 2^-12 is below 1 in magnitude; its additions (at most 70) are charged
- * one ulp each.  R = fl(acc_h + 2^-12 acc_l) (one fma) then enters the column pass (jx_fdct8,
- * FOps) as usual.
+ * sum_k s_k (Bl_k [+ Bm_k]) 2^-12 is below 1 in magnitude; each of its additions is charged
+ * one ulp.  R = fl(acc_h + 2^-12 acc_l) (one fma) then enters the column pass (jx_fdct8,
+ * FOps, two blocks per v_pk_* pair) as usual.
+ *
+ * K layout of the two 32x32x16 k-steps (lane half hA = lane >> 5 holds k = 8 hA + j, j < 8):
+ * each lane loads 16 pixel-row bytes at offset 8 hA, so
+ *   k-step 0:  hA = 0: bytes 0..7      hA = 1: bytes 8..15
+ *   k-step 1:  hA = 0: j = 0 the bias (A = 1.0), j > 0 weight 0 (A = bytes 9..15, ignored)
+ *              hA = 1: bytes 16..23
  */
 static const double kMxA[3][3] = {{0.299, 0.587, 0.114},
                                   {-0.168736, 0.331264, -0.5},
@@ -401,7 +407,7 @@ static long double f16_round(long double x, uint16_t *bits)
     return v;
 }
 
-/* exact B[k][n] (k < 24: matrix, k = 24: bias row, else 0; n < 24) */
+/* exact B[k][n] (k < 24: matrix, k = 24: bias row; n < 24) */
 static long double mx_exact(int k, int n)
 {
     if (n >= 24) return 0;
@@ -419,14 +425,15 @@ static long double mx_exact(int k, int n)
 }
 
 struct MxSplit {
-    long double h[32][32], l[32][32], m[32][32];
-    uint16_t bh[32][32], bl[32][32], bm[32][32];
+    long double h[25][32], l[25][32], m[25][32];      /* m = 0 unless JX_MX_PARTS == 3 */
+    uint16_t bh[25][32], bl[25][32], bm[25][32];
 };
 
 static int mx_split(MxSplit &S)
 {
-    for (int k = 0; k < 32; k++)
-        for (int n = 0; n < 32; n++) {
+    memset(&S, 0, sizeof S);
+    for (int k = 0; k < 25; k++)
+        for (int n = 0; n < 24; n++) {
             const long double B = mx_exact(k, n);
             long double hv;
             if (k < 24) {
@@ -441,9 +448,11 @@ static int mx_split(MxSplit &S)
              * would flush the third part to 0); k_mx takes R = acc_h + 2^-12 acc_l, exact
              * scaling.  S.l / S.m hold the unscaled values. */
             const long double ls = f16_round(ldexpl(B - hv, 12), &S.bl[k][n]);
-            const long double ms = f16_round(ldexpl(B - hv, 12) - ls, &S.bm[k][n]);
             S.l[k][n] = ldexpl(ls, -12);
-            S.m[k][n] = ldexpl(ms, -12);
+            if (JX_MX_PARTS == 3) {
+                const long double ms = f16_round(ldexpl(B - hv, 12) - ls, &S.bm[k][n]);
+                S.m[k][n] = ldexpl(ms, -12);
+            }
         }
     for (int n = 0; n < 24; n++) {              /* acc_h exactness: partial sums < 2^13 */
         long double sh = fabsl(S.h[24][n]);
@@ -453,19 +462,29 @@ static int mx_split(MxSplit &S)
     return JPGX_OK;
 }
 
-extern "C" int jx_mx_operands(uint16_t ops[6][64][8])
+/* source row of B for k-step ks, lane half hA, element j (the K layout above); -1: weight 0 */
+static int mx_src(int ks, int hA, int j)
+{
+    if (ks == 0) return 8 * hA + j;
+    if (hA == 0) return j == 0 ? 24 : -1;
+    return 16 + j;
+}
+
+extern "C" int jx_mx_operands(uint16_t ops[2 * JX_MX_PARTS][64][8])
 {
     static MxSplit S;
     const int rc = mx_split(S);
     if (rc) return rc;
-    /* operand i = 2 * part + kstep; lane l holds B[16 kstep + 8 (l >> 5) + j][l & 31] */
-    for (int part = 0; part < 3; part++)
+    /* operand i = 2 * part + kstep; lane l holds B[mx_src(kstep, l >> 5, j)][l & 31]; the
+     * MFMA's padding columns 24..31 repeat Y's columns 0..7 (k_mx: those lanes write the same
+     * values to the same stage addresses as lanes 0..7 instead of needing a dummy area) */
+    for (int part = 0; part < JX_MX_PARTS; part++)
         for (int ks = 0; ks < 2; ks++)
             for (int l = 0; l < 64; l++)
                 for (int j = 0; j < 8; j++) {
-                    const int k = 16 * ks + 8 * (l >> 5) + j, n = l & 31;
+                    const int k = mx_src(ks, l >> 5, j), n = (l & 31) % 24;
                     ops[2 * part + ks][l][j] =
-                        part == 0 ? S.bh[k][n] : (part == 1 ? S.bl[k][n] : S.bm[k][n]);
+                        k < 0 ? 0 : (part == 0 ? S.bh[k][n] : (part == 1 ? S.bl[k][n] : S.bm[k][n]));
                 }
     return JPGX_OK;
 }
@@ -486,7 +505,11 @@ static Bnd mx_row_bound(const MxSplit &S, int n)
         sl += 128.0L * (fabsl(S.l[k][n]) + fabsl(S.m[k][n]));
         rep += 128.0L * fabsl(mx_exact(k, n) - S.h[k][n] - S.l[k][n] - S.m[k][n]);
     }
-    const double el = (double)(70.0L * sl * 0x1p-23L + rep);
+    /* acc_l: 25 products per lo part over 2 k-steps; every addition (the MFMA's internal ones
+     * and the accumulation across instructions) charged one ulp of the magnitude bound, twice
+     * over for an unknown summation tree */
+    const double nadd = 2.0 * (25.0 * (JX_MX_PARTS - 1) + 2 * (JX_MX_PARTS - 1));
+    const double el = (double)(nadd * sl * 0x1p-23L + rep);
     return BoundOps::add(Bnd{(double)loh, (double)hih, 0.0},
                          Bnd{(double)lol - el, (double)hil + el, el});
 }
@@ -560,7 +583,7 @@ extern "C" long long jx_selftest_mx(long long nblocks, unsigned long long seed, 
                     const int sv = px[y][k] - 128;
                     ah += sv * S.h[k][n];
                     al = al + (float)(sv * S.l[k][n]);
-                    al = al + (float)(sv * S.m[k][n]);
+                    if (JX_MX_PARTS == 3) al = al + (float)(sv * S.m[k][n]);
                 }
                 R[y] = (float)ah + al;
             }

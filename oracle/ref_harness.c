@@ -65,6 +65,17 @@ int main(int argc, char **argv)
     if (getenv("REF_WATCH_PIXELS")) g_watch = (size_t)atol(getenv("REF_WATCH_PIXELS"));
 
     preprocess_jpeg(j);
+    if (getenv("REF_STOP_AFTER_PREPROCESS")) {
+        /* only the underflow bytes (recorded during preprocess_jpeg's r_new/g_new/b_new
+         * mallocs, preprocess.c:127-129): seconds instead of the DCT's minutes */
+        fprintf(stderr, "W=%d H=%d nb=%d\n", j->width, j->height, j->num_blocks_Y);
+        for (int i = 0; i < g_nseen; i++) {
+            fprintf(stderr, "pre[%d]=", i);
+            for (int k = 0; k < 8; k++) fprintf(stderr, "%02x", g_seen[i][k]);
+            fprintf(stderr, "\n");
+        }
+        return 0;
+    }
     chroma_subsample(j);
     dct(j);
     quantise(j);
