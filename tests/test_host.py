@@ -67,6 +67,20 @@ def test_underflow_survey_values():
     assert jpgx.glibc_underflow(16384 * 16384).hex() == "0210001000000000"
 
 
+def test_underflow_model_matches_real_mmap_bytes():
+    """The mmap case of the model against the bytes the REAL reference read in front of its
+    three planes (tests/golden/make_big_golden.py: the reference harness stopped after
+    preprocess_jpeg for 4096^2 and 8192^2, and the full 16384^2 run)."""
+    import json
+    with open(os.path.join(REPO, "tests", "golden", "big_golden.json")) as f:
+        g = json.load(f)
+    cases = {int(s) ** 2: v for s, v in g["mmap_underflow"].items()}
+    cases[16384 * 16384] = g["frame16k_q50_sr1"]["underflow"]
+    assert len(cases) == 3
+    for n, planes in cases.items():
+        assert [bytes(p) for p in planes] == [jpgx.glibc_underflow(n)] * 3, n
+
+
 def test_stripes_partition():
     for rows in (1, 7, 8, 135, 270, 2048):
         for n in (1, 2, 3, 4, 8):

@@ -7,7 +7,7 @@ cd "$ROOT"
 OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"
 export TMPDIR=/tmp
 STEPS=${STEPS:-20}
-timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=5 > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread --maxfail=5 > "$OUT/pytest_gpu.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -25 "$OUT/pytest_gpu.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?
