@@ -53,15 +53,15 @@ struct jx_limtab {
 
 /* k_mx (csrc/jpgx_mx.hip): the colour conversion + row DCT of each pixel row is one f16 MFMA
  * product with B split into JX_MX_PARTS f16 parts (hi exact, lo parts scaled by 2^12).  Per
- * quality, lane n = 8c + u of the MFMA result holds the scales and guard band of coefficients
- * (c, u, v = 0..7); columns 24..31 are MFMA padding (w 0, band never hit). */
+ * quality, plan column n = 8c + u holds the scales and guard band of coefficients (c, u,
+ * v = 0..7). */
 #ifndef JX_MX_PARTS
 #define JX_MX_PARTS 3
 #endif
 struct jx_mxtab {
-    float w[32][8];         /* 1/4 a(u) a(v) k(v) / Q[u][v] (row transform uses exact cosines) */
-    float lsq[32][8];       /* a float <= lim^2 of the rigorous band (flag: d*d - lsq >= 0);
-                               -1 with FORCE_EXACT, 3e38 for the padding columns              */
+    float w[24][8];         /* 1/4 a(u) a(v) k(v) / Q[u][v] (row transform uses exact cosines) */
+    float lsq[24][8];       /* a float <= lim^2 of the rigorous band (flag: d*d - lsq >= 0);
+                               -1 with FORCE_EXACT                                            */
     int16_t q[2][64];       /* scaled tables, q[t][u*8+v] = Qs[u][v] (src/quantise.c:58)       */
 };
 
@@ -99,7 +99,7 @@ void jx_under_dwords(const uint8_t under[3][8], uint32_t out[6]);
 long long jx_selftest_pk(long long nblocks, unsigned long long seed);
 /* k_mx: tables and f16 B operands (host plan), launch (device side) */
 int jx_plan_tables_mx(int quality, float w[24][8], float lim[24][8], int16_t q[2][64]);
-int jx_mx_operands(uint16_t ops[2 * JX_MX_PARTS][64][8]);
+int jx_mx_operands(uint16_t ops[3 * JX_MX_PARTS][64][8]);
 long long jx_selftest_mx(long long nblocks, unsigned long long seed, int quality,
                          long long *flagged, double *ratio);
 int jx_launch_mx(const struct jx_xform_args *xa, void *stream);

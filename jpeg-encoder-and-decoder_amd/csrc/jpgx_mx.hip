@@ -1,42 +1,36 @@
 /*
  * jpgx_mx.hip -- k_mx, the gfx950 block-transform kernel with the colour conversion and the
- * row DCT on the matrix cores (v_mfma_f32_32x32x16_f16), the column DCT, quantiser, guard
- * band and zig-zag in VALU, and the exact-order fp64 pass for guard-band coefficients inside
- * the same waves.
+ * row DCT on the matrix cores (v_mfma_f32_16x16x32_f16), the column DCT, quantiser, guard
+ * band and zig-zag in packed fp32 VALU (v_pk_*_f32), and the exact-order fp64 pass for
+ * guard-band coefficients inline, from the pixels already in LDS.
  *
  * Reference path: preprocess.c:160-162,186-188 (colour + level shift) -> dct.c:36-59 ->
  * quantise.c:52-72 (transposed divisor, round()) -> zig_zag.c:48-58; output = the three
  * JpgData.zig_zag_* arrays, [frame][Y|Cb|Cr][nb][64] int16.
  *
- * Work unit.  Each wave walks a contiguous range of "steps" of 8 consecutive blocks
- * (launch-global block index, frames concatenated); a step is two MFMA groups of 4 blocks.
- * Per group, lane l loads ONE 16-byte piece: pixel row y of block blk (the A-operand row
- * m = l & 31 of the group) at byte offset 8 hA, hA = l >> 5 (jpgx_plan.cpp: K layout), issued
- * a step ahead.  MFMA row m = 8i + 4hh + j <-> block blk = 2hh + (i >> 1)... precisely:
- *     i = (m & 3) + 4 (m >> 3),  blk = 2 ((m >> 2) & 1) + (i & 1),  y = i >> 1,
- * so that in the 32x32 result (column n = lane & 31 = 8c + u, rows (r & 3) + 8 (r >> 2) +
- * 4 (lane >> 5) in register r) lane half h holds all 8 pixel rows of blocks 2h, 2h + 1 as the
- * aligned register pairs (2y, 2y + 1):
- *     A[m][k]  = b_k - 128 (exact in f16; bytes -> f16 by v_perm + v_pk_add_f16),
- *                the bias slot A = 1.0 (k-step 1, lane half 0, element 0)
- *     R[m][n]  = (A Bh) + 2^-12 (A Bl [+ A Bm])    (acc_h exact: jpgx_plan.cpp)
- * = the colour-converted, level-shifted row transform of all three channels, 2 * JX_MX_PARTS
- * MFMAs per 4 blocks.  Each lane then runs the column DCT of its column for its two blocks in
- * lock-step (jx_fdct8 over v_pk_* pairs: lane by lane the FOps code the guard band is derived
- * for), quantises with the per-lane (c,u) scales (tm = F w + 1.5 2^23: the low 16 bits are the
- * rounded int16), writes each int16 to the wave's LDS stage at its zig-zag position, and folds
- * the guard-band test d^2 - lim^2 >= 0 (d = F w - rint, exact) into one running max.  After each
- * step, the 8 blocks x 3 channels x 128 B leave as three 1-KiB nontemporal stores.
- *
- * Exactness.  A group whose running max says "some coefficient inside the
- * band" (rare: wave-uniform branch) re-tests its coefficients, copies the flagged blocks'
- * pixel rows (already in registers) into an LDS slot and queues one task per flagged
- * coefficient.  A full queue, and the end of the wave's range, run the exact pass: eight tasks
- * at a time, eight lanes each -- lane x forms (X(x,y) c_u[x]) c_v[y] in fp64 for y = 0..7
- * with X in the reference's double colour arithmetic, the 64-term sum runs x-outer / y-inner
- * (dct.c:46-50) through lanes x = 0..7 in turn, then F = ((1/4 a(u)) a(v)) s and round(F / Q)
- * with the transposed divisor.  The exact value patches the LDS stage if its block belongs to
- * the step being built, else global memory (after the wave's earlier stores have landed).
+ * Work unit: a "step" of 8 consecutive blocks (launch-global block index, frames
+ * concatenated); each wave walks a contiguous range of steps.
+ *   Input   the step's 8 pixel rows x 8 blocks x 24 B land in a 1.5-KiB LDS slot ([y][24 jb + k])
+ *           by LDS-DMA (16-byte pieces), issued two steps ahead (3-slot ring).
+ *   Rows    set s (blocks 4s..4s+3), half h (pixel rows 4h..4h+3): a 16 x 32 f16 A operand,
+ *           row m = 4 jb + y, k = byte k of the pixel row (b - 128, exact in f16; k = 24 the
+ *           bias 1.0).  One product with B = colour x cosine gives, in C row m, column j, the
+ *           row transform of channel j/8 (Y, Cb), frequency u = j%8.  Cr: the two sets
+ *           concatenated along K (B zero outside its set's columns), so column j of the Cr tile
+ *           is set j/8's Cr at u = j%8.  B = Bh + 2^-12 (Bl + Bm), three f16 parts; acc_h =
+ *           A Bh is EXACT in any summation order (jpgx_plan.cpp); R = acc_h + 2^-12 acc_l.
+ *   Columns every lane then holds three whole columns (8 rows, registers 0..3 of the two
+ *           halves): (set 0, c = j/8, u), (set 1, same), (Cr, set j/8, u).  Each runs jx_fdct8_pk
+ *           (lane by lane the FOps code the band is derived for), the quantiser tm = F w +
+ *           1.5 2^23 (low 16 bits = the rounded int16) per v_pk_fma pair, the int16 to the LDS
+ *           stage at its zig-zag position, and the band test d^2 - lsq >= 0 (d = F w - rint,
+ *           exact) folded into a running max.
+ *   Exact   (rare) a column whose max says "some coefficient in the band" records its flagged
+ *           v's; after the step, eight flagged coefficients at a time, eight lanes each: lane x
+ *           forms (X(x,y) c_u[x]) c_v[y] in fp64 from the slot's pixel bytes, the sum runs
+ *           x-outer / y-inner (dct.c:46-50) lane to lane, F = ((1/4 a(u)) a(v)) s, round(F / Q)
+ *           patches the stage.
+ *   Output  channel c's 8 blocks x 128 B leave as one 1-KiB nontemporal store.
  */
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -57,61 +51,51 @@ namespace {
 
 typedef _Float16 mx_h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 mx_h2 __attribute__((ext_vector_type(2)));
-typedef float mx_f16 __attribute__((ext_vector_type(16)));
-typedef uint32_t mx_u4 __attribute__((ext_vector_type(4)));
+typedef float mx_f4 __attribute__((ext_vector_type(4)));
 typedef float mx_f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t mx_u4 __attribute__((ext_vector_type(4)));
+typedef uint32_t mx_u2 __attribute__((ext_vector_type(2)));
 
-constexpr float kMagic = 12582912.0f;   /* 1.5 * 2^23: x + kMagic rounds x to an integer   */
-constexpr int kParts = JX_MX_PARTS;
-constexpr int kSlots = 10;              /* LDS pixel slots (one block each) for exact tasks */
-constexpr int kRecs = 4;                /* flagged-group records per wave                   */
+constexpr float kMagic = 12582912.0f;   /* 1.5 * 2^23: x + kMagic rounds x to an integer     */
+constexpr unsigned kSlot = 1536;        /* one step's pixels: [y][8 blocks x 24 B]           */
+constexpr unsigned kRing = 3;
 #ifndef JX_MX_WPE
-#define JX_MX_WPE 4                     /* waves per SIMD the register allocation targets  */
+#define JX_MX_WPE 3                     /* waves per SIMD the register allocation targets    */
 #endif
 
-/* LDS stage: channel c at mx_stage_base(c), 8 blocks x 128 B each, blocks in step order,
- * zig-zag order inside a block.  The bases put the three channels' 16-bit zig-zag writes of one
- * instruction on different banks (bank = dword % 32: shifts 0, 4, 16 dwords; at most 3-way,
- * about 2-way on average over the 8 rows v) and keep every 16-byte store chunk aligned.  The
- * MFMA's padding columns 24..31 compute Y's columns again (jx_mx_operands), so those lanes
- * write the very values lanes 0..7 write to the same addresses: no dummy area, no exec mask. */
-__host__ __device__ constexpr unsigned mx_stage_base(unsigned c)
-{
-    return 1152u * c + 16u * (c + 2u * (c >> 1));
-}
-constexpr unsigned kStageBytes = mx_stage_base(2) + 1024;
+/* LDS stage: channel c's 8 blocks at mx_sb(c) + 144 jb, 128 B each in zig-zag order.  The
+ * 16-B block padding and the channel offsets keep the column writes at most 3-way (mean 2.3)
+ * on a bank and the 16-B store reads conflict-free (searched offline). */
+__host__ __device__ constexpr unsigned mx_sb(unsigned c) { return c == 0 ? 0u : (c == 1 ? 1216u : 2368u); }
+constexpr unsigned kBS = 144;
+constexpr unsigned kStageBytes = 2368 + 8 * kBS;
 
 struct MxLds {
+    uint8_t ring[kRing][kSlot];
     uint8_t stage[kStageBytes];
-    mx_u4 in[2][2][64];                 /* [step & 1][group][lane]: the A-operand pieces, landed
-                                           by LDS-DMA one step ahead                         */
-    uint8_t pix[kSlots][8][24];         /* exact tasks: the flagged blocks' 8 pixel rows    */
-    uint16_t rbits[kRecs][64];          /* flagged-group record: per lane, bit 2v + j = its
-                                           coefficient (u, v) of block 2h + j is in the band */
-    uint32_t rblk[kRecs];               /* the group's first launch-global block            */
-    uint8_t rslot[kRecs][4];            /* pixel slot of each of its 4 blocks               */
-    uint32_t tblk[8];                   /* one exact batch: launch-global block             */
-    uint16_t tcode[8];                  /*                  slot << 9 | c << 6 | v << 3 | u  */
+    uint16_t task[8];                   /* one exact batch: source lane << 8 | column << 3 | v */
 };
-static_assert(kStageBytes % 16 == 0, "LDS-DMA pieces must stay 16-byte aligned");
+static_assert(kSlot % 16 == 0 && kStageBytes % 16 == 0, "16-byte aligned LDS regions");
 
-__device__ mx_u4 g_mxB[2 * kParts][64];          /* B operands: (part, kstep) x lane      */
-__device__ jx_mxtab g_mxtab[2][JX_MAXQ + 1];     /* [force][quality]                      */
+#ifdef JX_MX_DBG_COUNT          /* measurement only: exact-pass calls and tasks per launch */
+__device__ unsigned long long g_mx_dbg[4];
+#endif
+__device__ mx_u4 g_mxB[3 * JX_MX_PARTS][64];     /* B operands: (part, which) x lane        */
+__device__ jx_mxtab g_mxtab[2][JX_MAXQ + 1];     /* [force][quality]                        */
 __constant__ double kMxCos[8][8] = JX_COS_INIT;
 __constant__ int kMxScan[8][8] = JX_SCAN_ORDER_INIT;
-constexpr double kMxAlpha0 = JX_ALPHA0;
+/* ((0.25 a(u)) a(v)) of dct.c:54, 0.25 a(u) exact in a double */
+__constant__ double kMxQuarterAlpha[8] = {0.25 * JX_ALPHA0, 0.25, 0.25, 0.25, 0.25, 0.25, 0.25, 0.25};
+__constant__ double kMxAlpha[8] = {JX_ALPHA0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0};
 /* per channel the reference's colour constants as the exact pass uses them: t = (k0 r + k1 g)
  * + k2 b (the signs of its subtractions folded into k1, k2: a - b*k == a + b*(-k) exactly),
  * then (A + S t) - 128 with (A, S) = (0, 1) Y, (128, -1) Cb, (128, 1) Cr */
-__constant__ double kMxQuarterAlpha[8] = {0.25 * JX_ALPHA0, 0.25, 0.25, 0.25, 0.25, 0.25, 0.25, 0.25};
-__constant__ double kMxAlpha[8] = {JX_ALPHA0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0};
 __constant__ double kMxColour[3][5] = {{0.299, 0.587, 0.114, 0.0, 1.0},
                                        {0.168736, -0.331264, 0.5, 128.0, -1.0},
                                        {0.5, -0.418688, -0.081312, 128.0, 1.0}};
 
-/* Order this wave's LDS accesses across lanes: a wave's LDS instructions execute in program
- * order, so only the compiler must be kept from moving memory operations across this point
- * (no fence: a wavefront-scope fence makes the compiler drain the vector memory counter). */
+/* Keep the compiler from moving this wave's LDS accesses across this point (a wave's LDS
+ * instructions execute in program order; no fence: that would drain the memory counters). */
 __device__ __forceinline__ void mx_wave_sync()
 {
     __builtin_amdgcn_wave_barrier();
@@ -124,9 +108,7 @@ __device__ __forceinline__ int mx_rank(uint64_t m)
                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-/* The lane id, recomputed where it is used by the rare paths: an opaque (volatile) value
- * cannot be hoisted, so the rare paths' lane-derived constants do not occupy registers
- * across the tile loop. */
+/* the lane id, opaque, for rare paths (lane-derived values are then not kept live) */
 __device__ __forceinline__ unsigned mx_lane()
 {
     unsigned l;
@@ -134,18 +116,40 @@ __device__ __forceinline__ unsigned mx_lane()
     return l;
 }
 
-/* four pixel bytes of dword d -> two f16 b - 128: perm makes 0x64bb (= 1024 + b) from each
- * byte (K = 0x64646481: byte 5 is 0x64, byte 4 is 0x81 = 129, which the bias selector of
- * lane half 0 picks to make 1153 - 1152 = 1.0), then one packed subtraction, exact. */
-__device__ __forceinline__ uint32_t mx_cvt2(uint32_t K, uint32_t d, uint32_t sel)
+/* Two pixel bytes -> two f16 (b - 128): perm makes 0x64bb (= 1024 + b) from each byte of d
+ * (K = 0x64806481 supplies 0x64, and for the bias lanes 0x81 / 0x80 = 1153 / 1152, i.e. 1.0 /
+ * 0.0 after the subtraction), then one packed subtraction, exact. */
+__device__ __forceinline__ uint32_t mx_cvt2(uint32_t d, uint32_t sel)
 {
-    const mx_h2 v = __builtin_bit_cast(mx_h2, __builtin_amdgcn_perm(K, d, sel)) -
+    const mx_h2 v = __builtin_bit_cast(mx_h2, __builtin_amdgcn_perm(0x64806481u, d, sel)) -
                     (mx_h2){(_Float16)1152.0f, (_Float16)1152.0f};
     return __builtin_bit_cast(uint32_t, v);
 }
 
-/* The launch geometry as plain values (references into the kernel-argument struct, or indexed
- * reads of its arrays, make the compiler copy it to scratch) */
+__device__ __forceinline__ mx_h8 mx_aop(mx_u2 d, uint32_t s0, uint32_t s1, uint32_t s2)
+{
+    const mx_u4 a = {mx_cvt2(d.x, s0), mx_cvt2(d.x, s1), mx_cvt2(d.y, s2), mx_cvt2(d.y, s1)};
+    return __builtin_bit_cast(mx_h8, a);
+}
+
+__device__ __forceinline__ mx_f4 mx_mma(mx_h8 a, mx_u4 b, mx_f4 c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, __builtin_bit_cast(mx_h8, b), c, 0, 0, 0);
+}
+
+/* v_pk_*_f32 pairs for jx_fdct8_pk (lane by lane the scalar FOps operations) */
+struct MxPair {
+    typedef mx_f2 V;
+    static __device__ __forceinline__ V mk(float a, float b) { return V{a, b}; }
+    static __device__ __forceinline__ float lo(V a) { return a.x; }
+    static __device__ __forceinline__ float hi(V a) { return a.y; }
+    static __device__ __forceinline__ V add(V a, V b) { return a + b; }
+    static __device__ __forceinline__ V sub(V a, V b) { return a - b; }
+    static __device__ __forceinline__ V mul(V a, V b) { return a * b; }
+    static __device__ __forceinline__ V fma(V a, V b, V c) { return __builtin_elementwise_fma(a, b, c); }
+};
+
+/* The launch geometry as plain values */
 struct MxG {
     const uint8_t *rgb;
     int16_t *out;
@@ -154,27 +158,6 @@ struct MxG {
     int row0, quality, force;
     uint32_t u[6];                      /* the underflow pixel row (jx_geom.under) */
 };
-
-typedef const mx_u4 __attribute__((address_space(1))) *mx_gp;   /* global (not flat) loads */
-
-/*
- * Address of the 16 bytes of pixel row y of block b (launch-global, clamped into range) at
- * offset 8 hA, with the reference's addressing: blockToCoords (preprocess.c:199-211) gives
- * x0 = -8 for the last block of a block-row, i.e. pixel row 8r+y-1, columns W-8..W-1; at frame
- * block-row 0, y = 0 those are the bytes in front of the planes (the underflow row): *under is
- * set and the address points at a readable row (the value is replaced at its use).
- */
-__device__ __forceinline__ const uint8_t *mx_addr_general(const MxG &g, unsigned b, unsigned y,
-                                                         unsigned hA, bool *under)
-{
-    b = b < g.total ? b : g.total - 1u;
-    const unsigned f = b / g.nb, bi = b - f * g.nb;
-    const unsigned r = bi / g.bpr, c = bi - r * g.bpr;
-    const bool last = c == g.bpr - 1u;
-    *under = last && y == 0 && g.row0 + (int)r == 0;
-    const long long pr = *under ? 0 : 8ll * r + y - (last ? 1 : 0);
-    return g.rgb + (long long)f * g.fstride + pr * g.pitch + 24ll * c + 8 * hA;
-}
 
 /* position of a step's first block: frame f, block bi in the frame, block-row r, column c */
 struct MxPos {
@@ -197,85 +180,94 @@ __device__ __forceinline__ void mx_advance(MxPos &p, const MxG &g)
     }
 }
 
-/* the step's 8 blocks lie in one block-row of one frame, none is the row's last block, and
- * all are in range: the fast (one-add) load and store addressing applies */
-__device__ __forceinline__ bool mx_simple(const MxPos &p, const MxG &g, unsigned b0)
+/* the step's 8 blocks lie in one block-row of one frame, none is the row's last block, all in
+ * range: lane-linear source addresses */
+__device__ __forceinline__ bool mx_simple_load(const MxPos &p, const MxG &g, unsigned b0)
 {
     return p.c + 8u < g.bpr && b0 + 8u <= g.total;
 }
-
-/* The two group loads of the step at position P (first block b0), by LDS-DMA into dst[q]
- * (lane l's 16 bytes land at dst[q][l]): one global_load_lds_dwordx4 per group on every path
- * (the general path only computes other addresses; bit q of the return value marks a lane
- * whose group-q piece is the underflow row, replaced at its use). */
-__device__ __forceinline__ uint32_t mx_issue(const MxG &g, const MxPos &P, unsigned b0,
-                                             bool simple, uint32_t laneoff, mx_u4 (*dst)[64])
+__device__ __forceinline__ bool mx_simple_store(const MxPos &p, const MxG &g, unsigned b0)
 {
-    const uint8_t *p[2];
-    uint32_t un = 0;
+    return p.bi + 8u <= g.nb && b0 + 8u <= g.total;
+}
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+/* LDS pointer as the DMA builtin wants it */
+typedef __attribute__((address_space(3))) void *mx_lp;
+typedef const __attribute__((address_space(1))) void *mx_gp;
+
+/*
+ * The pixels of the step starting at block b0 (position P) into `slot` ([y][24 jb + k]).
+ * Simple steps: two LDS-DMA instructions of 16-byte pieces (piece p = lane, and 64 + lane for
+ * lanes < 32: row p / 12, bytes 16 (p % 12); the LDS destination of an LDS-DMA is base + 16 lane
+ * for 12- and 16-byte pieces alike, so the slot is filled contiguously).  Other steps (a row's
+ * last block, row or frame crossings, the launch's last step): lane l loads pixel row y = l & 7
+ * of block jb = l >> 3 with the reference's addressing -- blockToCoords (preprocess.c:199-211)
+ * gives x0 = -8 for the last block of a block-row, i.e. pixel row 8r + y - 1, columns W-8..W-1,
+ * and at frame block-row 0, y = 0 those are the bytes in front of the planes (g.u) -- and
+ * writes it to the slot itself; it waits for every outstanding VMEM operation (rare), so the
+ * caller's vmcnt accounting, which counts two DMA operations per step, stays conservative.
+ */
+__device__ __forceinline__ void mx_issue(const MxG &g, const MxPos &P, unsigned b0, bool simple,
+                                         uint32_t off0, uint32_t off1, uint8_t *slot)
+{
     if (simple) {
-        const uint8_t *base = g.rgb + (long long)P.f * g.fstride + 8ll * P.r * g.pitch +
-                              24ll * P.c + laneoff;
-        p[0] = base;
-        p[1] = base + 96;
-    } else {
-        const unsigned lane = mx_lane(), m = lane & 31u, hA = lane >> 5;
-        const unsigned iA = (m & 3u) + 4u * (m >> 3);
-        const unsigned blkA = 2u * ((m >> 2) & 1u) + (iA & 1u), yA = iA >> 1;
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            bool uq;
-            p[q] = mx_addr_general(g, b0 + 4u * q + blkA, yA, hA, &uq);
-            un |= (uq ? 1u : 0u) << q;
-        }
+        const uint8_t *base = g.rgb + (long long)P.f * g.fstride + 8ll * P.r * g.pitch + 24ll * P.c;
+        __builtin_amdgcn_global_load_lds((mx_gp)(base + off0), (mx_lp)slot, 16, 0, 0);
+        if (mx_lane() < 32)
+            __builtin_amdgcn_global_load_lds((mx_gp)(base + off1), (mx_lp)(slot + 1024u), 16, 0, 0);
+        return;
     }
-#ifdef JX_MX_DBG_NOLOAD        /* timing experiments only: no pixel loads (pieces set once) */
-    if (un != 0xdeadbeefu) {
-        const unsigned l = mx_lane();
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const uint32_t h = (l * 2654435761u) ^ (q * 0x9e3779b9u) ^ b0;
-            dst[q][l] = mx_u4{h, h * 747796405u + 1u, h ^ 0x5bd1e995u, h * 3u + 7u};
-        }
-        return un;
+    const unsigned lane = mx_lane(), y = lane & 7u, jb = lane >> 3;
+    unsigned b = b0 + jb;
+    b = b < g.total ? b : g.total - 1u;
+    const unsigned f = b / g.nb, bi = b - f * g.nb;
+    const unsigned r = bi / g.bpr, c = bi - r * g.bpr;
+    const bool last = c == g.bpr - 1u;
+    const bool under = last && y == 0 && g.row0 + (int)r == 0;
+    const long long prow = under ? 8ll * r : 8ll * r + y - (last ? 1 : 0);
+    typedef const __attribute__((address_space(1))) mx_u2 gu2;
+    const gu2 *src = (const gu2 *)(g.rgb + (long long)f * g.fstride + prow * g.pitch + 24ll * c);
+    mx_u2 v0 = src[0], v1 = src[1], v2 = src[2];
+    if (under) {
+        v0 = mx_u2{g.u[0], g.u[1]};
+        v1 = mx_u2{g.u[2], g.u[3]};
+        v2 = mx_u2{g.u[4], g.u[5]};
     }
-#endif
-#pragma unroll
-    for (int q = 0; q < 2; q++)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)p[q],
-                                         (__attribute__((address_space(3))) void *)&dst[q][0],
-                                         16, 0, 0);
-    return un;
+    uint8_t *d = slot + 192u * y + 24u * jb;
+    *(mx_u2 *)d = v0;
+    *(mx_u2 *)(d + 8) = v1;
+    *(mx_u2 *)(d + 16) = v2;
+    __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0) (see above) */
 }
 
 /*
- * One exact batch of n <= 8 tasks (L.tblk / L.tcode), eight lanes each: lane x of task i forms
- * the products (X(x,y) c_u[x]) c_v[y], y = 0..7 (dct.c:48-50, X in the reference's double
- * colour arithmetic, preprocess.c:160-162,186-188), and the sum runs x-outer / y-inner
- * (dct.c:46-47) through lanes x = 0..7 in turn; F = ((1/4 a(u)) a(v)) s (dct.c:54) and
- * round(F / Q) with the transposed divisor (quantise.c:58).  Blocks >= step_b0 (the step whose
- * stage is being built) patch the stage; the others global memory (the caller has waited for
- * the wave's stores).
+ * One exact batch of nt <= 8 tasks (L.task), eight lanes each: lane x of task i forms the
+ * products (X(x,y) c_u[x]) c_v[y], y = 0..7 (dct.c:48-50, X in the reference's double colour
+ * arithmetic, preprocess.c:160-162,186-188), and the sum runs x-outer / y-inner (dct.c:46-47)
+ * through lanes x = 0..7 in turn; F = ((1/4 a(u)) a(v)) s (dct.c:54) and round(F / Q) with the
+ * transposed divisor (quantise.c:58) patches the stage.
  */
-__device__ __forceinline__ void mx_batch(MxLds &L, int nt, const MxG &g, unsigned step_b0)
+__device__ __forceinline__ void mx_batch(MxLds &L, const uint8_t *slot, int nt, const jx_mxtab &T)
 {
     const unsigned lane = mx_lane();
-    const jx_mxtab &T = g_mxtab[0][g.quality];
     const unsigned i = lane >> 3, x = lane & 7u;
     const bool live = (int)i < nt;
-    const unsigned blk = L.tblk[live ? i : 0u];
-    const unsigned code = L.tcode[live ? i : 0u];
-    const int slot = (int)(code >> 9), ch = (int)((code >> 6) & 7u), v = (int)((code >> 3) & 7u),
-              u = (int)(code & 7u);
+    const unsigned code = L.task[live ? i : 0u];
+    const unsigned sl = code >> 8, col = (code >> 3) & 3u, v = code & 7u;
+    const unsigned gg = sl >> 4, jj = sl & 15u, u = jj & 7u;
+    const unsigned ch = col < 2 ? (jj >> 3) : 2u;
+    const unsigned jb = col == 0 ? gg : (col == 1 ? 4u + gg : (jj < 8 ? gg : 4u + gg));
     const double cu = kMxCos[u][x];
     const double k0c = kMxColour[ch][0], k1c = kMxColour[ch][1], k2c = kMxColour[ch][2];
     const double Ac = kMxColour[ch][3], Sc = kMxColour[ch][4];
     double prod[8];
+    const lds_u8 *sl8 = (const lds_u8 *)slot;
 #pragma unroll
     for (int y = 0; y < 8; y++) {
-        const uint8_t *px = &L.pix[slot][y][3 * x];
-        const double rr = (double)px[0], gg = (double)px[1], bb = (double)px[2];
-        const double tt = (k0c * rr + k1c * gg) + k2c * bb;
+        const lds_u8 *px = sl8 + 192u * (unsigned)y + 24u * jb + 3u * x;
+        const double rr = (double)px[0], gv = (double)px[1], bv = (double)px[2];
+        const double tt = (k0c * rr + k1c * gv) + k2c * bv;
         const double X = (Ac + Sc * tt) - 128.0;
         prod[y] = X * cu * kMxCos[v][y];
     }
@@ -289,155 +281,104 @@ __device__ __forceinline__ void mx_batch(MxLds &L, int nt, const MxG &g, unsigne
         sum = __shfl(sum, (int)((lane & ~7u) | (unsigned)xx), 64);
     }
     if (live && x == 0) {
-        /* ((0.25 * a(u)) * a(v)) * s, dct.c:54 (0.25 * a(u) is exact in the table) */
         const double F = kMxQuarterAlpha[u] * kMxAlpha[v] * sum;
         const int q = T.q[ch == 0 ? 0 : 1][u * 8 + v];
         const int16_t val = (int16_t)(int)round(F / (double)q);
-        const int z = kMxScan[v][u];
-        if (blk >= step_b0) {
-            *(int16_t *)(L.stage + mx_stage_base((unsigned)ch) + (blk - step_b0) * 128u + 2u * z) = val;
-        } else {
-            const unsigned f = blk / g.nb, bi = blk - f * g.nb;
-            g.out[(long long)f * g.ofstride + ((long long)ch * g.nb + bi) * 64 + z] = val;
-        }
+        *(__attribute__((address_space(3))) int16_t *)((lds_u8 *)L.stage + mx_sb(ch) + kBS * jb +
+                                                       2u * (unsigned)kMxScan[v][u]) = val;
     }
-    mx_wave_sync();                                    /* batch buffer reused */
+    mx_wave_sync();                                    /* task buffer reused */
 }
 
-/* Exact pass over every recorded flagged group: tasks eight at a time (the records are
- * expanded lane by lane, lowest bit first). */
-__device__ __forceinline__ void mx_drain(MxLds &L, int nrec, const MxG &g, unsigned step_b0)
+/* Exact pass of one step: every flagged coefficient (bit 8 col + v of a lane's `bits`) */
+__device__ __forceinline__ void mx_exact(MxLds &L, const uint8_t *slot, uint32_t bits,
+                                      const jx_mxtab &T)
 {
     const unsigned lane = mx_lane();
-#ifdef JX_MX_EXPERIMENT_NODRAIN
-    return;
-#endif
-    const unsigned n = lane & 31u, h = lane >> 5, c = n >> 3, u = n & 7u;
-    __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0): the wave's stores landed */
     mx_wave_sync();
-    int nt = 0;
-    for (int r = 0; r < nrec; r++) {
-        uint32_t bits = L.rbits[r][lane];
-        const unsigned gb0 = L.rblk[r];
-        for (;;) {
-            const uint64_t act = __ballot(bits != 0);
-            if (!act) break;
-            const int room = 8 - nt, rk = mx_rank(act);
-            if (bits != 0 && rk < room) {
-                const int k = __builtin_ctz(bits);
-                bits &= bits - 1u;
-                const unsigned v = (unsigned)k >> 1, blk = 2u * h + ((unsigned)k & 1u);
-                L.tblk[nt + rk] = gb0 + blk;
-                L.tcode[nt + rk] = (uint16_t)((unsigned)L.rslot[r][blk] << 9 | c << 6 | v << 3 | u);
-            }
-            nt += std::min((int)__popcll(act), room);
-            mx_wave_sync();
-            if (nt == 8) {
-                mx_batch(L, 8, g, step_b0);
-                nt = 0;
-            }
+#ifdef JX_MX_DBG_COUNT
+    {
+        const unsigned ntask = __builtin_amdgcn_readfirstlane(0u) + 0u;
+        unsigned c = __popc(bits);
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if (lane == 0) {
+            atomicAdd(&g_mx_dbg[0], 1ull);
+            atomicAdd(&g_mx_dbg[1], (unsigned long long)c);
         }
+        (void)ntask;
     }
-    if (nt) mx_batch(L, nt, g, step_b0);
-    /* nothing of the exact pass stays in flight: the tile loop's wait accounting (and the
-     * compiler's, which would otherwise drain the counter at every reuse of these registers)
-     * starts clean */
-    __builtin_amdgcn_s_waitcnt(0xF70);
+#endif
+    for (;;) {
+        const uint64_t act = __ballot(bits != 0);
+        if (!act) break;
+#ifdef JX_MX_DBG_COUNT
+        if (lane == 0) atomicAdd(&g_mx_dbg[2], 1ull);
+#endif
+        const int rk = mx_rank(act);
+        if (bits != 0 && rk < 8) {
+            const unsigned b = (unsigned)__builtin_ctz(bits);
+            bits &= bits - 1u;
+            L.task[rk] = (uint16_t)(lane << 8 | (b >> 3) << 3 | (b & 7u));
+        }
+        mx_wave_sync();
+        mx_batch(L, slot, std::min((int)__popcll(act), 8), T);
+    }
 }
 
-/*
- * Rare path of one group (some lane's running max says a coefficient is inside the band):
- * re-test every coefficient (the fast path's arithmetic exactly) and record the flagged ones
- * with the flagged blocks' pixel rows (already in registers) copied to LDS slots; the caller
- * guarantees room for one record and four slots.
- */
-__device__ __forceinline__ void mx_record(MxLds &L, int &nrec, int &nslot, const mx_f2 (&F)[8],
-                                          const float (&w)[8], const float (&lsq)[8], mx_u4 ld,
-                                          unsigned gb0)
+/* Column pass of one column (8 rows as 4 register pairs), quantiser, stage writes, band max */
+__device__ __forceinline__ void mx_column(const mx_f2 (&R)[4], const mx_f2 (&W)[4], const mx_f2 (&Lq)[4],
+                                          uint8_t *st, const uint32_t (&zo)[8], float &emax,
+                                          mx_f2 (&F)[4])
 {
-    const unsigned lane = mx_lane();
-    const unsigned n = lane & 31u;
-    const unsigned m = lane & 31u, hA = lane >> 5;
-    const unsigned iA = (m & 3u) + 4u * (m >> 3);
-    const unsigned blkA = 2u * ((m >> 2) & 1u) + (iA & 1u), yA = iA >> 1;
-    uint32_t bits = 0;
+    jx_fdct8_pk<MxPair>(R, F);
+    const mx_f2 M2 = {kMagic, kMagic};
 #pragma unroll
-    for (int v = 7; v >= 0; v--) {
-        const float t0 = __builtin_fmaf(F[v].x, w[v], kMagic);
-        const float t1 = __builtin_fmaf(F[v].y, w[v], kMagic);
-        const float d0 = __builtin_fmaf(F[v].x, w[v], -(t0 - kMagic));
-        const float d1 = __builtin_fmaf(F[v].y, w[v], -(t1 - kMagic));
-        const float e0 = __builtin_fmaf(d0, d0, -lsq[v]);
-        const float e1 = __builtin_fmaf(d1, d1, -lsq[v]);
-        bits = (bits << 2) | (e1 >= 0.0f ? 2u : 0u) | (e0 >= 0.0f ? 1u : 0u);
+    for (int p = 0; p < 4; p++) {
+        const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
+        *(uint16_t *)(st + zo[jx_pk_k(p, 0)]) = (uint16_t)__float_as_uint(tm.x);
+        *(uint16_t *)(st + zo[jx_pk_k(p, 1)]) = (uint16_t)__float_as_uint(tm.y);
+        const mx_f2 rr = tm - M2;
+        const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
+        const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
+        emax = __builtin_fmaxf(emax, __builtin_fmaxf(e.x, e.y));
     }
-    if (n >= 24) bits = 0;
-    /* flagged blocks of the group: bit (2h + j) */
-    const uint64_t m0 = __ballot((bits & 0x5555u) != 0), m1 = __ballot((bits & 0xaaaau) != 0);
-    const unsigned blkmask = ((uint32_t)m0 ? 1u : 0u) | ((uint32_t)m1 ? 2u : 0u) |
-                             ((m0 >> 32) ? 4u : 0u) | ((m1 >> 32) ? 8u : 0u);
-    if (!blkmask) return;
-    const int r = nrec;
-    L.rbits[r][lane] = (uint16_t)bits;
-    if (lane == 0) L.rblk[r] = gb0;
-    if (lane < 4) {
-        const bool fl = (blkmask >> lane) & 1u;
-        L.rslot[r][lane] = fl ? (uint8_t)(nslot + __builtin_popcount(blkmask & ((1u << lane) - 1u))) : 0;
-    }
-    if ((blkmask >> blkA) & 1u) {
-        const int sl = nslot + __builtin_popcount(blkmask & ((1u << blkA) - 1u));
-        uint8_t *row = &L.pix[sl][yA][8 * hA];
-        *(uint32_t *)(row + 0) = ld.x;
-        *(uint32_t *)(row + 4) = ld.y;
-        *(uint32_t *)(row + 8) = ld.z;
-        *(uint32_t *)(row + 12) = ld.w;
-    }
-    nrec++;
-    nslot += __builtin_popcount(blkmask);
 }
 
-/* Colour conversion + row DCT of one group of 4 blocks through the matrix cores: R[y] =
- * (block 2h, block 2h + 1) at pixel row y for this lane's column n. */
-__device__ __forceinline__ void mx_rows(mx_u4 ld, uint32_t K, uint32_t selb, const mx_h8 (&B)[2 * kParts],
-                                        mx_f2 (&R)[8])
+/* rare: the flagged v's of one column (the same arithmetic as mx_column) */
+__device__ __forceinline__ uint32_t mx_flags(const mx_f2 (&F)[4], const mx_f2 (&W)[4], const mx_f2 (&Lq)[4])
 {
-    const uint32_t s0 = 0x05010500u, s1 = 0x05030502u;
-    const mx_u4 a0 = {mx_cvt2(K, ld.x, s0), mx_cvt2(K, ld.x, s1), mx_cvt2(K, ld.y, s0),
-                      mx_cvt2(K, ld.y, s1)};
-    const mx_u4 a1 = {mx_cvt2(K, ld.z, selb), mx_cvt2(K, ld.z, s1), mx_cvt2(K, ld.w, s0),
-                      mx_cvt2(K, ld.w, s1)};
-    const mx_h8 A0 = __builtin_bit_cast(mx_h8, a0), A1 = __builtin_bit_cast(mx_h8, a1);
-    const mx_f16 zero = {};
-    mx_f16 ah = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B[0], zero, 0, 0, 0);
-    mx_f16 al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B[2], zero, 0, 0, 0);
-    ah = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B[1], ah, 0, 0, 0);
-    al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B[3], al, 0, 0, 0);
-    if (kParts == 3) {
-        al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B[4 % (2 * kParts)], al, 0, 0, 0);
-        al = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B[5 % (2 * kParts)], al, 0, 0, 0);
-    }
+    const mx_f2 M2 = {kMagic, kMagic};
+    uint32_t m = 0;
 #pragma unroll
-    for (int y = 0; y < 8; y++)
-        R[y] = __builtin_elementwise_fma(mx_f2{al[2 * y], al[2 * y + 1]},
-                                         mx_f2{0x1p-12f, 0x1p-12f},
-                                         mx_f2{ah[2 * y], ah[2 * y + 1]});
+    for (int p = 0; p < 4; p++) {
+        const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
+        const mx_f2 rr = tm - M2;
+        const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
+        const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
+        m |= (e.x >= 0.0f ? 1u : 0u) << jx_pk_k(p, 0);
+        m |= (e.y >= 0.0f ? 1u : 0u) << jx_pk_k(p, 1);
+    }
+    return m;
 }
 
-/* v_pk_*_f32 pairs: two blocks' columns in lock-step, lane by lane the FOps sequence */
-struct MxPair {
-    typedef mx_f2 V;
-    static __device__ __forceinline__ V mk(float a, float b) { return V{a, b}; }
-    static __device__ __forceinline__ float lo(V a) { return a.x; }
-    static __device__ __forceinline__ float hi(V a) { return a.y; }
-    static __device__ __forceinline__ V add(V a, V b) { return a + b; }
-    static __device__ __forceinline__ V sub(V a, V b) { return a - b; }
-    static __device__ __forceinline__ V mul(V a, V b) { return a * b; }
-    static __device__ __forceinline__ V fma(V a, V b, V c) { return __builtin_elementwise_fma(a, b, c); }
-};
+/* R pairs (y, y+1) of one column from the lo (rows 0..3) and hi (rows 4..7) tiles */
+__device__ __forceinline__ void mx_combine(mx_f4 hl, mx_f4 ll, mx_f4 hh, mx_f4 lh, mx_f2 (&R)[4])
+{
+#ifdef JX_MX_DBG_NOPS          /* experiment: extra wait states between the MFMAs and their reads */
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7");
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    const mx_f2 s = {0x1p-12f, 0x1p-12f};
+    R[0] = __builtin_elementwise_fma(mx_f2{ll.x, ll.y}, s, mx_f2{hl.x, hl.y});
+    R[1] = __builtin_elementwise_fma(mx_f2{ll.z, ll.w}, s, mx_f2{hl.z, hl.w});
+    R[2] = __builtin_elementwise_fma(mx_f2{lh.x, lh.y}, s, mx_f2{hh.x, hh.y});
+    R[3] = __builtin_elementwise_fma(mx_f2{lh.z, lh.w}, s, mx_f2{hh.z, hh.w});
+}
 
 __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
 {
-    __shared__ MxLds s_lds[4];
+    __shared__ __attribute__((aligned(16))) MxLds s_lds[4];
     MxG g;
     g.rgb = a.g.rgb;
     g.out = a.g.out;
@@ -455,7 +396,6 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
 
     const unsigned lane = threadIdx.x & 63u;
     MxLds &L = s_lds[threadIdx.x >> 6];
-    /* each wave walks a contiguous range of steps */
     const unsigned nsteps = (g.total + 7u) / 8u;
     const unsigned nw = gridDim.x * 4u;
     const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -463,31 +403,41 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     unsigned s = (unsigned)(((unsigned long long)nsteps * wv) / nw);
     if (s >= s_end) return;
 
-    /* A-operand row of this lane (both groups): block blkA of the group, pixel row yA */
-    const unsigned hA = lane >> 5, m = lane & 31u;
-    const unsigned iA = (m & 3u) + 4u * (m >> 3);
-    const unsigned blkA = 2u * ((m >> 2) & 1u) + (iA & 1u), yA = iA >> 1;
-    const uint32_t laneoff = (uint32_t)(yA * (unsigned)g.pitch + 24u * blkA + 8u * hA);
-    const uint32_t K = 0x64646481u;
-    const uint32_t selb = hA ? 0x05010500u : 0x05010504u;
+    /* A operand of this lane: row m = lane & 15 (block m >> 2 of the set, pixel row m & 3 of the
+     * half), k-group q = lane >> 4 (bytes 8q..8q+7; q = 3: the bias) */
+    const unsigned m = lane & 15u, q = lane >> 4;
+    const uint32_t aoff = 192u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 0u);
+    const uint32_t s0 = q < 3 ? 0x05010500u : 0x07060504u;
+    const uint32_t s1 = q < 3 ? 0x05030502u : 0x07060706u;
+    const uint32_t s2 = q < 3 ? 0x05010500u : 0x07060706u;
+    /* DMA pieces p = lane, 64 + lane: pixel row p / 12, bytes 16 (p % 12) of the step's row */
+    const uint32_t off0 = (uint32_t)((lane / 12u) * (unsigned)g.pitch + 16u * (lane % 12u));
+    const uint32_t off1 = (uint32_t)(((64u + lane) / 12u) * (unsigned)g.pitch + 16u * ((64u + lane) % 12u));
 
-    /* output column n = 8c + u of this lane; C-layout lane half h = blocks 2h, 2h + 1 */
-    const unsigned n = lane & 31u, h = lane >> 5;
-    const unsigned cz = (n >> 3) % 3u, uz = n & 7u;     /* padding columns 24..31 = Y again */
+    /* C layout: lane (gq = lane >> 4, j = lane & 15) holds column j of rows 4 gq..4 gq + 3 */
+    const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
     const jx_mxtab &T = g_mxtab[g.force ? 1 : 0][g.quality];
-    float w[8], lsq[8];
+    const unsigned ny = j, nc = 16u + u;                /* plan columns n = 8c + u */
+    mx_f2 Wy[4], Ly[4], Wc[4], Lc[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const int v0 = jx_pk_k(p, 0), v1 = jx_pk_k(p, 1);
+        Wy[p] = mx_f2{T.w[ny][v0], T.w[ny][v1]};
+        Ly[p] = mx_f2{T.lsq[ny][v0], T.lsq[ny][v1]};
+        Wc[p] = mx_f2{T.w[nc][v0], T.w[nc][v1]};
+        Lc[p] = mx_f2{T.lsq[nc][v0], T.lsq[nc][v1]};
+    }
     uint32_t zo[8];
 #pragma unroll
-    for (int v = 0; v < 8; v++) {
-        w[v] = T.w[n][v];
-        lsq[v] = T.lsq[n][v];
-        zo[v] = mx_stage_base(cz) + 256u * h + 2u * (unsigned)kMxScan[v][uz];
-    }
-    mx_h8 B[2 * kParts];
+    for (int v = 0; v < 8; v++) zo[v] = 2u * (unsigned)kMxScan[v][u];
+    uint8_t *const st1 = L.stage + mx_sb(j >> 3) + kBS * gq;           /* set 0: block gq       */
+    uint8_t *const st3 = L.stage + mx_sb(2) + kBS * (j < 8 ? gq : 4u + gq);
+    mx_u4 B[3][3];
 #pragma unroll
-    for (int i = 0; i < 2 * kParts; i++) B[i] = __builtin_bit_cast(mx_h8, g_mxB[i][lane]);
+    for (int p = 0; p < 3; p++)
+#pragma unroll
+        for (int w = 0; w < 3; w++) B[p][w] = g_mxB[3 * p + w][lane];
 
-    int nrec = 0, nslot = 0;               /* flagged-group records, pixel slots in use */
     MxPos P;
     {
         const unsigned b0 = 8u * s;
@@ -496,114 +446,133 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         P.r = P.bi / g.bpr;
         P.c = P.bi - P.r * g.bpr;
     }
-    /* the loads of the wave's first step; every later step issues the next step's loads
-     * right after waiting for its own (vmcnt counts loads, LDS-DMA and stores in issue order:
-     * younger than this step's DMA are only the previous step's three stores) */
-    uint32_t un = mx_issue(g, P, 8u * s, mx_simple(P, g, 8u * s), laneoff, L.in[s & 1u]);
-    __builtin_amdgcn_s_waitcnt(0xF70);           /* vmcnt(0): tables, operands, first step */
-    bool first = true;
-    for (; s < s_end; s++) {
+    /* prologue: the first two steps' DMA (ring slots 0, 1) */
+    MxPos PN = P;                                  /* position of the next step to issue */
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const unsigned sn = s + (unsigned)k;
+        if (sn < s_end) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[k]);
+        mx_advance(PN, g);
+    }
+    unsigned slot = 0, it = 0;
+    for (; s < s_end; s++, it++) {
         const unsigned b0 = 8u * s;
-        const MxPos PC = P;
-        if (!first) __builtin_amdgcn_s_waitcnt(0xF73);   /* vmcnt(3) */
-        first = false;
-        mx_wave_sync();
-        const uint32_t uc = un;
-        mx_advance(P, g);
-        if (s + 1u < s_end)
-            un = mx_issue(g, P, b0 + 8u, mx_simple(P, g, b0 + 8u), laneoff, L.in[(s + 1u) & 1u]);
-        const bool underrow = !mx_simple(PC, g, b0) && __ballot(uc != 0) != 0;
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            mx_u4 ld = L.in[s & 1u][q][lane];
-            if (underrow && ((uc >> q) & 1u))       /* rare: the underflow row */
-                ld = hA ? mx_u4{g.u[2], g.u[3], g.u[4], g.u[5]} : mx_u4{g.u[0], g.u[1], g.u[2], g.u[3]};
-            mx_f2 R[8], F[8];
-#if defined(JX_MX_DBG_NOCOMPUTE)  /* timing experiments only: the stage writes, no transform */
-#pragma unroll
-            for (int v = 0; v < 8; v++) {
-                *(uint16_t *)(L.stage + zo[v] + 512u * q) = (uint16_t)(ld[v & 3] >> (v & 16));
-                *(uint16_t *)(L.stage + zo[v] + 512u * q + 128u) = (uint16_t)(ld[(v + 1) & 3]);
-            }
-            if (ld.x == 0xdeadbeefu)
-#endif
-            {
-#ifdef JX_MX_DBG_NOMFMA          /* timing experiments only: R by VALU from the bytes */
-#pragma unroll
-            for (int y = 0; y < 8; y++)
-                R[y] = mx_f2{(float)((ld[y & 3] >> (8 * (y >> 2))) & 0xffu) - 128.0f,
-                             (float)((ld[(y + 1) & 3] >> 8) & 0xffu) - 128.0f} * 7.0f;
+        /* this step's DMA: younger VMEM operations are the next step's 2 pieces and the last
+         * two steps' 3 stores each (vmcnt counts loads, LDS-DMA and stores in issue order) */
+        {
+            /* VMEM operations younger than this step's DMA (in issue order): step s-2's three
+             * stores, step s+1's two DMA pieces, step s-1's three stores */
+#ifdef JX_MX_DBG_VMCNT0         /* measurement only: drain every VMEM operation per step */
+            const unsigned young = 0;
 #else
-            mx_rows(ld, K, selb, B, R);
+            const unsigned young = (it >= 2 ? 3u : 0u) + (s + 1u < s_end ? 2u : 0u) + (it >= 1 ? 3u : 0u);
 #endif
-            jx_fdct8<PairOps<MxPair>>(R, F);
+            switch (young) {
+            case 8: __builtin_amdgcn_s_waitcnt(0xF78); break;
+            case 6: __builtin_amdgcn_s_waitcnt(0xF76); break;
+            case 5: __builtin_amdgcn_s_waitcnt(0xF75); break;
+            case 3: __builtin_amdgcn_s_waitcnt(0xF73); break;
+            case 2: __builtin_amdgcn_s_waitcnt(0xF72); break;
+            default: __builtin_amdgcn_s_waitcnt(0xF70); break;
             }
-            float emax = -1.0f;
-#if defined(JX_MX_DBG_NOCOMPUTE)
-            if (ld.x == 0xdeadbeefu)
-#endif
-#pragma unroll
-            for (int v = 0; v < 8; v++) {
-                /* quant_coef: tm = F w + 1.5 2^23 (low 16 bits = the rounded int16), d = F w -
-                 * rint (exact); band test d*d - lsq >= 0 folded into a running max */
-                const float t0 = __builtin_fmaf(F[v].x, w[v], kMagic);
-                const float t1 = __builtin_fmaf(F[v].y, w[v], kMagic);
-#ifndef JX_MX_DBG_NOSTAGE        /* timing experiments only: no zig-zag LDS writes */
-                *(uint16_t *)(L.stage + zo[v] + 512u * q) = (uint16_t)__float_as_uint(t0);
-                *(uint16_t *)(L.stage + zo[v] + 512u * q + 128u) = (uint16_t)__float_as_uint(t1);
-#else
-                emax += __uint_as_float(__float_as_uint(t0) ^ __float_as_uint(t1)) * 1e-30f;
-#endif
-                const float d0 = __builtin_fmaf(F[v].x, w[v], -(t0 - kMagic));
-                const float d1 = __builtin_fmaf(F[v].y, w[v], -(t1 - kMagic));
-                const float e0 = __builtin_fmaf(d0, d0, -lsq[v]);
-                const float e1 = __builtin_fmaf(d1, d1, -lsq[v]);
-                emax = __builtin_fmaxf(emax, __builtin_fmaxf(e0, e1));
-            }
-#ifdef JX_MX_DBG_NORARE           /* timing experiments only: no exact pass */
-            if (emax == 12345.0f)
-#else
-            if (__ballot(emax >= 0.0f))              /* rare: some coefficient in the band */
-#endif
-                mx_record(L, nrec, nslot, F, w, lsq, ld, b0 + 4u * q);
-            __builtin_amdgcn_sched_barrier(0);
         }
         mx_wave_sync();
-        /* exact pass when the next step might not find room (rarely before the wave's end) */
-        if (nrec > kRecs - 2 || nslot > kSlots - 8) {
-            mx_drain(L, nrec, g, b0);
-            nrec = 0;
-            nslot = 0;
+        uint8_t *const sp = L.ring[slot];
+        /* the step after next: its DMA into the slot step s-1 used */
+        {
+            const unsigned sn = s + 2u, nslot = slot == 0 ? 2u : slot - 1u;
+            if (sn < s_end) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[nslot]);
+            mx_advance(PN, g);
         }
-        /* stores: channel c's 8 blocks x 128 B are contiguous, 16 B per lane; always three
-         * store instructions (the vmcnt(3) above counts on it) */
-#ifdef JX_MX_DBG_NOSTORE        /* timing experiments only: no coefficient stores */
-        if (b0 == 0xdeadbeefu)
+        /* A operands: set 0/1 x half lo/hi */
+        const mx_u2 d00 = *(const mx_u2 *)(sp + aoff);
+        const mx_u2 d01 = *(const mx_u2 *)(sp + aoff + 768u);
+        const mx_u2 d10 = *(const mx_u2 *)(sp + aoff + 96u);
+        const mx_u2 d11 = *(const mx_u2 *)(sp + aoff + 864u);
+        const mx_h8 A00 = mx_aop(d00, s0, s1, s2), A01 = mx_aop(d01, s0, s1, s2);
+        const mx_h8 A10 = mx_aop(d10, s0, s1, s2), A11 = mx_aop(d11, s0, s1, s2);
+        const mx_f4 z = {};
+        uint32_t fl = 0;                               /* bit 8 col + v: flagged (rare) */
+        float em = -1.0f;
+        mx_f2 R[4], F[4];
+        /* MFMAs one column ahead of the VALU work: MFMA(c0), MFMA(c1), VALU(c0), MFMA(c2),
+         * VALU(c1), VALU(c2) -- an accumulator is read only after another column's products or
+         * VALU work (no exposed MFMA latency, and far more than the MFMA -> VALU wait states the
+         * hardware needs), with two columns' accumulators live at a time */
+        mx_f4 acc[3][4];                               /* [column][hl, ll, hh, lh] */
+        const auto mma_set = [&](mx_f4(&o)[4], const mx_h8 &Alo, const mx_h8 &Ahi) {
+            o[0] = mx_mma(Alo, B[0][0], z);
+            o[2] = mx_mma(Ahi, B[0][0], z);
+            o[1] = mx_mma(Alo, B[1][0], z);
+            o[3] = mx_mma(Ahi, B[1][0], z);
+            o[1] = mx_mma(Alo, B[2][0], o[1]);
+            o[3] = mx_mma(Ahi, B[2][0], o[3]);
+        };
+        const auto column = [&](int k) {
+            mx_combine(acc[k][0], acc[k][1], acc[k][2], acc[k][3], R);
+            float e = -1.0f;
+            const mx_f2(&W)[4] = k < 2 ? Wy : Wc;
+            const mx_f2(&Lq)[4] = k < 2 ? Ly : Lc;
+            mx_column(R, W, Lq, k == 0 ? st1 : (k == 1 ? st1 + 4u * kBS : st3), zo, e, F);
+            if (__builtin_expect(__ballot(e >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * k);
+            em = __builtin_fmaxf(em, e);
+        };
+        mma_set(acc[0], A00, A01);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_set(acc[1], A10, A11);
+        __builtin_amdgcn_sched_barrier(0);
+        column(0);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[2][0] = mx_mma(A00, B[0][1], z);
+        acc[2][2] = mx_mma(A01, B[0][1], z);
+        acc[2][1] = mx_mma(A00, B[1][1], z);
+        acc[2][3] = mx_mma(A01, B[1][1], z);
+        acc[2][0] = mx_mma(A10, B[0][2], acc[2][0]);
+        acc[2][2] = mx_mma(A11, B[0][2], acc[2][2]);
+        acc[2][1] = mx_mma(A10, B[1][2], acc[2][1]);
+        acc[2][3] = mx_mma(A11, B[1][2], acc[2][3]);
+        acc[2][1] = mx_mma(A00, B[2][1], acc[2][1]);
+        acc[2][3] = mx_mma(A01, B[2][1], acc[2][3]);
+        acc[2][1] = mx_mma(A10, B[2][2], acc[2][1]);
+        acc[2][3] = mx_mma(A11, B[2][2], acc[2][3]);
+        __builtin_amdgcn_sched_barrier(0);
+        column(1);
+        __builtin_amdgcn_sched_barrier(0);
+        column(2);
+        (void)em;
+        mx_wave_sync();
+#ifndef JX_MX_DBG_NOEXACT        /* measurement only: no exact pass (NOT bit-exact) */
+        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx_exact(L, sp, fl, T);
 #endif
-        if (mx_simple(PC, g, b0)) {
-            int16_t *ob = g.out + (long long)PC.f * g.ofstride + (long long)PC.bi * 64 + lane * 8;
+        /* stores: channel c's 8 blocks x 128 B; always three store instructions (the vmcnt
+         * accounting above counts on it) */
+        if (mx_simple_store(P, g, b0)) {
+            int16_t *ob = g.out + (long long)P.f * g.ofstride + (long long)P.bi * 64 + lane * 8;
+            const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
 #pragma unroll
             for (int c = 0; c < 3; c++) {
-                const mx_u4 val = *(const mx_u4 *)(L.stage + mx_stage_base(c) + lane * 16);
+                const mx_u4 val = *(const mx_u4 *)(L.stage + mx_sb((unsigned)c) + ro);
                 __builtin_nontemporal_store(val, (mx_u4 *)(ob + (long long)c * g.nb * 64));
             }
         } else {
-            /* lanes past the end rewrite the last block's chunk with its own bytes */
-            const unsigned lane = mx_lane();
-            const unsigned bl = b0 + (lane >> 3), b = bl < g.total ? bl : g.total - 1u;
+            /* lanes past the end rewrite the last block's chunk with its own bytes (the clamped
+             * blocks computed the last block) */
+            const unsigned l = mx_lane();
+            const unsigned bl = b0 + (l >> 3), b = bl < g.total ? bl : g.total - 1u;
             const unsigned f = b / g.nb, bi = b - f * g.nb;
-            const unsigned src = bl < g.total ? lane : ((g.total - 1u - b0) << 3) | (lane & 7u);
+            const uint32_t ro = (l >> 3) * kBS + (l & 7u) * 16u;
 #pragma unroll
             for (int c = 0; c < 3; c++) {
-                const mx_u4 val = *(const mx_u4 *)(L.stage + mx_stage_base(c) + src * 16);
+                const mx_u4 val = *(const mx_u4 *)(L.stage + mx_sb((unsigned)c) + ro);
                 __builtin_nontemporal_store(
                     val, (mx_u4 *)(g.out + (long long)f * g.ofstride +
-                                   ((long long)c * g.nb + bi) * 64 + (lane & 7u) * 8));
+                                   ((long long)c * g.nb + bi) * 64 + (l & 7u) * 8));
             }
         }
         mx_wave_sync();
+        mx_advance(P, g);
+        slot = slot == 2 ? 0u : slot + 1u;
     }
-    if (nrec) mx_drain(L, nrec, g, 0xffffffffu);
 }
 
 int mx_rc(hipError_t e) { return e == hipSuccess ? JPGX_OK : JPGX_EHIP; }
@@ -638,14 +607,14 @@ int mx_tables_for_current_device(int *waves)
             for (int f = 0; f < 2; f++) {
                 jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
                 memcpy(t.q, qq, sizeof qq);
-                for (int n = 0; n < 32; n++)        /* columns 24..31 repeat Y's 0..7 */
+                for (int n = 0; n < 24; n++)
                     for (int v = 0; v < 8; v++) {
-                        t.w[n][v] = w[n % 24][v];
-                        t.lsq[n][v] = f ? -1.0f : mx_lsq(lim[n % 24][v]);
+                        t.w[n][v] = w[n][v];
+                        t.lsq[n][v] = f ? -1.0f : mx_lsq(lim[n][v]);
                     }
             }
         }
-        uint16_t ops[2 * kParts][64][8];
+        static uint16_t ops[3 * JX_MX_PARTS][64][8];
         if (!rc) rc = jx_mx_operands(ops);
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxtab), tab.data(),
                                               tab.size() * sizeof(jx_mxtab)));
@@ -664,6 +633,18 @@ int mx_tables_for_current_device(int *waves)
 }
 
 }  // namespace
+
+#ifdef JX_MX_DBG_COUNT
+/* measurement only: {exact passes, tasks, batches} since the last call (then reset) */
+extern "C" int jx_mx_dbg_read(unsigned long long out[4])
+{
+    hipDeviceSynchronize();
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mx_dbg), 4 * sizeof(unsigned long long)) != hipSuccess)
+        return JPGX_EHIP;
+    unsigned long long z[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_mx_dbg), z, sizeof z) == hipSuccess ? JPGX_OK : JPGX_EHIP;
+}
+#endif
 
 /* k_mx over every frame of the stripe (4:4:4 / reference-parity output); no workspace. */
 extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)

@@ -374,11 +374,11 @@ extern "C" {
  * one ulp.  R = fl(acc_h + 2^-12 acc_l) (one fma) then enters the column pass (jx_fdct8,
  * FOps, two blocks per v_pk_* pair) as usual.
  *
- * K layout of the two 32x32x16 k-steps (lane half hA = lane >> 5 holds k = 8 hA + j, j < 8):
- * each lane loads 16 pixel-row bytes at offset 8 hA, so
- *   k-step 0:  hA = 0: bytes 0..7      hA = 1: bytes 8..15
- *   k-step 1:  hA = 0: j = 0 the bias (A = 1.0), j > 0 weight 0 (A = bytes 9..15, ignored)
- *              hA = 1: bytes 16..23
+ * Operand layout (v_mfma_f32_16x16x32_f16: lane l holds A[row l & 15][k = 8 (l >> 4) + e] and
+ * B[k = 8 (l >> 4) + e][column l & 15], e = 0..7): k < 24 is byte k of the pixel row, k = 24
+ * the bias (A = 1.0), k > 24 weight 0.  Three B matrices ("which"): 0 = columns j = 8c + u for
+ * c = Y, Cb; 1 = Cr at u = j for j < 8, zero columns j >= 8; 2 = zero columns j < 8, Cr at
+ * u = j - 8 for j >= 8 (k_mx sums A_set0 B1 + A_set1 B2: the two sets concatenated along K).
  */
 static const double kMxA[3][3] = {{0.299, 0.587, 0.114},
                                   {-0.168736, 0.331264, -0.5},
@@ -462,29 +462,25 @@ static int mx_split(MxSplit &S)
     return JPGX_OK;
 }
 
-/* source row of B for k-step ks, lane half hA, element j (the K layout above); -1: weight 0 */
-static int mx_src(int ks, int hA, int j)
-{
-    if (ks == 0) return 8 * hA + j;
-    if (hA == 0) return j == 0 ? 24 : -1;
-    return 16 + j;
-}
-
-extern "C" int jx_mx_operands(uint16_t ops[2 * JX_MX_PARTS][64][8])
+extern "C" int jx_mx_operands(uint16_t ops[3 * JX_MX_PARTS][64][8])
 {
     static MxSplit S;
     const int rc = mx_split(S);
     if (rc) return rc;
-    /* operand i = 2 * part + kstep; lane l holds B[mx_src(kstep, l >> 5, j)][l & 31]; the
-     * MFMA's padding columns 24..31 repeat Y's columns 0..7 (k_mx: those lanes write the same
-     * values to the same stage addresses as lanes 0..7 instead of needing a dummy area) */
+    /* operand 3 * part + which; lane l holds B[k = 8 (l >> 4) + e][plan column of l & 15] */
     for (int part = 0; part < JX_MX_PARTS; part++)
-        for (int ks = 0; ks < 2; ks++)
+        for (int which = 0; which < 3; which++)
             for (int l = 0; l < 64; l++)
-                for (int j = 0; j < 8; j++) {
-                    const int k = mx_src(ks, l >> 5, j), n = (l & 31) % 24;
-                    ops[2 * part + ks][l][j] =
-                        k < 0 ? 0 : (part == 0 ? S.bh[k][n] : (part == 1 ? S.bl[k][n] : S.bm[k][n]));
+                for (int e = 0; e < 8; e++) {
+                    const int k = 8 * (l >> 4) + e, j = l & 15;
+                    int n = -1;
+                    if (which == 0) n = j;
+                    else if (which == 1 && j < 8) n = 16 + j;
+                    else if (which == 2 && j >= 8) n = 16 + j - 8;
+                    uint16_t v = 0;
+                    if (n >= 0 && k <= 24)
+                        v = part == 0 ? S.bh[k][n] : (part == 1 ? S.bl[k][n] : S.bm[k][n]);
+                    ops[3 * part + which][l][e] = v;
                 }
     return JPGX_OK;
 }
@@ -505,10 +501,11 @@ static Bnd mx_row_bound(const MxSplit &S, int n)
         sl += 128.0L * (fabsl(S.l[k][n]) + fabsl(S.m[k][n]));
         rep += 128.0L * fabsl(mx_exact(k, n) - S.h[k][n] - S.l[k][n] - S.m[k][n]);
     }
-    /* acc_l: 25 products per lo part over 2 k-steps; every addition (the MFMA's internal ones
-     * and the accumulation across instructions) charged one ulp of the magnitude bound, twice
-     * over for an unknown summation tree */
-    const double nadd = 2.0 * (25.0 * (JX_MX_PARTS - 1) + 2 * (JX_MX_PARTS - 1));
+    /* acc_l: per lo part one MFMA of 32 products (K = 32: 25 weights, 7 zeros; the Cr tile's
+     * second, K-concatenated MFMA adds exact zeros in every column) plus the accumulator input;
+     * every addition charged one ulp of the magnitude bound, twice over for an unknown
+     * summation tree and rounding mode */
+    const double nadd = 2.0 * (33.0 * (JX_MX_PARTS - 1));
     const double el = (double)(nadd * sl * 0x1p-23L + rep);
     return BoundOps::add(Bnd{(double)loh, (double)hih, 0.0},
                          Bnd{(double)lol - el, (double)hil + el, el});

@@ -145,48 +145,35 @@ def test_mx_guard_band_holds_on_emulated_arithmetic(q):
 
 
 def test_mx_operands_make_the_hi_product_exact():
-    """k_mx's B operands (jpgx_plan.cpp jx_mx_operands, K layout: k-step 0 = bytes 8hA..8hA+7
-    of lane half hA, k-step 1 = the bias slot (hA 0, j 0) and bytes 16..23 (hA 1)): the hi part
-    is a multiple of 2^-11 whose products with b - 128 sum below 2^13 in every column (so the
-    MFMA's hi accumulation is exact in fp32 whatever its internal order), hi + lo [+ lo2]
-    reconstruct the colour x cosine matrix (and the level-shift bias) to the split's precision
-    (the lo parts are stored scaled by 2^12), every other K slot is 0, and the MFMA padding
-    columns 24..31 repeat Y's columns 0..7."""
+    """k_mx's B operands (jpgx_plan.cpp jx_mx_operands; v_mfma_f32_16x16x32_f16 layout: lane l
+    holds B[k = 8 (l >> 4) + e][column l & 15]; k < 24 the pixel-row bytes, k = 24 the bias,
+    k > 24 zero; operand 3 part + which, which 0 = Y | Cb columns, 1 = Cr in columns 0..7, 2 = Cr
+    in columns 8..15, the other half zero): the hi part is a multiple of 2^-11 whose products
+    with b - 128 sum below 2^13 in every column (so the MFMA's hi accumulation is exact in fp32
+    whatever its internal order), and hi + lo + lo2 reconstruct the colour x cosine matrix and
+    the level-shift bias (the lo parts are stored scaled by 2^12)."""
     import ctypes
     import math
-    parts_n = int(os.environ.get("JX_MX_PARTS_TEST", "3"))
-    ops = np.zeros((2 * parts_n, 64, 8), np.uint16)
+    parts_n = 3
+    ops = np.zeros((3 * parts_n, 64, 8), np.uint16)
     f = jpgx.lib.jx_mx_operands
     f.restype = ctypes.c_int
     assert f(ops.ctypes.data_as(ctypes.c_void_p)) == 0
-    vals = ops.view(np.float16).astype(np.float64)            # [part*2 + kstep][lane][j]
-
-    def src(ks, hA, j):
-        if ks == 0:
-            return 8 * hA + j
-        if hA == 0:
-            return 24 if j == 0 else -1
-        return 16 + j
-
-    B = np.zeros((parts_n, 25, 32))
-    for part in range(parts_n):
-        for ks in range(2):
-            for lane in range(64):
-                for j in range(8):
-                    k = src(ks, lane >> 5, j)
-                    v = vals[2 * part + ks, lane, j]
-                    if k < 0:
-                        assert v == 0
-                    elif ks == 0 and (lane >> 5) == 1 and j < 8 and k < 16:
-                        B[part, k, lane & 31] = v
-                    else:
-                        B[part, k, lane & 31] = v
-    assert np.array_equal(B[:, :, 24:], B[:, :, :8])          # padding columns = Y
-    hi = B[0]
-    lo = sum(B[p] for p in range(1, parts_n)) * 2.0 ** -12      # lo parts stored x 2^12
+    vals = ops.view(np.float16).astype(np.float64)            # [3 part + which][lane][e]
+    B = np.zeros((parts_n, 3, 32, 16))                        # [part][which][k][column]
+    for lane in range(64):
+        for e in range(8):
+            B[:, :, 8 * (lane >> 4) + e, lane & 15] = vals.reshape(parts_n, 3, 64, 8)[:, :, lane, e]
+    assert not np.any(B[:, :, 25:, :])                          # K padding weighs 0
+    assert not np.any(B[:, 1, :, 8:]) and not np.any(B[:, 2, :, :8])
+    assert np.array_equal(B[:, 1, :, :8], B[:, 2, :, 8:])      # Cr of either set
+    # plan columns n = 8c + u: Y|Cb from which 0, Cr from which 1
+    M = np.concatenate([B[:, 0], B[:, 1, :, :8]], axis=2)      # [part][k][24]
+    hi = M[0]
+    lo = (M[1] + M[2]) * 2.0 ** -12                            # lo parts stored x 2^12
     assert np.all(hi * 2048 == np.round(hi * 2048))
-    assert np.all(128 * np.abs(hi[:24, :24]).sum(axis=0) + np.abs(hi[24, :24]) < 8192)
-    tol = 2 ** -30 if parts_n == 3 else 2 ** -23
+    assert np.all(128 * np.abs(hi[:24]).sum(axis=0) + np.abs(hi[24]) < 8192)
+    tol = 2 ** -30
     a = [(0.299, 0.587, 0.114), (-0.168736, 0.331264, -0.5), (0.5, -0.418688, -0.081312)]
     for c in range(3):
         for u in range(8):
