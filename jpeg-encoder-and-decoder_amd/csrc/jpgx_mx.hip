@@ -70,10 +70,15 @@ __host__ __device__ constexpr unsigned mx_sb(unsigned c) { return c == 0 ? 0u : 
 constexpr unsigned kBS = 144;
 constexpr unsigned kStageBytes = 2368 + 8 * kBS;
 
+constexpr int kSide = 8;                /* deferred exact tasks (and their blocks) per wave  */
 struct MxLds {
     uint8_t ring[kRing][kSlot];
     uint8_t stage[kStageBytes];
-    uint16_t task[8];                   /* one exact batch: source lane << 8 | column << 3 | v */
+    uint8_t pix[kSide][192];            /* deferred blocks' pixel rows, [y][24]              */
+    uint32_t sblk[kSide];               /* and their launch-global block indices             */
+    uint16_t dtask[kSide];              /* deferred tasks: slot << 8 | c << 6 | v << 3 | u   */
+    uint16_t task[8];                   /* inline batch: source lane << 8 | column << 3 | v  */
+    uint32_t dummy[64];                 /* landing area of padding DMA operations            */
 };
 static_assert(kSlot % 16 == 0 && kStageBytes % 16 == 0, "16-byte aligned LDS regions");
 
@@ -159,34 +164,44 @@ struct MxG {
     uint32_t u[6];                      /* the underflow pixel row (jx_geom.under) */
 };
 
-/* position of a step's first block: frame f, block bi in the frame, block-row r, column c */
-struct MxPos {
+/* A step's position: frame f, block bi in the frame, block-row r, column c, and running
+ * pointers to its pixel (8c, 8r) and to its first block's channel-0 output. */
+struct MxCur {
     unsigned f, bi, r, c;
+    const uint8_t *src;
+    int16_t *dst;
 };
 
-__device__ __forceinline__ void mx_advance(MxPos &p, const MxG &g)
+__device__ __forceinline__ void mx_seek(MxCur &P, const MxG &g, unsigned b0)
 {
-    p.bi += 8u;
-    p.c += 8u;
-    while (p.c >= g.bpr) {
-        p.c -= g.bpr;
-        p.r++;
-    }
-    while (p.bi >= g.nb) {          /* next frame (frames smaller than a step: several) */
-        p.bi -= g.nb;
-        p.f++;
-        p.r = p.bi / g.bpr;
-        p.c = p.bi - p.r * g.bpr;
+    P.f = b0 / g.nb;
+    P.bi = b0 - P.f * g.nb;
+    P.r = P.bi / g.bpr;
+    P.c = P.bi - P.r * g.bpr;
+    P.src = g.rgb + (long long)P.f * g.fstride + 8ll * P.r * g.pitch + 24ll * P.c;
+    P.dst = g.out + (long long)P.f * g.ofstride + 64ll * P.bi;
+}
+
+/* to the next step (first block b0 + 8): pointer bumps inside a block-row, a seek otherwise */
+__device__ __forceinline__ void mx_next(MxCur &P, const MxG &g, unsigned b0)
+{
+    if (__builtin_expect(P.c + 8u < g.bpr && P.bi + 8u < g.nb, 1)) {
+        P.c += 8u;
+        P.bi += 8u;
+        P.src += 192;
+        P.dst += 512;
+    } else {
+        mx_seek(P, g, b0 + 8u);
     }
 }
 
 /* the step's 8 blocks lie in one block-row of one frame, none is the row's last block, all in
  * range: lane-linear source addresses */
-__device__ __forceinline__ bool mx_simple_load(const MxPos &p, const MxG &g, unsigned b0)
+__device__ __forceinline__ bool mx_simple_load(const MxCur &p, const MxG &g, unsigned b0)
 {
     return p.c + 8u < g.bpr && b0 + 8u <= g.total;
 }
-__device__ __forceinline__ bool mx_simple_store(const MxPos &p, const MxG &g, unsigned b0)
+__device__ __forceinline__ bool mx_simple_store(const MxCur &p, const MxG &g, unsigned b0)
 {
     return p.bi + 8u <= g.nb && b0 + 8u <= g.total;
 }
@@ -208,11 +223,11 @@ typedef const __attribute__((address_space(1))) void *mx_gp;
  * writes it to the slot itself; it waits for every outstanding VMEM operation (rare), so the
  * caller's vmcnt accounting, which counts two DMA operations per step, stays conservative.
  */
-__device__ __forceinline__ void mx_issue(const MxG &g, const MxPos &P, unsigned b0, bool simple,
+__device__ __forceinline__ void mx_issue(const MxG &g, const MxCur &P, unsigned b0, bool simple,
                                          uint32_t off0, uint32_t off1, uint8_t *slot)
 {
     if (simple) {
-        const uint8_t *base = g.rgb + (long long)P.f * g.fstride + 8ll * P.r * g.pitch + 24ll * P.c;
+        const uint8_t *base = P.src;
         __builtin_amdgcn_global_load_lds((mx_gp)(base + off0), (mx_lp)slot, 16, 0, 0);
         if (mx_lane() < 32)
             __builtin_amdgcn_global_load_lds((mx_gp)(base + off1), (mx_lp)(slot + 1024u), 16, 0, 0);
@@ -241,32 +256,43 @@ __device__ __forceinline__ void mx_issue(const MxG &g, const MxPos &P, unsigned 
     __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0) (see above) */
 }
 
-/*
- * One exact batch of nt <= 8 tasks (L.task), eight lanes each: lane x of task i forms the
- * products (X(x,y) c_u[x]) c_v[y], y = 0..7 (dct.c:48-50, X in the reference's double colour
- * arithmetic, preprocess.c:160-162,186-188), and the sum runs x-outer / y-inner (dct.c:46-47)
- * through lanes x = 0..7 in turn; F = ((1/4 a(u)) a(v)) s (dct.c:54) and round(F / Q) with the
- * transposed divisor (quantise.c:58) patches the stage.
- */
-__device__ __forceinline__ void mx_batch(MxLds &L, const uint8_t *slot, int nt, const jx_mxtab &T)
+/* s of lane x - 1 (DPP row shift by one; lane 0 of a 16-lane row gets 0) */
+__device__ __forceinline__ double mx_shr1(double s)
 {
-    const unsigned lane = mx_lane();
-    const unsigned i = lane >> 3, x = lane & 7u;
-    const bool live = (int)i < nt;
-    const unsigned code = L.task[live ? i : 0u];
-    const unsigned sl = code >> 8, col = (code >> 3) & 3u, v = code & 7u;
-    const unsigned gg = sl >> 4, jj = sl & 15u, u = jj & 7u;
-    const unsigned ch = col < 2 ? (jj >> 3) : 2u;
-    const unsigned jb = col == 0 ? gg : (col == 1 ? 4u + gg : (jj < 8 ? gg : 4u + gg));
+    const uint64_t b = __builtin_bit_cast(uint64_t, s);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x111, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x111, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+}
+
+/* n padding VMEM operations (4-byte LDS-DMA of the input's first bytes into L.dummy): they keep
+ * the number of VMEM operations per step constant, so that one vmcnt(8) always waits for exactly
+ * the step's own DMA */
+__device__ __forceinline__ void mx_pad(const MxG &g, MxLds &L, int n)
+{
+    for (int i = 0; i < n; i++)
+        __builtin_amdgcn_global_load_lds((mx_gp)g.rgb, (mx_lp)L.dummy, 4, 0, 0);
+}
+
+/*
+ * One exact coefficient per 8-lane group (lane = 8 i + x), in the reference's operation order:
+ * lane x forms X(x,y) in double colour arithmetic (preprocess.c:160-162,186-188) and the
+ * products (X c_u[x]) c_v[y] (dct.c:48-50); the 64-term sum runs x-outer / y-inner
+ * (dct.c:46-47) lane to lane; F = ((1/4 a(u)) a(v)) s (dct.c:54) and round(F / Q) with the
+ * transposed divisor (quantise.c:58).  px = the block's pixel row 0, rows rs bytes apart.  The
+ * result is valid in lane x == 7.
+ */
+__device__ __forceinline__ int mx_exact_coef(const lds_u8 *px, unsigned rs, unsigned ch, unsigned u,
+                                             unsigned v, unsigned x, const jx_mxtab &T)
+{
     const double cu = kMxCos[u][x];
     const double k0c = kMxColour[ch][0], k1c = kMxColour[ch][1], k2c = kMxColour[ch][2];
     const double Ac = kMxColour[ch][3], Sc = kMxColour[ch][4];
     double prod[8];
-    const lds_u8 *sl8 = (const lds_u8 *)slot;
 #pragma unroll
     for (int y = 0; y < 8; y++) {
-        const lds_u8 *px = sl8 + 192u * (unsigned)y + 24u * jb + 3u * x;
-        const double rr = (double)px[0], gv = (double)px[1], bv = (double)px[2];
+        const lds_u8 *p = px + rs * (unsigned)y + 3u * x;
+        const double rr = (double)p[0], gv = (double)p[1], bv = (double)p[2];
         const double tt = (k0c * rr + k1c * gv) + k2c * bv;
         const double X = (Ac + Sc * tt) - 128.0;
         prod[y] = X * cu * kMxCos[v][y];
@@ -278,51 +304,150 @@ __device__ __forceinline__ void mx_batch(MxLds &L, const uint8_t *slot, int nt, 
 #pragma unroll
             for (int y = 0; y < 8; y++) sum += prod[y];
         }
-        sum = __shfl(sum, (int)((lane & ~7u) | (unsigned)xx), 64);
+        if (xx < 7) sum = mx_shr1(sum);
     }
-    if (live && x == 0) {
-        const double F = kMxQuarterAlpha[u] * kMxAlpha[v] * sum;
-        const int q = T.q[ch == 0 ? 0 : 1][u * 8 + v];
-        const int16_t val = (int16_t)(int)round(F / (double)q);
-        *(__attribute__((address_space(3))) int16_t *)((lds_u8 *)L.stage + mx_sb(ch) + kBS * jb +
-                                                       2u * (unsigned)kMxScan[v][u]) = val;
-    }
-    mx_wave_sync();                                    /* task buffer reused */
+    const double F = kMxQuarterAlpha[u] * kMxAlpha[v] * sum;
+    const int q = T.q[ch == 0 ? 0 : 1][u * 8 + v];
+    return (int)round(F / (double)q);
 }
 
-/* Exact pass of one step: every flagged coefficient (bit 8 col + v of a lane's `bits`) */
-__device__ __forceinline__ void mx_exact(MxLds &L, const uint8_t *slot, uint32_t bits,
-                                      const jx_mxtab &T)
+__device__ __forceinline__ lds_u8 *mx_lds(void *p) { return (lds_u8 *)p; }
+
+/* the step's block jb and channel of a lane's column k (k_mx column layout) */
+__device__ __forceinline__ unsigned mx_col_block(unsigned k, unsigned sl)
+{
+    const unsigned gg = sl >> 4, jj = sl & 15u;
+    return k == 0 ? gg : (k == 1 ? 4u + gg : (jj < 8 ? gg : 4u + gg));
+}
+
+/* Inline exact pass of one step (a step with more tasks than the deferred queue holds, e.g.
+ * FLAG_FORCE_EXACT): every flagged coefficient (bit 8 col + v of a lane's `bits`), eight at a
+ * time, patching the stage. */
+__device__ __forceinline__ void mx_exact_inline(MxLds &L, const uint8_t *slot, uint32_t bits,
+                                                const jx_mxtab &T)
 {
     const unsigned lane = mx_lane();
     mx_wave_sync();
 #ifdef JX_MX_DBG_COUNT
-    {
-        const unsigned ntask = __builtin_amdgcn_readfirstlane(0u) + 0u;
-        unsigned c = __popc(bits);
-        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-        if (lane == 0) {
-            atomicAdd(&g_mx_dbg[0], 1ull);
-            atomicAdd(&g_mx_dbg[1], (unsigned long long)c);
-        }
-        (void)ntask;
-    }
+    if (lane == 0) atomicAdd(&g_mx_dbg[2], 1ull);
 #endif
     for (;;) {
         const uint64_t act = __ballot(bits != 0);
         if (!act) break;
-#ifdef JX_MX_DBG_COUNT
-        if (lane == 0) atomicAdd(&g_mx_dbg[2], 1ull);
-#endif
         const int rk = mx_rank(act);
         if (bits != 0 && rk < 8) {
             const unsigned b = (unsigned)__builtin_ctz(bits);
             bits &= bits - 1u;
-            L.task[rk] = (uint16_t)(lane << 8 | (b >> 3) << 3 | (b & 7u));
+            L.task[rk] = (uint16_t)(lane << 8 | b);
         }
         mx_wave_sync();
-        mx_batch(L, slot, std::min((int)__popcll(act), 8), T);
+        const int nt = std::min((int)__popcll(act), 8);
+        const unsigned i = lane >> 3, x = lane & 7u;
+        const bool live = (int)i < nt;
+        const unsigned code = L.task[live ? i : 0u];
+        const unsigned sl = code >> 8, k = (code >> 3) & 3u, v = code & 7u;
+        const unsigned jj = sl & 15u, u = jj & 7u, ch = k < 2 ? (jj >> 3) : 2u;
+        const unsigned jb = mx_col_block(k, sl);
+        const int val = mx_exact_coef(mx_lds((void *)slot) + 24u * jb, 192u, ch, u, v, x, T);
+        if (live && x == 7)
+            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + mx_sb(ch) + kBS * jb +
+                                                           2u * (unsigned)kMxScan[v][u]) = (int16_t)val;
+        mx_wave_sync();
     }
+}
+
+/* Deferred exact pass: the queued tasks (pixels in L.pix), results straight to global memory
+ * once the wave's earlier stores have landed. */
+__device__ __forceinline__ void mx_flush(MxLds &L, int &nq, int &ns, const MxG &g, const jx_mxtab &T)
+{
+    __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0): the tasks' blocks are stored */
+    mx_wave_sync();
+    const unsigned lane = mx_lane(), i = lane >> 3, x = lane & 7u;
+#ifdef JX_MX_DBG_COUNT
+    if (lane == 0) {
+        atomicAdd(&g_mx_dbg[0], 1ull);
+        atomicAdd(&g_mx_dbg[1], (unsigned long long)nq);
+    }
+#endif
+    const bool live = (int)i < nq;
+    const unsigned code = L.dtask[live ? i : 0u];
+    const unsigned slot = code >> 8, ch = (code >> 6) & 3u, v = (code >> 3) & 7u, u = code & 7u;
+    const int val = mx_exact_coef(mx_lds(L.pix[slot]), 24u, ch, u, v, x, T);
+    if (live && x == 7) {
+        const unsigned b = L.sblk[slot], f = b / g.nb, bi = b - f * g.nb;
+        g.out[(long long)f * g.ofstride + ((long long)ch * g.nb + bi) * 64 + kMxScan[v][u]] = (int16_t)val;
+    }
+    mx_wave_sync();
+    nq = 0;
+    ns = 0;
+}
+
+/* A step with flagged coefficients (bit 8 col + v of `bits`): queue them with their blocks'
+ * pixels (flushing the queue first if it would overflow); a step with more tasks than the queue
+ * holds is done inline. */
+__device__ __forceinline__ void mx_defer(MxLds &L, const uint8_t *sp, uint32_t bits, unsigned b0,
+                                         int &nq, int &ns, const MxG &g, const jx_mxtab &T)
+{
+    const unsigned lane = mx_lane();
+    /* flagged blocks of the step, and the task count */
+    const uint64_t m0 = __ballot((bits & 0xffu) != 0), m1 = __ballot((bits & 0xff00u) != 0),
+                   m2 = __ballot((bits & 0xff0000u) != 0);
+    uint32_t blk = 0;
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) {
+        blk |= (((m0 >> (16 * gq)) & 0xffffu) ? 1u : 0u) << gq;
+        blk |= (((m1 >> (16 * gq)) & 0xffffu) ? 1u : 0u) << (4 + gq);
+        blk |= (((m2 >> (16 * gq)) & 0xffu) ? 1u : 0u) << gq;
+        blk |= (((m2 >> (16 * gq + 8)) & 0xffu) ? 1u : 0u) << (4 + gq);
+    }
+    const unsigned cnt = (unsigned)__popc(bits);
+    unsigned incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned o = __shfl_up(incl, d, 64);
+        if ((int)lane >= d) incl += o;
+    }
+    const int ntask = (int)__builtin_amdgcn_readlane(incl, 63);
+    const int nblk = __popc(blk);
+    if (nq + ntask > kSide || ns + nblk > kSide) {
+        if (nq) mx_flush(L, nq, ns, g, T);
+        if (ntask > kSide) {
+            mx_exact_inline(L, sp, bits, T);
+            return;
+        }
+    }
+    /* copy the flagged blocks' pixel rows to side slots ns.. (lane: row l / 6, dword l % 6) */
+    {
+        uint32_t bm = blk;
+        int t = ns;
+        while (bm) {
+            const unsigned jb = (unsigned)__builtin_ctz(bm);
+            bm &= bm - 1u;
+            if (lane < 48) {
+                const unsigned y = lane / 6u, k = lane - 6u * y;
+                *(__attribute__((address_space(3))) uint32_t *)(mx_lds(L.pix[t]) + 24u * y + 4u * k) =
+                    *(const __attribute__((address_space(3))) uint32_t *)(mx_lds((void *)sp) + 192u * y + 24u * jb + 4u * k);
+            }
+            if (lane == 0) L.sblk[t] = b0 + jb;
+            t++;
+        }
+    }
+    /* this lane's tasks at queue positions nq + (exclusive prefix) */
+    {
+        unsigned pos = (unsigned)nq + incl - cnt;
+        const unsigned jj = lane & 15u, u = jj & 7u;
+        while (bits) {
+            const unsigned b = (unsigned)__builtin_ctz(bits);
+            bits &= bits - 1u;
+            const unsigned k = b >> 3, v = b & 7u, ch = k < 2 ? (jj >> 3) : 2u;
+            const unsigned jb = mx_col_block(k, lane);
+            const unsigned slot = (unsigned)ns + (unsigned)__popc(blk & ((1u << jb) - 1u));
+            L.dtask[pos++] = (uint16_t)(slot << 8 | ch << 6 | v << 3 | u);
+        }
+    }
+    mx_wave_sync();
+    nq += ntask;
+    ns += nblk;
 }
 
 /* Column pass of one column (8 rows as 4 register pairs), quantiser, stage writes, band max */
@@ -340,7 +465,7 @@ __device__ __forceinline__ void mx_column(const mx_f2 (&R)[4], const mx_f2 (&W)[
         const mx_f2 rr = tm - M2;
         const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
         const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
-        emax = __builtin_fmaxf(emax, __builtin_fmaxf(e.x, e.y));
+        emax = __builtin_fmaxf(__builtin_fmaxf(emax, e.x), e.y);          /* v_max3_f32 */
     }
 }
 
@@ -438,51 +563,38 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
 #pragma unroll
         for (int w = 0; w < 3; w++) B[p][w] = g_mxB[3 * p + w][lane];
 
-    MxPos P;
-    {
-        const unsigned b0 = 8u * s;
-        P.f = b0 / g.nb;
-        P.bi = b0 - P.f * g.nb;
-        P.r = P.bi / g.bpr;
-        P.c = P.bi - P.r * g.bpr;
-    }
-    /* prologue: the first two steps' DMA (ring slots 0, 1) */
-    MxPos PN = P;                                  /* position of the next step to issue */
+    MxCur P;
+    mx_seek(P, g, 8u * s);
+    /* prologue: the first two steps' DMA (ring slots 0, 1), each followed by three padding
+     * operations in place of the stores of the (absent) steps s-2 and s-1 */
+    MxCur PN = P;                                  /* position of the next step to issue */
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         const unsigned sn = s + (unsigned)k;
         if (sn < s_end) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[k]);
-        mx_advance(PN, g);
+        else mx_pad(g, L, 2);
+        mx_pad(g, L, 3);
+        mx_next(PN, g, 8u * sn);
     }
-    unsigned slot = 0, it = 0;
-    for (; s < s_end; s++, it++) {
+    unsigned slot = 0;
+    int nq = 0, ns = 0;                            /* deferred exact tasks, their blocks */
+    for (; s < s_end; s++) {
         const unsigned b0 = 8u * s;
         /* this step's DMA: younger VMEM operations are the next step's 2 pieces and the last
          * two steps' 3 stores each (vmcnt counts loads, LDS-DMA and stores in issue order) */
-        {
-            /* VMEM operations younger than this step's DMA (in issue order): step s-2's three
-             * stores, step s+1's two DMA pieces, step s-1's three stores */
-#ifdef JX_MX_DBG_VMCNT0         /* measurement only: drain every VMEM operation per step */
-            const unsigned young = 0;
-#else
-            const unsigned young = (it >= 2 ? 3u : 0u) + (s + 1u < s_end ? 2u : 0u) + (it >= 1 ? 3u : 0u);
-#endif
-            switch (young) {
-            case 8: __builtin_amdgcn_s_waitcnt(0xF78); break;
-            case 6: __builtin_amdgcn_s_waitcnt(0xF76); break;
-            case 5: __builtin_amdgcn_s_waitcnt(0xF75); break;
-            case 3: __builtin_amdgcn_s_waitcnt(0xF73); break;
-            case 2: __builtin_amdgcn_s_waitcnt(0xF72); break;
-            default: __builtin_amdgcn_s_waitcnt(0xF70); break;
-            }
-        }
+        /* VMEM operations younger than this step's DMA, in issue order: step s-2's three stores,
+         * step s+1's two DMA pieces, step s-1's three stores (padding operations stand in for
+         * the ones that do not exist; a general step's loads and the exact flush wait for
+         * themselves, which only makes this count conservative) */
+        __builtin_amdgcn_s_waitcnt(0xF78);             /* vmcnt(8) */
         mx_wave_sync();
         uint8_t *const sp = L.ring[slot];
         /* the step after next: its DMA into the slot step s-1 used */
         {
             const unsigned sn = s + 2u, nslot = slot == 0 ? 2u : slot - 1u;
             if (sn < s_end) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[nslot]);
-            mx_advance(PN, g);
+            else mx_pad(g, L, 2);
+            mx_next(PN, g, 8u * sn);
         }
         /* A operands: set 0/1 x half lo/hi */
         const mx_u2 d00 = *(const mx_u2 *)(sp + aoff);
@@ -542,12 +654,12 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         (void)em;
         mx_wave_sync();
 #ifndef JX_MX_DBG_NOEXACT        /* measurement only: no exact pass (NOT bit-exact) */
-        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx_exact(L, sp, fl, T);
+        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx_defer(L, sp, fl, b0, nq, ns, g, T);
 #endif
         /* stores: channel c's 8 blocks x 128 B; always three store instructions (the vmcnt
          * accounting above counts on it) */
         if (mx_simple_store(P, g, b0)) {
-            int16_t *ob = g.out + (long long)P.f * g.ofstride + (long long)P.bi * 64 + lane * 8;
+            int16_t *ob = P.dst + lane * 8;
             const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
 #pragma unroll
             for (int c = 0; c < 3; c++) {
@@ -570,9 +682,10 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             }
         }
         mx_wave_sync();
-        mx_advance(P, g);
+        mx_next(P, g, b0);
         slot = slot == 2 ? 0u : slot + 1u;
     }
+    if (nq) mx_flush(L, nq, ns, g, T);
 }
 
 int mx_rc(hipError_t e) { return e == hipSuccess ? JPGX_OK : JPGX_EHIP; }

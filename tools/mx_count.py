@@ -29,5 +29,5 @@ for q in (50, 90):
     jpgx.blocks_gpu(fr, jpgx.default_params(W, H, q), d_in, out, ws)
     rd(buf)
     steps = F * nb // 8
-    print(f"q{q}: steps {steps} exact passes {buf[0]} ({buf[0] / steps:.3f}/step) tasks {buf[1]} "
-          f"({buf[1] / steps:.3f}/step) batches {buf[2]}")
+    print(f"q{q}: steps {steps} flushes {buf[0]} ({buf[0] / steps:.4f}/step) deferred tasks {buf[1]} "
+          f"({buf[1] / steps:.3f}/step) inline passes {buf[2]}")
