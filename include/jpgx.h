@@ -44,6 +44,7 @@ extern "C" {
 #define JPGX_EHIP (-5)       /* HIP runtime error                                          */
 #define JPGX_EWORKSPACE (-6) /* workspace smaller than jpgx_workspace_size()               */
 #define JPGX_ENODEV (-7)     /* no usable GPU                                              */
+#define JPGX_ENOMEM (-8)     /* host allocation failed                                     */
 
 /* Chroma sampling constants, src/headers/jpg_encode.h:13-15.  The reference does not
  * actually subsample (src/downsample.c:24-32): 1 and 2 only tighten the geometry rule
@@ -114,8 +115,9 @@ size_t jpgx_chroma_blocks(int width, int row_begin, int row_end, int sample_rati
 
 /* ---- device path (pointers are device pointers; `stream` is a hipStream_t or NULL) ---- */
 
-/* Bytes of device workspace one jpgx_blocks_gpu call on `fr` needs.  Currently 0 for every
- * geometry (the exact-path queue lives in LDS); kept so callers stay source-compatible. */
+/* Bytes of device workspace one jpgx_blocks_gpu call on `fr` needs: 0 for every geometry
+ * (both 4:4:4 kernels and k_chroma keep their exact-pass queues in LDS; d_workspace may then
+ * be NULL).  Kept so callers stay source-compatible. */
 size_t jpgx_workspace_size(const jpgx_frames *fr);
 
 /* The fused hot path: RGB -> quantised zig-zag int16 for every block of fr's stripe of every

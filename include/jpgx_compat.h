@@ -107,9 +107,11 @@ typedef struct jpgx_jpeg_data {
 } jpgx_jpeg_data;
 typedef jpgx_jpeg_data *jpgx_JpgData;
 
-/* j->width, j->height must be set (multiples of 8).  Sets num_blocks_* = (W/8)(H/8)
- * (preprocess.c:45-47), allocates zig_zag_* as zig_zag() does (an int* array of int[64],
- * zig_zag.c:24-32) and widens coef [3][nb][64] into it.  Returns 0 or JPGX_EARG. */
+/* j->width, j->height must be set (multiples of 8) and zig_zag_Y/Cb/Cr must be NULL (a filled
+ * JpgData is released with jpgx_free_jpgdata first).  Allocates zig_zag_* as zig_zag() does
+ * (an int* array of int[64], zig_zag.c:24-32), widens coef [3][nb][64] into it and then sets
+ * num_blocks_* = (W/8)(H/8) (preprocess.c:45-47).  Returns 0, JPGX_EARG, or JPGX_ENOMEM
+ * (then j is unchanged). */
 int jpgx_fill_jpgdata(jpgx_JpgData j, const int16_t *coef);
 /* frees what jpgx_fill_jpgdata allocated (zig_zag_*), leaves the rest */
 void jpgx_free_jpgdata(jpgx_JpgData j);

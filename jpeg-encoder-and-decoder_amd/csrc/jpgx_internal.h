@@ -32,21 +32,12 @@ struct jx_qtab {
     float w[3][8][8];       /* [ch][u][v]: fp32 scale of coefficient (u,v), 1/Q folded    */
     int16_t q[2][64];       /* scaled tables, q[t][u*8+v] = Qs[u][v] as the reference
                                indexes them (src/quantise.c:58)                           */
-    float wp[3][4][8][2];   /* packed path: [ch][j][v] = (w(u0,v), w(u1,v)) for the column
-                               pair j = (u0,u1) = (0,4), (2,6), (1,3), (5,7) (jx_pk_k)    */
 };
 
 /* guard band: |t - rint(t)| >= lim -> exact path.  [0] = rigorous band, [1] = FORCE_EXACT
  * (every entry -1: every coefficient takes the exact path) */
 struct jx_limtab {
     float lim[3][8][8];     /* [ch][u][v] */
-    float limcol[3][8];     /* [ch][u]: min over v (one limit per column, JX_FLAG_MODE 3)  */
-    float lsq[3][4][8][2];  /* packed path: a float <= lim^2 (or -1 where lim < 0), pair
-                               order as jx_qtab.wp: flag when d*d - lsq >= 0                */
-    float lsqn[3][8][8];    /* [ch][u][v]: a float <= lim^2 (-1 where lim < 0): the packed
-                               band test d*d - lsqn >= 0 of JX_FLAG_MODE 4                  */
-    float limh[3][4][8];    /* two-lane kernel: [ch][k][v] = min(lim(k,v), lim(4+k,v)), one
-                               band for the two half-waves (columns k and 4+k)             */
 };
 
 #define JX_MAXQ 97
@@ -56,7 +47,8 @@ struct jx_limtab {
  * quality, plan column n = 8c + u holds the scales and guard band of coefficients (c, u,
  * v = 0..7). */
 #ifndef JX_MX_PARTS
-#define JX_MX_PARTS 3
+#define JX_MX_PARTS 2       /* 2: hi + one lo part (band 1.28x that of 3 parts, 16 MFMAs per
+                               8 blocks instead of 24: jpgx_plan.cpp's bound covers either) */
 #endif
 struct jx_mxtab {
     float w[24][8];         /* 1/4 a(u) a(v) k(v) / Q[u][v] (row transform uses exact cosines) */
@@ -65,26 +57,18 @@ struct jx_mxtab {
     int16_t q[2][64];       /* scaled tables, q[t][u*8+v] = Qs[u][v] (src/quantise.c:58)       */
 };
 
-/* Device workspace: per k_xform wave and channel, the blocks with a coefficient inside the
- * guard band (no atomics: every wave owns a region), consumed by k_fix. */
-struct jx_fixlist {
-    unsigned *count;        /* [3][nwaves] items per wave and channel (all written)       */
-    uint32_t *items;        /* [3][nwaves][capw] launch-global block indices              */
-    unsigned nwaves;        /* k_xform waves of the launch                                */
-    unsigned capw;          /* items per wave and channel = 64 * tiles per wave           */
-};
-#define JX_WS_HEADER 256    /* bytes before the item lists in the workspace               */
-
 struct jx_xform_args {
     jx_geom g;
-    jx_fixlist fix;
     int quality;            /* index into the device table                                */
     int force_exact;        /* JPGX_FLAG_FORCE_EXACT: flag every coefficient              */
     int luma_only;          /* k_xform: channel 0 only (chroma from k_chroma)             */
     int sub;                /* k_chroma: 1 = true 4:2:2, 2 = true 4:2:0                   */
-    unsigned *rec_pg;       /* k_mx: flagged pair-group records (workspace), [pair-groups]  */
-    uint64_t *rec_sv;       /*       and their lane masks [pair-groups][2][8]               */
 };
+
+/* the 4:4:4 kernel used when JPGX_KERNEL is unset: 1 = k_mx, 0 = k_xform */
+#ifndef JX_DEFAULT_MX
+#define JX_DEFAULT_MX 0
+#endif
 
 
 #ifdef __cplusplus
@@ -97,6 +81,7 @@ int jx_plan_tables_mode(int quality, int sub, float w[3][64], float lim[3][64], 
 void jx_under_dwords(const uint8_t under[3][8], uint32_t out[6]);
 /* packed-pair vs scalar transform, bit for bit (host; returns the mismatch count) */
 long long jx_selftest_pk(long long nblocks, unsigned long long seed);
+int jx_mx_parts(void);
 /* k_mx: tables and f16 B operands (host plan), launch (device side) */
 int jx_plan_tables_mx(int quality, float w[24][8], float lim[24][8], int16_t q[2][64]);
 int jx_mx_operands(uint16_t ops[3 * JX_MX_PARTS][64][8]);

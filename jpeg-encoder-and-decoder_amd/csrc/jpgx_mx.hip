@@ -57,8 +57,18 @@ typedef uint32_t mx_u4 __attribute__((ext_vector_type(4)));
 typedef uint32_t mx_u2 __attribute__((ext_vector_type(2)));
 
 constexpr float kMagic = 12582912.0f;   /* 1.5 * 2^23: x + kMagic rounds x to an integer     */
+constexpr int kParts = JX_MX_PARTS;     /* f16 parts of B: hi (exact products) + lo [+ lo2]  */
 constexpr unsigned kSlot = 1536;        /* one step's pixels: [y][8 blocks x 24 B]           */
-constexpr unsigned kRing = 3;
+#ifndef JX_MX_DIST
+#define JX_MX_DIST 2                    /* DMA issued this many steps ahead                  */
+#endif
+constexpr unsigned kDist = JX_MX_DIST;
+constexpr unsigned kRing = kDist + 1;   /* LDS input slots                                   */
+/* s_waitcnt immediate for vmcnt(5 kDist - 2): the VMEM operations younger than a step's DMA
+ * (kDist steps' 3 stores each, kDist - 1 steps' 2 DMA pieces each) */
+constexpr unsigned kVmWait = 5 * kDist - 2;
+constexpr int kWaitImm = (int)((kVmWait & 15u) | ((kVmWait >> 4) << 14) | 0xF70u);
+static_assert(kVmWait < 64, "vmcnt is 6 bits");
 #ifndef JX_MX_WPE
 #define JX_MX_WPE 3                     /* waves per SIMD the register allocation targets    */
 #endif
@@ -211,6 +221,14 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) void *mx_lp;
 typedef const __attribute__((address_space(1))) void *mx_gp;
 
+/* n 4-byte LDS-DMA operations of the input's first bytes into dst (timing experiments) */
+[[maybe_unused]] __device__ __forceinline__ void mx_pad_raw(const MxG &g, uint8_t *dst, int n)
+{
+    for (int i = 0; i < n; i++)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g.rgb,
+                                         (__attribute__((address_space(3))) void *)dst, 4, 0, 0);
+}
+
 /*
  * The pixels of the step starting at block b0 (position P) into `slot` ([y][24 jb + k]).
  * Simple steps: two LDS-DMA instructions of 16-byte pieces (piece p = lane, and 64 + lane for
@@ -226,6 +244,12 @@ typedef const __attribute__((address_space(1))) void *mx_gp;
 __device__ __forceinline__ void mx_issue(const MxG &g, const MxCur &P, unsigned b0, bool simple,
                                          uint32_t off0, uint32_t off1, uint8_t *slot)
 {
+#ifdef JX_MX_DBG_NOLOAD        /* timing experiments only: padding instead of the pixel DMA */
+    if (b0 != 0xffffffffu) {
+        mx_pad_raw(g, slot, 2);
+        return;
+    }
+#endif
     if (simple) {
         const uint8_t *base = P.src;
         __builtin_amdgcn_global_load_lds((mx_gp)(base + off0), (mx_lp)slot, 16, 0, 0);
@@ -460,8 +484,15 @@ __device__ __forceinline__ void mx_column(const mx_f2 (&R)[4], const mx_f2 (&W)[
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
+#ifdef JX_MX_DBG_NOSTAGE       /* timing experiments only: no zig-zag LDS writes */
+        emax += __uint_as_float((__float_as_uint(tm.x) ^ __float_as_uint(tm.y)) & 0x007fffffu);
+#else
         *(uint16_t *)(st + zo[jx_pk_k(p, 0)]) = (uint16_t)__float_as_uint(tm.x);
         *(uint16_t *)(st + zo[jx_pk_k(p, 1)]) = (uint16_t)__float_as_uint(tm.y);
+#endif
+#ifdef JX_MX_DBG_NOBAND        /* timing experiments only: no band test (NOT exact) */
+        continue;
+#endif
         const mx_f2 rr = tm - M2;
         const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
         const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
@@ -557,19 +588,19 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     for (int v = 0; v < 8; v++) zo[v] = 2u * (unsigned)kMxScan[v][u];
     uint8_t *const st1 = L.stage + mx_sb(j >> 3) + kBS * gq;           /* set 0: block gq       */
     uint8_t *const st3 = L.stage + mx_sb(2) + kBS * (j < 8 ? gq : 4u + gq);
-    mx_u4 B[3][3];
+    mx_u4 B[kParts][3];
 #pragma unroll
-    for (int p = 0; p < 3; p++)
+    for (int p = 0; p < kParts; p++)
 #pragma unroll
         for (int w = 0; w < 3; w++) B[p][w] = g_mxB[3 * p + w][lane];
 
     MxCur P;
     mx_seek(P, g, 8u * s);
-    /* prologue: the first two steps' DMA (ring slots 0, 1), each followed by three padding
-     * operations in place of the stores of the (absent) steps s-2 and s-1 */
+    /* prologue: the first kDist steps' DMA (ring slots 0..kDist-1), each followed by three
+     * padding operations in place of the stores of the (absent) steps before s */
     MxCur PN = P;                                  /* position of the next step to issue */
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < (int)kDist; k++) {
         const unsigned sn = s + (unsigned)k;
         if (sn < s_end) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[k]);
         else mx_pad(g, L, 2);
@@ -582,16 +613,16 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         const unsigned b0 = 8u * s;
         /* this step's DMA: younger VMEM operations are the next step's 2 pieces and the last
          * two steps' 3 stores each (vmcnt counts loads, LDS-DMA and stores in issue order) */
-        /* VMEM operations younger than this step's DMA, in issue order: step s-2's three stores,
-         * step s+1's two DMA pieces, step s-1's three stores (padding operations stand in for
-         * the ones that do not exist; a general step's loads and the exact flush wait for
-         * themselves, which only makes this count conservative) */
-        __builtin_amdgcn_s_waitcnt(0xF78);             /* vmcnt(8) */
+        /* VMEM operations younger than this step's DMA, in issue order: the three stores of each
+         * of steps s-kDist..s-1 and the two DMA pieces of each of steps s+1..s+kDist-1 (padding
+         * operations stand in for the ones that do not exist; a general step's loads and the
+         * exact flush wait for themselves, which only makes this count conservative) */
+        __builtin_amdgcn_s_waitcnt(kWaitImm);
         mx_wave_sync();
         uint8_t *const sp = L.ring[slot];
         /* the step after next: its DMA into the slot step s-1 used */
         {
-            const unsigned sn = s + 2u, nslot = slot == 0 ? 2u : slot - 1u;
+            const unsigned sn = s + kDist, nslot = slot == 0 ? kRing - 1u : slot - 1u;
             if (sn < s_end) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[nslot]);
             else mx_pad(g, L, 2);
             mx_next(PN, g, 8u * sn);
@@ -617,8 +648,10 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             o[2] = mx_mma(Ahi, B[0][0], z);
             o[1] = mx_mma(Alo, B[1][0], z);
             o[3] = mx_mma(Ahi, B[1][0], z);
-            o[1] = mx_mma(Alo, B[2][0], o[1]);
-            o[3] = mx_mma(Ahi, B[2][0], o[3]);
+            if (kParts == 3) {
+                o[1] = mx_mma(Alo, B[kParts - 1][0], o[1]);
+                o[3] = mx_mma(Ahi, B[kParts - 1][0], o[3]);
+            }
         };
         const auto column = [&](int k) {
             mx_combine(acc[k][0], acc[k][1], acc[k][2], acc[k][3], R);
@@ -643,10 +676,12 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         acc[2][2] = mx_mma(A11, B[0][2], acc[2][2]);
         acc[2][1] = mx_mma(A10, B[1][2], acc[2][1]);
         acc[2][3] = mx_mma(A11, B[1][2], acc[2][3]);
-        acc[2][1] = mx_mma(A00, B[2][1], acc[2][1]);
-        acc[2][3] = mx_mma(A01, B[2][1], acc[2][3]);
-        acc[2][1] = mx_mma(A10, B[2][2], acc[2][1]);
-        acc[2][3] = mx_mma(A11, B[2][2], acc[2][3]);
+        if (kParts == 3) {
+            acc[2][1] = mx_mma(A00, B[kParts - 1][1], acc[2][1]);
+            acc[2][3] = mx_mma(A01, B[kParts - 1][1], acc[2][3]);
+            acc[2][1] = mx_mma(A10, B[kParts - 1][2], acc[2][1]);
+            acc[2][3] = mx_mma(A11, B[kParts - 1][2], acc[2][3]);
+        }
         __builtin_amdgcn_sched_barrier(0);
         column(1);
         __builtin_amdgcn_sched_barrier(0);
@@ -658,6 +693,11 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
 #endif
         /* stores: channel c's 8 blocks x 128 B; always three store instructions (the vmcnt
          * accounting above counts on it) */
+#ifdef JX_MX_DBG_NOSTORE       /* timing experiments only: padding instead of the stores */
+        if (b0 != 0xffffffffu) {
+            mx_pad(g, L, 3);
+        } else
+#endif
         if (mx_simple_store(P, g, b0)) {
             int16_t *ob = P.dst + lane * 8;
             const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
@@ -683,7 +723,7 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         }
         mx_wave_sync();
         mx_next(P, g, b0);
-        slot = slot == 2 ? 0u : slot + 1u;
+        slot = slot == kRing - 1u ? 0u : slot + 1u;
     }
     if (nq) mx_flush(L, nq, ns, g, T);
 }

@@ -462,6 +462,8 @@ static int mx_split(MxSplit &S)
     return JPGX_OK;
 }
 
+extern "C" int jx_mx_parts(void) { return JX_MX_PARTS; }
+
 extern "C" int jx_mx_operands(uint16_t ops[3 * JX_MX_PARTS][64][8])
 {
     static MxSplit S;

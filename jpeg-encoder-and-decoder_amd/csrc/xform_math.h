@@ -65,45 +65,6 @@ JX_HD typename O::T jx_pixel(typename O::T r, typename O::T g, typename O::T b)
     return O::fmac(r, JX_K(0.5), O::fmac(g, JX_K(-0.418688), O::mulc(b, JX_K(-0.081312))));
 }
 
-#ifndef JX_DCT_AAN   /* 1: Arai-Agui-Nakajima factorisation with FMAs (30 ops, scaled outputs) */
-#define JX_DCT_AAN 0
-#endif
-
-#if JX_DCT_AAN
-/*
- * Scaled 8-point DCT-II after Arai, Agui and Nakajima, with multiply-adds fused: 30 ops.
- * Output k is a fixed multiple of sum_x in[x] cos((2x+1)k pi/16); jx_dct_kfactor(k) (computed
- * on the host from this same code) undoes it inside the per-coefficient scale w(u,v).
- */
-template <class O>
-JX_HD void jx_fdct8(const typename O::T *in, typename O::T *out)
-{
-    typedef typename O::T T;
-    const T s0 = O::add(in[0], in[7]), d0 = O::sub(in[0], in[7]);
-    const T s1 = O::add(in[1], in[6]), d1 = O::sub(in[1], in[6]);
-    const T s2 = O::add(in[2], in[5]), d2 = O::sub(in[2], in[5]);
-    const T s3 = O::add(in[3], in[4]), d3 = O::sub(in[3], in[4]);
-    /* even part */
-    const T t10 = O::add(s0, s3), t13 = O::sub(s0, s3);
-    const T t11 = O::add(s1, s2), t12 = O::sub(s1, s2);
-    out[0] = O::add(t10, t11);
-    out[4] = O::sub(t10, t11);
-    const T z1 = O::add(t12, t13);
-    out[2] = O::fmac(z1, JX_K(JX_C4), t13);
-    out[6] = O::fmac(z1, JX_K(-JX_C4), t13);
-    /* odd part */
-    const T o10 = O::add(d3, d2), o11 = O::add(d2, d1), o12 = O::add(d1, d0);
-    const T z5 = O::mulc(O::sub(o10, o12), JX_K(JX_C6));
-    const T z2 = O::fmac(o10, JX_K(JX_C2 - JX_C6), z5);
-    const T z4 = O::fmac(o12, JX_K(JX_C2 + JX_C6), z5);
-    const T z11 = O::fmac(o11, JX_K(JX_C4), d0);
-    const T z13 = O::fmac(o11, JX_K(-JX_C4), d0);
-    out[5] = O::add(z13, z2);
-    out[3] = O::sub(z13, z2);
-    out[1] = O::add(z11, z4);
-    out[7] = O::sub(z11, z4);
-}
-#else
 /* Unnormalised 8-point DCT-II, even/odd split; out[4] lacks its cos(pi/4) factor. 34 ops. */
 template <class O>
 JX_HD void jx_fdct8(const typename O::T *in, typename O::T *out)
@@ -125,9 +86,7 @@ JX_HD void jx_fdct8(const typename O::T *in, typename O::T *out)
     out[7] = O::fmac(d0, JX_K(JX_C7), O::fmac(d1, JX_K(-JX_C5), O::fmac(d2, JX_K(JX_C3), O::mulc(d3, JX_K(-JX_C1)))));
 }
 
-#endif
 
-#if !JX_DCT_AAN
 /* Factor the computed out[k] must be multiplied by to give sum_x in[x] cos((2x+1)k pi/16). */
 JX_HD double jx_dct_kfactor(int k) { return k == 4 ? JX_C4 : 1.0; }
 
@@ -192,6 +151,5 @@ JX_HD constexpr int jx_pk_k(int j, int lane)
     return lane == 0 ? (j == 0 ? 0 : j == 1 ? 2 : j == 2 ? 1 : 5)
                      : (j == 0 ? 4 : j == 1 ? 6 : j == 2 ? 3 : 7);
 }
-#endif
 
 #endif

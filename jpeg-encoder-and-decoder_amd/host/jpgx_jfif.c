@@ -10,7 +10,8 @@
  *
  * The coefficients are the reference's, quirks included, and the file describes them
  * faithfully: the DQT entries are the divisors the reference actually applied, i.e. the scaled
- * table transposed (src/quantise.c:58).  A standard decoder therefore reproduces the
+ * table transposed (src/quantise.c:58); when one exceeds 255 (q <= 23) the tables are 16-bit
+ * and the frame is extended sequential (SOF1) instead of baseline.  A standard decoder therefore reproduces the
  * reference's pipeline output -- including the effects of its Cb sign error
  * (src/preprocess.c:161) and of the x0 = -8 last-column quirk.  AC magnitudes above 1023
  * (possible only for chroma at q >= 93 with the sign error) are clamped to the baseline range.
@@ -204,20 +205,30 @@ int jpgx_write_jfif_sub(const int16_t *coef, int width, int height, int quality,
     put_u16(&o, 1);
     put_u16(&o, 1);
     put_byte(&o, 0); put_byte(&o, 0);
-    for (int t = 0; t < 2; t++) {                          /* DQT: the divisors applied */
-        uint8_t zz[64];
+    /* DQT: the divisors applied.  For q <= 23 some exceed 255 (q = 1: 6050); baseline allows
+     * only 8-bit tables, so then both tables are written with 16-bit precision (Pq = 1) and
+     * the frame is extended sequential (SOF1, same Huffman coding), as libjpeg does. */
+    int wide = 0;
+    for (int t = 0; t < 2; t++)
+        for (int i = 0; i < 64; i++)
+            if (qs[t][i / 8][i % 8] > 255) wide = 1;
+    for (int t = 0; t < 2; t++) {
+        int zz[64];
         for (int v = 0; v < 8; v++)
             for (int u = 0; u < 8; u++) {
-                int q = qs[t][u][v];                       /* coefficient (row v, col u) was
+                const int q = qs[t][u][v];                 /* coefficient (row v, col u) was
                                                               divided by Qs[u][v] */
-                zz[scan[v][u]] = (uint8_t)(q < 1 ? 1 : (q > 255 ? 255 : q));
+                zz[scan[v][u]] = q < 1 ? 1 : q;
             }
         put_u16(&o, 0xffdb);
-        put_u16(&o, 2 + 65);
-        put_byte(&o, (uint8_t)t);
-        for (int k = 0; k < 64; k++) put_byte(&o, zz[k]);
+        put_u16(&o, (unsigned)(2 + 1 + 64 * (wide ? 2 : 1)));
+        put_byte(&o, (uint8_t)(wide << 4 | t));
+        for (int k = 0; k < 64; k++) {
+            if (wide) put_u16(&o, (unsigned)zz[k]);
+            else put_byte(&o, (uint8_t)zz[k]);
+        }
     }
-    put_u16(&o, 0xffc0);                                   /* SOF0 */
+    put_u16(&o, wide ? 0xffc1 : 0xffc0);                   /* SOF1 / SOF0 */
     put_u16(&o, 8 + 3 * 3);
     put_byte(&o, 8);
     put_u16(&o, (unsigned)height);

@@ -30,8 +30,8 @@ int jpgx_fill_jpgdata(jpgx_JpgData j, const int16_t *coef)
 {
     if (!j || !coef || j->width <= 0 || j->height <= 0 || j->width % 8 || j->height % 8)
         return JPGX_EARG;
+    if (j->zig_zag_Y || j->zig_zag_Cb || j->zig_zag_Cr) return JPGX_EARG;  /* would leak */
     const int nb = (j->width / 8) * (j->height / 8);  /* preprocess.c:45-47, every ratio */
-    j->num_blocks_Y = j->num_blocks_Cb = j->num_blocks_Cr = nb;
     int **zz[3] = {NULL, NULL, NULL};
     for (int c = 0; c < 3; c++) {                     /* zig_zag.c:24-32                */
         zz[c] = (int **)calloc((size_t)nb, sizeof(int *));
@@ -47,10 +47,11 @@ int jpgx_fill_jpgdata(jpgx_JpgData j, const int16_t *coef)
     j->zig_zag_Y = zz[0];
     j->zig_zag_Cb = zz[1];
     j->zig_zag_Cr = zz[2];
+    j->num_blocks_Y = j->num_blocks_Cb = j->num_blocks_Cr = nb;   /* only once all exist */
     return JPGX_OK;
 oom:                                                  /* rows not yet allocated are NULL */
     for (int c = 0; c < 3; c++) free_rows(zz[c], nb);
-    return JPGX_EARG;
+    return JPGX_ENOMEM;
 }
 
 void jpgx_dpcm(jpgx_JpgData j)
@@ -139,7 +140,7 @@ int jpgx_encode_bmp(const char *path, int quality, int sample_ratio, int device,
     int16_t *coef = NULL;
     if (!rc) {
         coef = (int16_t *)malloc((size_t)w * h * 3 * sizeof(int16_t));
-        rc = coef ? jpgx_blocks(rgb, w, h, (size_t)w * 3, &p, coef, device) : JPGX_EARG;
+        rc = coef ? jpgx_blocks(rgb, w, h, (size_t)w * 3, &p, coef, device) : JPGX_ENOMEM;
     }
     free(rgb);
     if (!rc) {

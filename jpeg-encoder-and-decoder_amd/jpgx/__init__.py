@@ -27,9 +27,9 @@ HORIZONTAL_VERTICAL_SUBSAMPLING = 2
 FLAG_FORCE_EXACT = 1
 FLAG_SUBSAMPLE = 2      # true 4:2:2 / 4:2:0 chroma (extension; see include/jpgx.h)
 
-OK, EGEOMETRY, EQUALITY, ESAMPLE, EARG, EHIP, EWORKSPACE, ENODEV = 0, -1, -2, -3, -4, -5, -6, -7
+OK, EGEOMETRY, EQUALITY, ESAMPLE, EARG, EHIP, EWORKSPACE, ENODEV, ENOMEM = 0, -1, -2, -3, -4, -5, -6, -7, -8
 _ERRNAMES = {-1: "EGEOMETRY", -2: "EQUALITY", -3: "ESAMPLE", -4: "EARG", -5: "EHIP",
-             -6: "EWORKSPACE", -7: "ENODEV"}
+             -6: "EWORKSPACE", -7: "ENODEV", -8: "ENOMEM"}
 
 # every function include/jpgx.h and include/jpgx_compat.h declare (tests check the library
 # exports them all)

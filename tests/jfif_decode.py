@@ -1,5 +1,5 @@
 """Minimal baseline-JPEG entropy decoder (test helper): parses the markers jpgx_write_jfif
-emits (SOF0, DQT, DHT, one interleaved SOS, no restart markers) and returns the quantised
+emits (SOF0, or SOF1 with 16-bit DQT, DHT, one interleaved SOS, no restart markers) and returns the quantised
 zig-zag coefficients [ncomp][nblocks][64] (a list [Y, Cb, Cr] for 4:2:2 / 4:2:0) and the
 DQT tables -- an independent check of the
 writer, written from ITU-T T.81 (Annex C canonical codes, F.2.2 decoding, F.1.2.3 stuffing)."""
@@ -62,7 +62,7 @@ def decode(data: bytes):
     b = bytes(data)
     assert b[:2] == b"\xff\xd8", "no SOI"
     i = 2
-    dqt, dht, comps, W, H = {}, {}, [], 0, 0
+    dqt, dht, comps, W, H, sof = {}, {}, [], 0, 0, None
     while True:
         assert b[i] == 0xFF
         m = b[i + 1]
@@ -71,9 +71,12 @@ def decode(data: bytes):
         if m == 0xDB:
             j = 0
             while j < len(seg):
-                assert seg[j] >> 4 == 0, "8-bit tables only"
-                dqt[seg[j] & 15] = list(seg[j + 1:j + 65])
-                j += 65
+                pq = seg[j] >> 4                       # 0: 8-bit, 1: 16-bit entries (T.81 B.2.4.1)
+                if pq == 0:
+                    dqt[seg[j] & 15] = list(seg[j + 1:j + 65])
+                else:
+                    dqt[seg[j] & 15] = [_u16(seg, j + 1 + 2 * k) for k in range(64)]
+                j += 1 + 64 * (pq + 1)
         elif m == 0xC4:
             j = 0
             while j < len(seg):
@@ -81,7 +84,8 @@ def decode(data: bytes):
                 n = sum(bits)
                 dht[tc_th] = _table(bits, list(seg[j + 17:j + 17 + n]))
                 j += 17 + n
-        elif m == 0xC0:
+        elif m in (0xC0, 0xC1):                        # baseline / extended sequential, Huffman
+            sof = m
             assert seg[0] == 8
             H, W = _u16(seg, 1), _u16(seg, 3)
             comps = [(seg[6 + 3 * k], seg[7 + 3 * k], seg[8 + 3 * k]) for k in range(seg[5])]
@@ -132,5 +136,5 @@ def decode(data: bytes):
         out = np.stack(out)
     rest = br.d[br.i:]
     assert rest[-2:] == b"\xff\xd9", "no EOI after the scan"
-    return {"width": W, "height": H, "coef": out, "dqt": dqt,
+    return {"width": W, "height": H, "coef": out, "dqt": dqt, "sof": sof,
             "qsel": [c[2] for c in comps], "sampling": (hs, vs)}

@@ -8,6 +8,7 @@ import pytest
 
 import oracle as O
 from conftest import GOLDEN, coef_sha, sha
+import jpgx
 from jpgx import compat as C
 from test_oracle import CHR, KAT_IN, LUM
 
@@ -180,8 +181,11 @@ def test_jfif_roundtrip_random(q):
                      [3, 8, 12, 17, 25, 30, 41, 43], [9, 11, 18, 24, 31, 40, 44, 53],
                      [10, 19, 23, 32, 39, 45, 52, 54], [20, 22, 33, 38, 46, 51, 55, 60],
                      [21, 34, 37, 47, 50, 56, 59, 61], [35, 36, 48, 49, 57, 58, 62, 63]])
+    wide = max(O.scale_table(LUM, q).max(), O.scale_table(CHR, q).max()) > 255
+    assert d["sof"] == (0xC1 if wide else 0xC0)        # 16-bit tables: extended sequential
+    assert wide == (q <= 23)
     for t, base in ((0, LUM), (1, CHR)):
-        qs = np.clip(O.scale_table(base, q), 1, 255)
+        qs = np.maximum(O.scale_table(base, q), 1)     # the true divisors, never clamped
         zz = np.zeros(64, np.int32)
         for v in range(8):
             for u in range(8):
@@ -205,14 +209,19 @@ def test_jfif_roundtrip_edge_values():
     _roundtrip(coef, W, H, 97)
 
 
-def test_jfif_decodes_with_pil():
-    """a standard decoder (PIL/libjpeg) accepts the file"""
+@pytest.mark.parametrize("q", [75, 1])
+def test_jfif_decodes_with_pil(q):
+    """a standard decoder (PIL/libjpeg) accepts the file: baseline at q = 75, extended
+    sequential with 16-bit quantisation tables at q = 1 (divisors up to 6050)"""
     import io
     Image = pytest.importorskip("PIL.Image")
     W, H = 64, 48
-    coef = O.blocks(O.gen_splitmix(11, W, H), 75)
-    img = Image.open(io.BytesIO(C.write_jfif(coef, W, H, 75)))
+    coef = O.blocks(O.gen_splitmix(11, W, H), q)
+    img = Image.open(io.BytesIO(C.write_jfif(coef, W, H, q)))
     img.load()
+    assert img.size == (W, H)
+    if q == 1:
+        assert max(max(t) for t in img.quantization.values()) > 255
     assert img.size == (W, H) and img.mode == "RGB"
 
 
@@ -245,3 +254,21 @@ def test_encode_bmp_to_jpeg_file(golden, name, tmp_path):
         C.encode_bmp_to_jpeg(src, dst, int(q))
         d = decode(open(dst, "rb").read())
         assert coef_sha(d["coef"].astype(np.int16)) == h, (name, q)
+
+
+def test_fill_jpgdata_refuses_to_leak():
+    """a JpgData that already holds zig_zag arrays is refused (JPGX_EARG, nothing changed);
+    after jpgx_free_jpgdata it can be filled again."""
+    import ctypes
+    W, H = 16, 8
+    coef = O.blocks(O.gen_splitmix(3, W, H), 50)
+    j = C.jpgdata_from_coef(W, H, coef)
+    nb = j.num_blocks_Y
+    rc = C.lib.jpgx_fill_jpgdata(ctypes.byref(j), np.ascontiguousarray(coef, np.int16).ctypes.data)
+    assert rc == jpgx.EARG and j.num_blocks_Y == nb
+    assert np.array_equal(C.jpgdata_zigzag(j), coef)
+    C.lib.jpgx_free_jpgdata(ctypes.byref(j))
+    assert not j.zig_zag_Y
+    rc = C.lib.jpgx_fill_jpgdata(ctypes.byref(j), np.ascontiguousarray(coef, np.int16).ctypes.data)
+    assert rc == jpgx.OK and np.array_equal(C.jpgdata_zigzag(j), coef)
+    C.lib.jpgx_free_jpgdata(ctypes.byref(j))

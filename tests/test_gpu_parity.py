@@ -152,9 +152,13 @@ def test_invalid_arguments_gpu(cuda):
         jpgx.blocks_gpu(jpgx.frames(16, 16, rows=(1, 3)), jpgx.default_params(16, 16, 50), rgb,
                         out, 0)
     assert e.value.rc == jpgx.EARG
-    small = torch.empty(jpgx.workspace_size(fr) - 4, dtype=torch.uint8, device=cuda)
-    with pytest.raises(jpgx.JpgxError) as e:        # workspace too small
-        jpgx.blocks_gpu(fr, jpgx.default_params(16, 16, 50), rgb, out, small)
+    assert jpgx.workspace_size(fr) == 0             # no workspace: NULL / 0 bytes accepted
+    jpgx.blocks_gpu(fr, jpgx.default_params(16, 16, 50), rgb, out, 0)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), O.blocks(np.zeros((16, 16, 3), np.uint8), 50))
+    ws = torch.empty(64, dtype=torch.uint8, device=cuda)
+    with pytest.raises(jpgx.JpgxError) as e:        # misaligned workspace pointer
+        jpgx.blocks_gpu(fr, jpgx.default_params(16, 16, 50), rgb, out, ws.data_ptr() + 4)
     assert e.value.rc == jpgx.EWORKSPACE
 
 

@@ -115,16 +115,10 @@ def test_kernel_cos_table_is_glibc():
 
 
 def test_workspace_size():
-    # k_xform: header + per-wave counts + per-wave lists with room for every block of its
-    # tiles; k_mx needs none (its exact-pass records live in LDS)
-    def expect(nblocks, nframes=1):
-        tiles = (nblocks + 63) // 64
-        return 256 + (3 * (tiles + 3) * 4 + 255) // 256 * 256 + 3 * (2 * tiles + 3) * 256
-    nb = (3840 // 8) * (2160 // 8) * 8
-    assert jpgx.workspace_size(jpgx.frames(3840, 2160, nframes=8)) == expect(nb, 8)
-    assert jpgx.workspace_size(jpgx.frames(64, 64, rows=(2, 5))) == expect(3 * 8)
-    assert jpgx.workspace_size(jpgx.frames(8, 8, nframes=1000)) == expect(1000, 1000)
-    assert jpgx.workspace_size(jpgx.frames(64, 64, rows=(3, 3))) == 0
+    # every kernel keeps its exact-pass queue in LDS: no device workspace for any geometry
+    for fr in (jpgx.frames(3840, 2160, nframes=8), jpgx.frames(64, 64, rows=(2, 5)),
+               jpgx.frames(8, 8, nframes=1000), jpgx.frames(64, 64, rows=(3, 3))):
+        assert jpgx.workspace_size(fr) == 0
 
 
 @pytest.mark.parametrize("q", [10, 50, 75, 90, 97])
@@ -150,11 +144,12 @@ def test_mx_operands_make_the_hi_product_exact():
     k > 24 zero; operand 3 part + which, which 0 = Y | Cb columns, 1 = Cr in columns 0..7, 2 = Cr
     in columns 8..15, the other half zero): the hi part is a multiple of 2^-11 whose products
     with b - 128 sum below 2^13 in every column (so the MFMA's hi accumulation is exact in fp32
-    whatever its internal order), and hi + lo + lo2 reconstruct the colour x cosine matrix and
-    the level-shift bias (the lo parts are stored scaled by 2^12)."""
+    whatever its internal order), and hi + lo [+ lo2] reconstruct the colour x cosine matrix and
+    the level-shift bias to the split's precision (the lo parts are stored scaled by 2^12)."""
     import ctypes
     import math
-    parts_n = 3
+    parts_n = jpgx.lib.jx_mx_parts()
+    assert parts_n in (2, 3)
     ops = np.zeros((3 * parts_n, 64, 8), np.uint16)
     f = jpgx.lib.jx_mx_operands
     f.restype = ctypes.c_int
@@ -170,10 +165,10 @@ def test_mx_operands_make_the_hi_product_exact():
     # plan columns n = 8c + u: Y|Cb from which 0, Cr from which 1
     M = np.concatenate([B[:, 0], B[:, 1, :, :8]], axis=2)      # [part][k][24]
     hi = M[0]
-    lo = (M[1] + M[2]) * 2.0 ** -12                            # lo parts stored x 2^12
+    lo = M[1:].sum(axis=0) * 2.0 ** -12                        # lo parts stored x 2^12
     assert np.all(hi * 2048 == np.round(hi * 2048))
     assert np.all(128 * np.abs(hi[:24]).sum(axis=0) + np.abs(hi[24]) < 8192)
-    tol = 2 ** -30
+    tol = 2 ** -30 if parts_n == 3 else 2 ** -23
     a = [(0.299, 0.587, 0.114), (-0.168736, 0.331264, -0.5), (0.5, -0.418688, -0.081312)]
     for c in range(3):
         for u in range(8):
