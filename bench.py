@@ -6,7 +6,7 @@ Workload (BASELINE.json metric "Mpixels/sec RGB->quantised-coeff, 4K 4:4:4 q=90"
   frames_per_gpu * N synthetic 3840x2160 RGB frames (4:4:4, q=90) -- configs[3]'s
   "batch of 64 x 4K frames, row-stripe sharded across 8 GPUs" at N=8, weak scaling.
   Frames are generated on the device (splitmix64) before timing; a step is one
-  jpgx_blocks_gpu() call over all frames of the stripe (one k_xform launch, whose in-kernel
+  jpgx_blocks_gpu() call over all frames of the stripe (one k_mx launch, whose in-kernel
   exact path recomputes the guard-band coefficients).
   8 frames per GPU = 597 MB moved per step, more than the 256 MiB Infinity Cache.
 
@@ -80,19 +80,51 @@ def _reference_rate(width, quality, seconds, jpgx):
     return width * 8 * rows / dt / 1e6, rows, dt, bool(np.array_equal(gpu, ref))
 
 
+def host_cpus():
+    """(usable cores, how that was determined, CPU model): the process's affinity set, capped
+    by a cgroup v2 CPU quota when one is set (a GPU box may show the whole machine's CPUs)."""
+    n, how = len(os.sched_getaffinity(0)), "sched_getaffinity"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, -(-int(quota) // int(period)))
+            if q < n:
+                n, how = q, f"cgroup cpu.max quota ({quota}/{period})"
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return n, how, model
+
+
 def cpu_baseline(width, height, quality, seconds, jpgx):
+    """CPU rates on bounded samples of the bench workload (rates are per pixel, so a sample of
+    the frame's first block-rows gives the same Mpixels/s as a whole frame at this per-block
+    cost; the sample is named in each entry)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    allc = max(1, min(16, len(os.sched_getaffinity(0))))
+    allc, how, model = host_cpus()
     p_all, rows_all, dt_all = _port_rate(width, height, quality, seconds / 3, allc)
-    extra = {"port_all_cores": {"value": round(p_all, 4), "cores": allc,
+    extra = {"cpu_model": model, "host_cores": allc, "host_cores_from": how,
+             "port_all_cores": {"value": round(p_all, 4), "cores": allc,
                                 "sample": f"block-rows 0..{rows_all} of a {width}x{height} "
-                                          f"frame, OpenMP over blocks, {dt_all:.1f} s"}}
+                                          f"frame ({rows_all * 8 * width} px, rate per pixel), "
+                                          f"OpenMP over blocks with {allc} threads, "
+                                          f"{dt_all:.1f} s"}}
     if os.path.exists(os.path.join(REPO, "oracle", "_ref", "ref_dump")):
         v, rows, dt, same = _reference_rate(width, quality, seconds, jpgx)
         return {"value": round(v, 4), "unit": "Mpixels/s", "cores": 1, "kind": "reference",
-                "sample": f"{width}x{8 * rows} synthetic BMP (splitmix seed 1), q={quality}, the "
-                          f"reference's preprocess->zig_zag compiled -O2 (oracle/_ref), "
-                          f"process wall {dt:.1f} s",
+                "sample": f"{width}x{8 * rows} synthetic BMP (splitmix seed 1), q={quality}: a "
+                          f"sub-frame of {8 * rows} of the {height} rows, its per-pixel rate "
+                          f"reported; the reference's preprocess->zig_zag compiled -O2 "
+                          f"(oracle/_ref), process wall {dt:.1f} s incl. BMP read",
                 "gpu_output_identical": same, **extra}
     v, rows, dt = _port_rate(width, height, quality, seconds, 1)
     return {"value": round(v, 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
@@ -101,16 +133,15 @@ def cpu_baseline(width, height, quality, seconds, jpgx):
                       f"{dt:.1f} s", **extra}
 
 
-def measured_traffic():
+def measured_traffic(kname):
     """HBM bytes per launch from the committed PMC profile (tools/pmc_summary.py, FETCH_SIZE x2
     + WRITE_SIZE per MI355X_MICROARCH.md), as a ratio to the algorithmic bytes -- only if it
     was measured on this exact kernel source.  rocprofv3 --pmc cannot run inside bench.py."""
     import glob
-    import hashlib
-    src = os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "csrc", "jpgx_kernels.hip")
-    with open(src, "rb") as f:
-        sha = hashlib.sha256(f.read()).hexdigest()
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_k_xform_pmc.json")),
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from pmc_summary import kernel_source_sha
+    sha = kernel_source_sha()
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{kname}_pmc.json")),
                        reverse=True):
         with open(path) as f:
             prof = json.load(f)
@@ -149,6 +180,46 @@ def max_over_ranks(x, world, device=None):
     return float(t.item())
 
 
+def check_output(d_out, plan, W, H, q, subsample, world, device, jpgx):
+    """After the timed region: hash the last step's output against tests/golden/big_golden.json
+    (the 64-frame 4K q90 batch, seeds 1000+f, pinned to the reference): every frame at N=1; at
+    N>1 frame 0, its stripes gathered to every rank (outside the timed region, the only data a
+    collective ever carries here).  None when the workload has no committed golden."""
+    import hashlib
+
+    import torch
+    path = os.path.join(REPO, "tests", "golden", "big_golden.json")
+    if subsample or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        gold = json.load(f)["batch64_4k_q90"]
+    if (W, H, q) != (gold["W"], gold["H"], gold["quality"]):
+        return None
+    frames = gold["frames"]
+    nb = plan["nb"]
+
+    def sha(t):
+        return hashlib.sha256(t.contiguous().cpu().numpy().astype("<i2").tobytes()).hexdigest()
+
+    if world == 1:
+        n = min(plan["B"], len(frames))
+        bad = [frames[f]["seed"] for f in range(n)
+               if sha(d_out[f].view(3, nb, 64)) != frames[f]["coef_sha256"]]
+        return {"frames_checked": n, "frames_wrong": bad, "ok": not bad,
+                "against": "tests/golden/big_golden.json batch64_4k_q90"}
+    import torch.distributed as dist
+    sizes = [rank_plan(W, H, 1, world, r, jpgx)["nb"] for r in range(world)]
+    nbmax = max(sizes)
+    mine = torch.zeros((3, nbmax, 64), dtype=torch.int16, device=device)
+    mine[:, :nb] = d_out[0].view(3, nb, 64)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather([p.view(torch.uint8) for p in parts], mine.view(torch.uint8))  # no int16
+    whole = torch.cat([p[:, :n] for p, n in zip(parts, sizes)], dim=1)
+    ok = sha(whole) == frames[0]["coef_sha256"]
+    return {"frames_checked": 1, "frames_wrong": [] if ok else [frames[0]["seed"]], "ok": ok,
+            "against": "tests/golden/big_golden.json batch64_4k_q90 (frame 0, all stripes)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -162,15 +233,15 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel", choices=["xform", "mx"], default=None,
-                    help="4:4:4 transform kernel (sets JPGX_KERNEL): k_xform (default) or k_mx, "
-                         "the matrix-core row pass (DESIGN.md 4.6)")
+                    help="4:4:4 transform kernel (sets JPGX_KERNEL): k_mx (default: colour and "
+                         "row DCT on the matrix cores) or k_xform (all-VALU), DESIGN.md 4")
     ap.add_argument("--subsample", action="store_true",
                     help="true 4:2:2 / 4:2:0 chroma (JPGX_FLAG_SUBSAMPLE, an extension; needs "
                          "--sample-ratio 1 or 2): not the headline metric")
     args = ap.parse_args()
     if args.kernel:
         os.environ["JPGX_KERNEL"] = args.kernel
-    kname = "k_mx" if os.environ.get("JPGX_KERNEL") == "mx" else "k_xform"
+    kname = "k_xform" if os.environ.get("JPGX_KERNEL") == "xform" else "k_mx"
 
     import torch
     import torch.distributed as dist
@@ -217,7 +288,7 @@ def main():
     for _ in range(args.warmup):
         step()
     # Kernel timing inside the timed region: HIP events on the launch stream around the whole
-    # loop of K back-to-back launches (the exact pass runs inside k_xform, so one launch per
+    # loop of K back-to-back launches (the exact pass runs inside the kernel, so one launch per
     # step); their span / K is the average launch duration, queue gaps included (the launches
     # are asynchronous, so the queue never drains between them).  The wall clock around the
     # same loop, bracketed by barrier + synchronize, gives the step time and `value`.
@@ -243,9 +314,9 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     achieved = bytes_per_px * px_rank_step / (xform_ms * 1e-3) / 1e9
 
+    check = check_output(d_out, plan, W, H, q, args.subsample, world, dev, jpgx)
     if rank == 0:
-        t_ratio, t_src = (measured_traffic() if not args.subsample and kname == "k_xform"
-                          else (None, None))
+        t_ratio, t_src = measured_traffic(kname) if not args.subsample else (None, None)
         cpu = None
         if N == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(W, H, q, args.cpu_seconds, jpgx)
@@ -272,10 +343,16 @@ def main():
                          "kernel_ms": round(xform_ms, 4),
                          "bytes_per_launch": bytes_per_px * px_rank_step},
             "cpu_baseline": cpu,
+            "output_check": check,
         }
         print(json.dumps(line), flush=True)
+    bad = check is not None and not check["ok"]
+    if bad and rank == 0:
+        log(f"bench: output differs from the golden hashes: {check}")
     if world > 1:
         dist.destroy_process_group()
+    if bad:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

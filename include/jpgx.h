@@ -21,7 +21,10 @@
  *
  * Conventions (unlike the reference, whose stages return void and mutate globals):
  *   - every entry point returns 0 or a negative JPGX_E* code;
- *   - callers own every buffer; the library keeps no global mutable state (reentrant);
+ *   - callers own every buffer; the device path keeps no global mutable state (reentrant);
+ *     the host-buffer path keeps its device buffers, streams and pinned staging in explicit
+ *     contexts (jpgx_host_*), which jpgx_blocks / jpgx_blocks_multi take from a thread-safe
+ *     process-wide pool (jpgx_host_release frees it);
  *   - quantisation tables are rebuilt from the pristine base tables on every call
  *     (the reference rescales its globals in place, src/quantise.c:34-35).
  */
@@ -154,14 +157,41 @@ int jpgx_gen_splitmix_gpu(uint8_t *d_dst, size_t nbytes, uint64_t seed, void *st
 /* Tie frame T: flat gray 8x8 blocks, v = 97 + 2*(block_index % 40), R=G=B. */
 int jpgx_gen_tie_gpu(uint8_t *d_dst, int width, int height, void *stream);
 
-/* ---- host-buffer conveniences (synchronous) ------------------------------------------ */
+/* ---- host-buffer path (synchronous; csrc/jpgx_host.cpp) ------------------------------ */
 
-/* Whole image in host memory -> host int16 [3][nb][64] on GPU `device`. */
+/* A host-buffer context: the image is cut into `nshards` balanced block-row shards
+ * (jpgx_stripe; MCU-row pairs for true 4:2:0), shard k runs on GPU devices[k] (NULL: k modulo
+ * the device count; several shards may name the same GPU), one host thread per shard, no
+ * communication between shards (each reads the pixel row above its first block row as halo and
+ * writes a disjoint range of the output).  A shard streams its rows through the device in
+ * chunks of `chunk_rows` block rows (0: about 4 MB of RGB per chunk), two chunks in flight on
+ * two streams, so one chunk's H2D overlaps the previous chunk's D2H.  Device chunk buffers,
+ * streams, events and pinned staging buffers are allocated on first use, grown when an image
+ * needs more, and kept until jpgx_host_destroy.  Pageable caller buffers are staged through
+ * the pinned buffers (host copies overlapped with the DMA); page-locked ones (hipHostMalloc,
+ * jpgx_host_register) are copied directly.  A context is used by one call at a time. */
+typedef struct jpgx_host_ctx jpgx_host_ctx;
+int jpgx_host_create(jpgx_host_ctx **ctx, int nshards, const int *devices, int chunk_rows);
+void jpgx_host_destroy(jpgx_host_ctx *ctx);
+
+/* Whole image in host memory (pixel rows `pitch` bytes apart) -> host int16 output laid out as
+ * jpgx_blocks_gpu's frame output ([3][nb][64], or Y | Cb | Cr with JPGX_FLAG_SUBSAMPLE). */
+int jpgx_host_blocks(jpgx_host_ctx *ctx, const uint8_t *rgb, int width, int height, size_t pitch,
+                     const jpgx_params *p, int16_t *out);
+
+/* Page-lock (hipHostRegister, portable) / release a caller buffer so that jpgx_host_blocks
+ * DMAs it directly. */
+int jpgx_host_register(void *ptr, size_t bytes);
+int jpgx_host_unregister(void *ptr);
+
+/* Frees the pooled contexts behind jpgx_blocks / jpgx_blocks_multi. */
+void jpgx_host_release(void);
+
+/* Whole image on GPU `device` (a pooled one-shard context). */
 int jpgx_blocks(const uint8_t *rgb, int width, int height, size_t pitch, const jpgx_params *p,
                 int16_t *out, int device);
 
-/* Same, sharded into ngpus block-row stripes (GPU 0..ngpus-1), one host thread and one
- * stream per GPU, no inter-GPU communication: the stripes' outputs are disjoint ranges. */
+/* Same, sharded into ngpus block-row stripes on GPUs 0..ngpus-1 (a pooled context). */
 int jpgx_blocks_multi(const uint8_t *rgb, int width, int height, size_t pitch,
                       const jpgx_params *p, int16_t *out, int ngpus);
 

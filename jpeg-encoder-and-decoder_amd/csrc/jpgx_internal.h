@@ -67,7 +67,7 @@ struct jx_xform_args {
 
 /* the 4:4:4 kernel used when JPGX_KERNEL is unset: 1 = k_mx, 0 = k_xform */
 #ifndef JX_DEFAULT_MX
-#define JX_DEFAULT_MX 0
+#define JX_DEFAULT_MX 1
 #endif
 
 

@@ -955,101 +955,4 @@ int jpgx_device_count(void)
     return n;
 }
 
-/* One GPU, one stripe: H2D of the stripe (+ the pixel row above it), run, D2H of the
- * stripe's three channel ranges into the whole-image host output: [3][nb][64], or with
- * JPGX_FLAG_SUBSAMPLE Y [nb][64] + Cb, Cr [nbc][64]. */
-static int run_stripe(const uint8_t *rgb, int width, int height, size_t pitch,
-                      const jpgx_params *p, int16_t *out, int device, int r0, int r1)
-{
-    if (r0 == r1) return JPGX_OK;
-    if (hipSetDevice(device) != hipSuccess) return JPGX_ENODEV;
-    const int bpr = width / 8;
-    const size_t row_bytes = (size_t)width * 3;
-    const size_t dpitch = (row_bytes + 7) & ~(size_t)7;
-    const int halo = r0 > 0 ? 1 : 0;
-    const size_t rows = (size_t)(r1 - r0) * 8 + halo;
-    const size_t nb_s = (size_t)(r1 - r0) * bpr, nb = (size_t)(height / 8) * bpr;
-    const size_t nbc_s = jpgx_chroma_blocks(width, r0, r1, p->sample_ratio, p->flags);
-    const size_t nbc = jpgx_chroma_blocks(width, 0, height / 8, p->sample_ratio, p->flags);
-    const size_t c0 = jpgx_chroma_blocks(width, 0, r0, p->sample_ratio, p->flags);
-    jpgx_frames fr;
-    memset(&fr, 0, sizeof fr);
-    fr.width = width;
-    fr.height = height;
-    fr.row_begin = r0;
-    fr.row_end = r1;
-    fr.nframes = 1;
-    fr.in_pitch = dpitch;
-    fr.in_frame_stride = dpitch * rows;
-    fr.out_frame_stride = (nb_s + 2 * nbc_s) * 64;
-    uint8_t *d_in = nullptr;
-    int16_t *d_out = nullptr;
-    void *d_ws = nullptr;
-    const size_t ws = jpgx_workspace_size(&fr);
-    hipStream_t s = nullptr;
-    int rc = JPGX_OK;
-    if (hipMalloc(&d_in, rows * dpitch) != hipSuccess ||
-        hipMalloc(&d_out, (nb_s + 2 * nbc_s) * 64 * sizeof(int16_t)) != hipSuccess ||
-        (ws && hipMalloc(&d_ws, ws) != hipSuccess) || hipStreamCreate(&s) != hipSuccess) {
-        rc = JPGX_EHIP;
-    }
-    if (!rc) {
-        const uint8_t *src = rgb + ((size_t)r0 * 8 - halo) * pitch;
-        rc = hip_rc(hipMemcpy2DAsync(d_in, dpitch, src, pitch, row_bytes, rows,
-                                     hipMemcpyHostToDevice, s));
-    }
-    if (!rc) rc = jpgx_blocks_gpu(&fr, p, d_in + halo * dpitch, d_out, d_ws, ws, s);
-    for (int ch = 0; ch < 3 && !rc; ch++) {
-        const size_t dst = ch == 0 ? (size_t)r0 * bpr : nb + (size_t)(ch - 1) * nbc + c0;
-        const size_t srcb = ch == 0 ? 0 : nb_s + (size_t)(ch - 1) * nbc_s;
-        const size_t cnt = ch == 0 ? nb_s : nbc_s;
-        rc = hip_rc(hipMemcpyAsync(out + dst * 64, d_out + srcb * 64, cnt * 64 * sizeof(int16_t),
-                                   hipMemcpyDeviceToHost, s));
-    }
-    if (!rc) rc = hip_rc(hipStreamSynchronize(s));
-    if (s) (void)hipStreamDestroy(s);
-    (void)hipFree(d_in);
-    (void)hipFree(d_out);
-    if (d_ws) (void)hipFree(d_ws);
-    return rc;
-}
-
-int jpgx_blocks(const uint8_t *rgb, int width, int height, size_t pitch, const jpgx_params *p,
-                int16_t *out, int device)
-{
-    if (!rgb || !out || !p) return JPGX_EARG;
-    int rc = jpgx_validate(width, height, p);
-    if (rc) return rc;
-    if (pitch < (size_t)width * 3) return JPGX_EARG;
-    if (device < 0 || device >= jpgx_device_count()) return JPGX_ENODEV;
-    return run_stripe(rgb, width, height, pitch, p, out, device, 0, height / 8);
-}
-
-int jpgx_blocks_multi(const uint8_t *rgb, int width, int height, size_t pitch,
-                      const jpgx_params *p, int16_t *out, int ngpus)
-{
-    if (!rgb || !out || !p || ngpus < 1) return JPGX_EARG;
-    int rc = jpgx_validate(width, height, p);
-    if (rc) return rc;
-    if (pitch < (size_t)width * 3) return JPGX_EARG;
-    if (ngpus > jpgx_device_count()) return JPGX_ENODEV;
-    std::vector<int> rcs(ngpus, JPGX_OK);
-    std::vector<std::thread> th;
-    /* true 4:2:0 stripes split MCU rows (pairs of block rows) */
-    const int unit = (p->flags & JPGX_FLAG_SUBSAMPLE) && p->sample_ratio == 2 ? 2 : 1;
-    for (int k = 0; k < ngpus; k++) {
-        th.emplace_back([&, k]() {
-            int r0, r1;
-            jpgx_stripe(height / 8 / unit, ngpus, k, &r0, &r1);
-            r0 *= unit;
-            r1 *= unit;
-            rcs[k] = run_stripe(rgb, width, height, pitch, p, out, k, r0, r1);
-        });
-    }
-    for (auto &t : th) t.join();
-    for (int k = 0; k < ngpus; k++)
-        if (rcs[k]) return rcs[k];
-    return JPGX_OK;
-}
-
 }  /* extern "C" */

@@ -39,7 +39,8 @@ EXPORTS = [
     "jpgx_gen_splitmix_gpu",
     "jpgx_gen_tie_gpu", "jpgx_blocks", "jpgx_blocks_multi", "jpgx_stripe",
     "jpgx_device_count", "jpgx_version", "jpgx_chroma_blocks", "jpgx_entropy_workspace_size",
-    "jpgx_entropy_stats_gpu",
+    "jpgx_entropy_stats_gpu", "jpgx_host_create", "jpgx_host_destroy", "jpgx_host_blocks",
+    "jpgx_host_register", "jpgx_host_unregister", "jpgx_host_release",
 ]
 COMPAT_EXPORTS = [
     "jpgx_new_block", "jpgx_get_value_block", "jpgx_set_value_block", "jpgx_copy_block",
@@ -105,6 +106,14 @@ def _load() -> ctypes.CDLL:
     L.jpgx_entropy_workspace_size.restype = sz
     L.jpgx_entropy_stats_gpu.argtypes = [vp, sz, sz, vp, vp, vp, vp, sz, vp]
     L.jpgx_version.restype = ctypes.c_char_p
+    L.jpgx_host_create.argtypes = [ctypes.POINTER(vp), i, vp, i]
+    L.jpgx_host_destroy.argtypes = [vp]
+    L.jpgx_host_destroy.restype = None
+    L.jpgx_host_blocks.argtypes = [vp, vp, i, i, sz, P, vp]
+    L.jpgx_host_register.argtypes = [vp, sz]
+    L.jpgx_host_unregister.argtypes = [vp]
+    L.jpgx_host_release.argtypes = []
+    L.jpgx_host_release.restype = None
     return L
 
 
@@ -293,3 +302,66 @@ def encode_blocks_multi(rgb: np.ndarray, quality: int, ngpus: int, sample_ratio:
     _check(lib.jpgx_blocks_multi(rgb.ctypes.data, W, H, W * 3, ctypes.byref(p), out.ctypes.data,
                                  ngpus), "jpgx_blocks_multi")
     return out
+
+
+class HostContext:
+    """jpgx_host_ctx: `nshards` block-row shards of every image, shard k on GPU devices[k]
+    (None: k modulo the device count), chunks of `chunk_rows` block rows (0: auto); device
+    buffers, streams and pinned staging persist across calls until close()."""
+
+    def __init__(self, nshards: int = 1, devices=None, chunk_rows: int = 0):
+        self._h = ctypes.c_void_p()
+        arr = None
+        if devices is not None:
+            devices = list(devices)
+            if len(devices) != nshards:
+                raise ValueError("one device per shard")
+            arr = (ctypes.c_int * nshards)(*devices)
+        _check(lib.jpgx_host_create(ctypes.byref(self._h), nshards,
+                                    ctypes.cast(arr, ctypes.c_void_p) if arr is not None else None,
+                                    chunk_rows), "jpgx_host_create")
+        self.nshards = nshards
+
+    def blocks(self, rgb: np.ndarray, quality: int, sample_ratio: int = 0, underflow=None,
+               flags: int = 0, out: np.ndarray | None = None) -> np.ndarray:
+        """Host (H, W, 3) uint8 -> host int16 coefficients (layout as encode_blocks)."""
+        if rgb.dtype != np.uint8 or rgb.ndim != 3 or rgb.shape[2] != 3 or rgb.strides[1:] != (3, 1):
+            raise ValueError("rgb must be (H, W, 3) uint8 with packed pixels")
+        H, W = rgb.shape[:2]
+        p = default_params(W, H, quality, sample_ratio, underflow, flags)
+        nb = (H // 8) * (W // 8)
+        nbc = chroma_blocks(W, 0, H // 8, sample_ratio, flags)
+        shape = (nb + 2 * nbc, 64) if flags & FLAG_SUBSAMPLE else (3, nb, 64)
+        if out is None:
+            out = np.empty(shape, np.int16)
+        elif out.shape != shape or out.dtype != np.int16 or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a contiguous int16 array of shape {shape}")
+        _check(lib.jpgx_host_blocks(self._h, rgb.ctypes.data, W, H, rgb.strides[0],
+                                    ctypes.byref(p), out.ctypes.data), "jpgx_host_blocks")
+        return out
+
+    def close(self) -> None:
+        if self._h:
+            lib.jpgx_host_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def host_register(a: np.ndarray) -> None:
+    """Page-lock a numpy buffer (jpgx_host_register) so jpgx_host_blocks DMAs it directly."""
+    _check(lib.jpgx_host_register(a.ctypes.data, a.nbytes), "jpgx_host_register")
+
+
+def host_unregister(a: np.ndarray) -> None:
+    _check(lib.jpgx_host_unregister(a.ctypes.data), "jpgx_host_unregister")

@@ -61,3 +61,55 @@ def _rank(rank, world, port, q):
 @pytest.mark.parametrize("q", [50, 90])
 def test_two_rank_stripes_stitch(q):
     mp.spawn(_rank, args=(2, _free_port(), q), nprocs=2, join=True)
+
+
+def _check_rank(rank, world, port, corrupt):
+    """bench.check_output's N>1 leg: frame 0's stripes gathered and hashed against the golden
+    64 x 4K q90 batch (each rank's stripe computed here by the oracle, as the GPU would)."""
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import jpgx
+    import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        Wk, Hk, q = 3840, 2160, 90
+        plan = bench.rank_plan(Wk, Hk, 1, world, rank, jpgx)
+        stripe = O.gen_splitmix(plan["seeds"][0], Wk, plan["rows_px"])
+        frame = np.zeros((Hk, Wk, 3), np.uint8)
+        top = 8 * plan["r0"] - plan["halo"]
+        frame[top:top + plan["rows_px"]] = stripe
+        out = O.blocks(frame, q, rows=(plan["r0"], plan["r1"]))
+        if corrupt and rank == world - 1:
+            out[2, -1, 63] ^= 1
+        d_out = torch.from_numpy(out.reshape(1, -1, 64))
+        res = bench.check_output(d_out, plan, Wk, Hk, q, False, world, torch.device("cpu"), jpgx)
+        assert res["frames_checked"] == 1 and res["ok"] is (not corrupt), res
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,corrupt", [(2, False), (3, False), (2, True)])
+def test_bench_output_check_gathers_stripes(world, corrupt):
+    mp.spawn(_check_rank, args=(world, _free_port(), corrupt), nprocs=world, join=True)
+
+
+def test_bench_output_check_single_rank():
+    """The N=1 leg hashes every frame of the step's output."""
+    import torch
+
+    import bench
+    import jpgx
+    import oracle as O
+    plan = bench.rank_plan(3840, 2160, 2, 1, 0, jpgx)
+    outs = np.stack([O.blocks(O.gen_splitmix(s, 3840, 2160), 90) for s in plan["seeds"]])
+    d_out = torch.from_numpy(outs.reshape(2, -1, 64))
+    res = bench.check_output(d_out, plan, 3840, 2160, 90, False, 1, None, jpgx)
+    assert res["ok"] and res["frames_checked"] == 2
+    d_out[1, 5, 7] += 1
+    res = bench.check_output(d_out, plan, 3840, 2160, 90, False, 1, None, jpgx)
+    assert not res["ok"] and res["frames_wrong"] == [1001]
+    assert bench.check_output(d_out, plan, 1920, 1080, 90, False, 1, None, jpgx) is None

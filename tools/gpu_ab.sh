@@ -1,15 +1,20 @@
 #!/bin/bash
-# A/B session: GPU parity tests on the default kernel, then bench default vs JPGX_KERNEL=xform.
+# A/B session: bench.py alternating between the two 4:4:4 kernels (REPS rounds, no CPU leg),
+# then the frames-per-launch sweep of both.  Usage (GPU box): bash tools/gpu_ab.sh [REPS]
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
-OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"
+OUT="$ROOT/gpurun_out/ab"; mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
-echo "pytest rc=$rc"; tail -30 "$OUT/pytest_gpu.log"
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-for k in default xform; do
-  if [ $k = xform ]; then export JPGX_KERNEL=xform; else unset JPGX_KERNEL; fi
-  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/bench_$k.json" 2> "$OUT/bench_$k.err"; rc=$?
-  echo "bench $k rc=$rc"; cat "$OUT/bench_$k.json"; tail -3 "$OUT/bench_$k.err"; [ $rc -eq 0 ] || exit $rc
+REPS=${1:-3}
+for r in $(seq 1 "$REPS"); do
+  for k in xform mx; do
+    timeout -k 10 300 python bench.py --kernel $k --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline > "$OUT/bench_${k}_$r.json" 2> "$OUT/bench_${k}_$r.err"; rc=$?
+    echo "bench $k rep $r rc=$rc $(python -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['frac'], d['output_check']['ok'])" "$OUT/bench_${k}_$r.json")"
+    [ $rc -eq 0 ] || { tail -5 "$OUT/bench_${k}_$r.err"; exit $rc; }
+  done
 done
+if [ "${SWEEP:-1}" = "1" ]; then
+  timeout -k 10 400 python tools/frames_sweep.py "$OUT/frames_sweep.json" xform mx > "$OUT/frames_sweep.log" 2>&1; rc=$?
+  echo "sweep rc=$rc"; tail -12 "$OUT/frames_sweep.log"; [ $rc -eq 0 ] || exit $rc
+fi

@@ -1,7 +1,7 @@
 """Summarise rocprofv3 output (tools/gpu_check.sh kernel-trace stats + tools/gpu_prof.sh PMC
 passes) for k_xform into a committed profile JSON.
 
-  python tools/pmc_summary.py gpurun_out profiles/r01_k_xform.json
+  python tools/pmc_summary.py gpurun_out profiles/r02_k_mx_pmc.json [k_mx|k_xform]
 
 HBM traffic per launch follows MI355X_MICROARCH.md's rocprofv3 section: FETCH_SIZE and
 WRITE_SIZE come from separate passes, are reported in KiB, and on gfx950 FETCH_SIZE counts half
@@ -15,13 +15,18 @@ import sys
 from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KSRC = os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "csrc", "jpgx_kernels.hip")
+CSRC = os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "csrc")
+KSRCS = ("jpgx_kernels.hip", "jpgx_mx.hip", "jpgx_internal.h", "xform_math.h")
 BYTES_PER_LAUNCH = 8 * 3840 * 2160 * 9          # bench.py workload, 9 B/px algorithmic
 
 
 def kernel_source_sha():
-    with open(KSRC, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()
+    """sha256 over the device sources both 4:4:4 kernels are built from."""
+    h = hashlib.sha256()
+    for name in KSRCS:
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
 
 
 def counters(path, kernel="k_xform"):
@@ -48,14 +53,14 @@ def mean(x):
     return sum(x) / len(x) if x else None
 
 
-def main(src, dst):
+def main(src, dst, kernel="k_xform"):
     pmc = {}
     for p in sorted(os.listdir(os.path.join(src, "pmc"))):
         f = os.path.join(src, "pmc", p, "run_counter_collection.csv")
         if os.path.exists(f):
-            for k, v in counters(f).items():
+            for k, v in counters(f, kernel).items():
                 pmc[k] = mean(v)
-    res = {"kernel": "k_xform", "kernel_source_sha256": kernel_source_sha(),
+    res = {"kernel": kernel, "kernel_source_sha256": kernel_source_sha(),
            "workload": "8 x 3840x2160 RGB, q=90 (bench.py)",
            "algorithmic_bytes_per_launch": BYTES_PER_LAUNCH, "pmc_mean_per_launch": pmc}
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
@@ -70,13 +75,18 @@ def main(src, dst):
         if os.path.exists(f):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if "k_xform" in row["Name"]:
+                    if kernel in row["Name"]:
                         res["rocprof_stats"] = {k: row[k] for k in row}
     tr = os.path.join(src, "prof", "run_kernel_trace.csv")
     if os.path.exists(tr):
-        ms = trace_ms(tr)
+        ms = trace_ms(tr, kernel)
         res["trace_mean_ms"] = mean(ms)
         res["trace_launches"] = len(ms)
+    for name in ("bench.json", "prof_bench.json"):    # bench lines of the same box session
+        f = os.path.join(src, name)
+        if os.path.exists(f) and os.path.getsize(f):
+            with open(f) as fh:
+                res["session_" + name.replace(".json", "")] = json.loads(fh.read().splitlines()[-1])
     os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
     with open(dst, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
@@ -84,4 +94,4 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])
