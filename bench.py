@@ -211,7 +211,7 @@ def check_output(d_out, plan, W, H, q, subsample, world, device, jpgx):
     sizes = [rank_plan(W, H, 1, world, r, jpgx)["nb"] for r in range(world)]
     nbmax = max(sizes)
     mine = torch.zeros((3, nbmax, 64), dtype=torch.int16, device=device)
-    mine[:, :nb] = d_out[0].view(3, nb, 64)
+    mine[:, :nb] = d_out[0].view(3, nb, 64).to(device)
     parts = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather([p.view(torch.uint8) for p in parts], mine.view(torch.uint8))  # no int16
     whole = torch.cat([p[:, :n] for p, n in zip(parts, sizes)], dim=1)
@@ -251,11 +251,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+    # one process per GPU over RCCL ("nccl").  JPGX_BENCH_BACKEND=gloo (with ranks placed on
+    # local_rank % device_count) rehearses the N>1 path on a box with fewer GPUs than ranks;
+    # it is never how numbers are taken.
+    backend = os.environ.get("JPGX_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group(backend)
+    cdev = dev if backend == "nccl" else torch.device("cpu")     # collectives' tensors
     N = world
 
     W, H, q = args.width, args.height, args.quality
@@ -305,7 +309,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, cdev)
 
     xform_ms = ev0.elapsed_time(ev1) / args.steps
     px_rank_step = B * (r1 - r0) * 8 * W
@@ -314,7 +318,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     achieved = bytes_per_px * px_rank_step / (xform_ms * 1e-3) / 1e9
 
-    check = check_output(d_out, plan, W, H, q, args.subsample, world, dev, jpgx)
+    check = check_output(d_out, plan, W, H, q, args.subsample, world, cdev, jpgx)
     if rank == 0:
         t_ratio, t_src = measured_traffic(kname) if not args.subsample else (None, None)
         cpu = None
@@ -333,13 +337,15 @@ def main():
                                    f", q={q}, block-row stripes",
                        "global_batch_frames": B, "width": W, "height": H, "quality": q,
                        "sample_ratio": args.sample_ratio, "parallelism": f"stripes{N}",
+                       "collectives": ("none" if N == 1 else
+                                       f"{backend}: barrier, max-time, output check"),
                        "kernel_timing": "HIP events around the K launches on their stream"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": (round(t_ratio * bytes_per_px * px_rank_step)
                                      if t_ratio else None),
                          "traffic_source": t_src,
-                         "kernel": kname if not args.subsample else "k_xform(Y)+k_chroma",
+                         "kernel": kname if not args.subsample else ("k_sub422" if args.sample_ratio == 1 and os.environ.get("JPGX_SUB422") != "two-pass" else "k_xform(Y)+k_chroma"),
                          "kernel_ms": round(xform_ms, 4),
                          "bytes_per_launch": bytes_per_px * px_rank_step},
             "cpu_baseline": cpu,

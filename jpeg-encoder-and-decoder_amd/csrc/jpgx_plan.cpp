@@ -64,18 +64,19 @@ struct BoundOps {
     static Bnd lit(jx_const k) { return Bnd{k.x, k.x, fabs((double)k.f - k.x)}; }
 };
 
-/* sub: 0 = one pixel per sample (4:4:4 and the reference's parity modes); 1 = the average
- * (p0 + p1) * 0.5 of two independent pixels (true 4:2:2); 2 = ((p00 + p01) + (p10 + p11)) * 0.25
- * (true 4:2:0), the kernel's (k_chroma) operation order */
+/* sub: 0 = one pixel per sample (4:4:4 and the reference's parity modes); 1 = true 4:2:2,
+ * 2 = true 4:2:0, in the kernels' (k_chroma, k_sub422) operation order: the colour transform
+ * of the pair's / quad's byte sums (exact integers <= 510 / 1020 in fp32), times 0.5 / 0.25.
+ * The exact value is the average of the pixels' samples (the oracle's definition); the colour
+ * transform being linear, it equals the transform of the sums scaled, in real arithmetic. */
 template <int CH>
 void coef_bounds(Bnd F[8][8], int sub = 0)
 {
-    const Bnd byte{0.0, 255.0, 0.0};
+    const Bnd byte{0.0, sub == 1 ? 510.0 : (sub == 2 ? 1020.0 : 255.0), 0.0};
     Bnd px[8], row[8];
     Bnd p = jx_pixel<BoundOps, CH>(byte, byte, byte);
-    if (sub == 1) p = BoundOps::mulc(BoundOps::add(p, p), JX_K(0.5));
-    if (sub == 2)
-        p = BoundOps::mulc(BoundOps::add(BoundOps::add(p, p), BoundOps::add(p, p)), JX_K(0.25));
+    if (sub == 1) p = BoundOps::mulc(p, JX_K(0.5));
+    if (sub == 2) p = BoundOps::mulc(p, JX_K(0.25));
     for (int x = 0; x < 8; x++) px[x] = p;
     jx_fdct8<BoundOps>(px, row);   /* every pixel row has the same bound */
     for (int u = 0; u < 8; u++) {

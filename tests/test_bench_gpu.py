@@ -1,0 +1,46 @@
+"""bench.py itself on the GPU: the N=1 line (contract keys, roofline, its own output check
+against the golden hashes) and the N>1 path rehearsed with two ranks on the box's one GPU
+(torch.distributed.run, gloo collectives: the stripes, per-rank seeds, barrier, max-over-ranks
+timing and the cross-rank output check all run; RCCL needs one GPU per rank)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+def _line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_single_gpu_line():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline"], cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert KEYS <= d.keys() and d["n_gpus"] == 1
+    assert d["output_check"]["ok"] and d["output_check"]["frames_checked"] == 8
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel"] == "k_mx"
+
+
+def test_bench_two_ranks_rehearsal():
+    env = dict(os.environ, JPGX_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        "29517", "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--frames-per-gpu", "2"], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch_frames"] == 4
+    assert d["cpu_baseline"] is None
+    assert d["output_check"]["ok"] and "all stripes" in d["output_check"]["against"]

@@ -75,6 +75,17 @@ def _dev(a, cuda):
     return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
 
 
+@pytest.fixture(params=["fused", "two-pass"])
+def impl(request, monkeypatch):
+    """True 4:2:2 runs as k_sub422 (one pass, the default) or, with JPGX_SUB422=two-pass, as
+    k_xform's Y + k_chroma<1>; 4:2:0 always uses the latter."""
+    if request.param == "two-pass":
+        monkeypatch.setenv("JPGX_SUB422", "two-pass")
+    else:
+        monkeypatch.delenv("JPGX_SUB422", raising=False)
+    return request.param
+
+
 def _check(rgb, q, sr, cuda, flags=0):
     H, W = rgb.shape[:2]
     out = jpgx.encode_blocks(_dev(rgb, cuda), q, sr, flags=jpgx.FLAG_SUBSAMPLE | flags)
@@ -92,19 +103,19 @@ def _check(rgb, q, sr, cuda, flags=0):
 @pytest.mark.gpu
 @pytest.mark.parametrize("sr", [1, 2])
 @pytest.mark.parametrize("q", [25, 50, 75, 90, 97])
-def test_gpu_subsample_random(cuda, sr, q):
+def test_gpu_subsample_random(cuda, impl, sr, q):
     _check(O.gen_splitmix(100 + q, 256, 128), q, sr, cuda)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sr", [1, 2])
-def test_gpu_subsample_force_exact(cuda, sr):
+def test_gpu_subsample_force_exact(cuda, impl, sr):
     _check(O.gen_splitmix(7, 128, 64), 75, sr, cuda, flags=jpgx.FLAG_FORCE_EXACT)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sr", [1, 2])
-def test_gpu_subsample_tie_and_flat(cuda, sr):
+def test_gpu_subsample_tie_and_flat(cuda, impl, sr):
     _check(O.gen_tie(256, 128), 50, sr, cuda)
     rgb = np.zeros((64, 128, 3), np.uint8)
     rgb[..., 0], rgb[..., 1], rgb[..., 2] = 255, 0, 128
@@ -113,13 +124,13 @@ def test_gpu_subsample_tie_and_flat(cuda, sr):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sr", [1, 2])
-def test_gpu_subsample_1080p_class(cuda, sr):
+def test_gpu_subsample_1080p_class(cuda, impl, sr):
     _check(O.gen_splitmix(2, 1920, 1072), 90, sr, cuda)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sr", [1, 2])
-def test_gpu_subsample_stripes_and_batch(cuda, sr):
+def test_gpu_subsample_stripes_and_batch(cuda, impl, sr):
     """Stripes of a batch of frames through the device entry point equal the whole frames."""
     import torch
     W, H, F = 256, 128, 3
@@ -148,6 +159,58 @@ def test_gpu_subsample_stripes_and_batch(cuda, sr):
     got = out.cpu().numpy()
     for f in range(F):
         assert np.array_equal(got[f], want[f]), f"frame {f}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sr", [1, 2])
+def test_gpu_subsample_4k_batch_golden(cuda, impl, sr):
+    """4 x 3840x2160 q75 true 4:2:2 / 4:2:0 frames in one launch, generated on the GPU, every
+    frame hashed against the oracle hashes in tests/golden/big_golden.json (sub_4k_q75)."""
+    import hashlib
+    import json
+    import os
+
+    import torch
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "big_golden.json")) as f:
+        ent = json.load(f)["sub_4k_q75"]
+    W, H, q = ent["W"], ent["H"], ent["quality"]
+    S = jpgx.FLAG_SUBSAMPLE
+    F = len(ent["seeds"])
+    d_in = torch.empty(F * W * H * 3, dtype=torch.uint8, device=cuda)
+    for i, seed in enumerate(ent["seeds"]):
+        jpgx.gen_splitmix_gpu(d_in[i * W * H * 3:(i + 1) * W * H * 3], seed)
+    nb = (H // 8) * (W // 8)
+    per = nb + 2 * jpgx.chroma_blocks(W, 0, H // 8, sr, S)
+    out = torch.empty((F, per, 64), dtype=torch.int16, device=cuda)
+    fr = jpgx.frames(W, H, nframes=F, out_frame_stride=per * 64)
+    jpgx.blocks_gpu(fr, jpgx.default_params(W, H, q, sr, flags=S), d_in, out, 0)
+    got = out.cpu().numpy()
+    bad = [seed for i, seed in enumerate(ent["seeds"])
+           if hashlib.sha256(got[i].astype("<i2").tobytes()).hexdigest()
+           != ent[f"sr{sr}_coef_sha256"][i]]
+    assert not bad, f"frames with wrong coefficients (seeds): {bad}"
+
+
+@pytest.mark.gpu
+def test_gpu_sub422_tiles_cross_frames(cuda, impl):
+    """nb = 170 blocks per frame (not a multiple of 64): tiles straddle frame ends, the last tile
+    is partial, every block row ends in the x0 = -8 quirk column (34 blocks per row)."""
+    import torch
+    W, H, F, q = 272, 40, 3, 80
+    frames = [O.gen_splitmix(90 + f, W, H) for f in range(F)]
+    S = jpgx.FLAG_SUBSAMPLE
+    nb = (H // 8) * (W // 8)
+    per = nb + 2 * jpgx.chroma_blocks(W, 0, H // 8, 1, S)
+    out = torch.zeros((F, per, 64), dtype=torch.int16, device=cuda)
+    fr = jpgx.frames(W, H, nframes=F, out_frame_stride=per * 64)
+    jpgx.blocks_gpu(fr, jpgx.default_params(W, H, q, 1, flags=S), _dev(np.stack(frames), cuda),
+                    out, 0)
+    got = out.cpu().numpy()
+    for f in range(F):
+        want = np.concatenate([O.blocks(frames[f], q, 1)[0],
+                               O.chroma_sub(frames[f], q, 1).reshape(-1, 64)])
+        assert np.array_equal(got[f], want), f"frame {f}"
 
 
 @pytest.mark.parametrize("sr", [1, 2])

@@ -15,15 +15,19 @@ import os, sys, json
 sys.path.insert(0, os.path.join(%(repo)r, "jpeg-encoder-and-decoder_amd"))
 import torch, jpgx, hashlib
 W, H, F, q = 3840, 2160, 8, 90
+sr = int(os.environ.get("VB_SUB", "0"))          # 1 / 2: true 4:2:2 / 4:2:0 at q75
+fl = jpgx.FLAG_SUBSAMPLE if sr else 0
+q = 75 if sr else q
 dev = torch.device("cuda:0")
 d_in = torch.empty(F * W * H * 3, dtype=torch.uint8, device=dev)
 for f in range(F):
     jpgx.gen_splitmix_gpu(d_in[f * W * H * 3:(f + 1) * W * H * 3], 1000 + f)
 nb = (W // 8) * (H // 8)
-out = torch.empty((F, 3, nb, 64), dtype=torch.int16, device=dev)
-fr = jpgx.frames(W, H, nframes=F)
+per = nb + 2 * jpgx.chroma_blocks(W, 0, H // 8, sr, fl)
+out = torch.empty((F, per, 64), dtype=torch.int16, device=dev)
+fr = jpgx.frames(W, H, nframes=F, out_frame_stride=per * 64)
 ws = torch.empty(max(jpgx.workspace_size(fr), 1), dtype=torch.uint8, device=dev)
-p = jpgx.default_params(W, H, q)
+p = jpgx.default_params(W, H, q, sr, flags=fl)
 for _ in range(3):
     jpgx.blocks_gpu(fr, p, d_in, out, ws)
 torch.cuda.synchronize()
@@ -65,7 +69,8 @@ def main():
             r = run(lib)
             res.setdefault(n, []).append(r)
     ref = res["default"][0].get("hash")
-    bytes_moved = 8 * 3840 * 2160 * 9
+    sr = int(os.environ.get("VB_SUB", "0"))
+    bytes_moved = 8 * 3840 * 2160 * (9 if sr == 0 else (7 if sr == 1 else 6))
     for n, rs in res.items():
         ms = sorted(m for r in rs for m in r.get("ms", []))
         ok = all(r.get("hash") == ref for r in rs)
