@@ -17,7 +17,8 @@
  *           bias 1.0).  One product with B = colour x cosine gives, in C row m, column j, the
  *           row transform of channel j/8 (Y, Cb), frequency u = j%8.  Cr: the two sets
  *           concatenated along K (B zero outside its set's columns), so column j of the Cr tile
- *           is set j/8's Cr at u = j%8.  B = Bh + 2^-12 (Bl + Bm), three f16 parts; acc_h =
+ *           is set j/8's Cr at u = j%8.  B = Bh + 2^-12 Bl (JX_MX_PARTS = 2 f16 parts; 3 adds a
+ *           second lo part for a 1.28x narrower band at 50% more MFMAs, measured slower); acc_h =
  *           A Bh is EXACT in any summation order (jpgx_plan.cpp); R = acc_h + 2^-12 acc_l.
  *   Columns every lane then holds three whole columns (8 rows, registers 0..3 of the two
  *           halves): (set 0, c = j/8, u), (set 1, same), (Cr, set j/8, u).  Each runs jx_fdct8_pk
@@ -26,10 +27,11 @@
  *           stage at its zig-zag position, and the band test d^2 - lsq >= 0 (d = F w - rint,
  *           exact) folded into a running max.
  *   Exact   (rare) a column whose max says "some coefficient in the band" records its flagged
- *           v's; after the step, eight flagged coefficients at a time, eight lanes each: lane x
- *           forms (X(x,y) c_u[x]) c_v[y] in fp64 from the slot's pixel bytes, the sum runs
- *           x-outer / y-inner (dct.c:46-50) lane to lane, F = ((1/4 a(u)) a(v)) s, round(F / Q)
- *           patches the stage.
+ *           v's; the step's flagged blocks' pixel rows are copied to a per-wave LDS side buffer
+ *           with their tasks (mx_defer); eight tasks at a time, eight lanes each (mx_flush):
+ *           lane x forms (X(x,y) c_u[x]) c_v[y] in fp64, the sum runs x-outer / y-inner
+ *           (dct.c:46-50) lane to lane over DPP, F = ((1/4 a(u)) a(v)) s, round(F / Q) goes to
+ *           HBM after the wave's own stores of those blocks have landed.
  *   Output  channel c's 8 blocks x 128 B leave as one 1-KiB nontemporal store.
  */
 #include <hip/hip_runtime.h>
