@@ -225,6 +225,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=200.0,
+                    help="after the W warmup steps, keep stepping (untimed) until this much time "
+                         "has passed, so the timed steps see the GPU's loaded steady state and not "
+                         "its ramp out of idle (about 20 ms of load; profiles/r02_ramp.json); 0 = off")
     ap.add_argument("--frames-per-gpu", type=int, default=8)
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
@@ -289,8 +293,25 @@ def main():
     def step(ev_mid=None):
         jpgx.blocks_gpu(fr, params, rgb_ptr, d_out, d_ws, event_between=ev_mid)
 
+    # W warmup steps, each timed on its own (reported as the cold start), then untimed steps
+    # until --settle-ms have passed: after idle the GPU's power management takes ~20 ms of load
+    # to reach its steady state (the first launches run 15-35% slower; profiles/r02_ramp.json)
+    cold = []
+    t_w = time.perf_counter()
     for _ in range(args.warmup):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         step()
+        e1.record()
+        cold.append((e0, e1))
+    settle_steps = 0
+    torch.cuda.synchronize()
+    while (time.perf_counter() - t_w) * 1e3 < args.settle_ms:
+        for _ in range(10):
+            step()
+        settle_steps += 10
+        torch.cuda.synchronize()
+    cold_ms = [a.elapsed_time(b) for a, b in cold]
     # Kernel timing inside the timed region: HIP events on the launch stream around the whole
     # loop of K back-to-back launches (the exact pass runs inside the kernel, so one launch per
     # step); their span / K is the average launch duration, queue gaps included (the launches
@@ -329,7 +350,10 @@ def main():
                       f"Mpixels/sec RGB->quantised-coeff, true {'4:2:2' if args.sample_ratio == 1 else '4:2:0'} "
                       f"q={q} (extension, not the headline)",
             "value": round(value, 1), "unit": "Mpixels/s", "n_gpus": N,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "steps": args.steps, "warmup": args.warmup,
+            "settle": {"ms": args.settle_ms, "extra_untimed_steps": settle_steps,
+                       "warmup_step_ms": [round(x, 4) for x in cold_ms]},
+            "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (splitmix64 RGB frames generated in HBM)",
             "config": {"workload": f"{args.frames_per_gpu} x {W}x{H} RGB frames per GPU, "
