@@ -225,6 +225,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--input-sets", type=int, default=2,
+                    help="copies of the input batch read by consecutive steps in turn (1 = the "
+                         "same input every step, which the Infinity Cache partly holds)")
     ap.add_argument("--settle-ms", type=float, default=200.0,
                     help="after the W warmup steps, keep stepping (untimed) until this much time "
                          "has passed, so the timed steps see the GPU's loaded steady state and not "
@@ -287,11 +290,19 @@ def main():
                      out_frame_stride=per * 64)
     d_ws = torch.empty(jpgx.workspace_size(fr), dtype=torch.uint8, device=dev)
     params = jpgx.default_params(W, H, q, args.sample_ratio, flags=flags)
-    rgb_ptr = d_in.data_ptr() + halo * row_bytes
+    # Consecutive steps read alternate copies of the batch (--input-sets): like a stream of new
+    # frames, a step's input is then not still resident in the 256 MiB Infinity Cache from the
+    # step before (2 x 199 MB per GPU at 8 frames; the frames sweep in DESIGN.md 4.3 measures
+    # what residency would be worth).  The copies are identical, so the output is checkable.
+    inputs = [d_in] + [d_in.clone() for _ in range(args.input_sets - 1)]
+    rgb_ptrs = [t.data_ptr() + halo * row_bytes for t in inputs]
     torch.cuda.synchronize()
+    nstep = [0]
 
     def step(ev_mid=None):
-        jpgx.blocks_gpu(fr, params, rgb_ptr, d_out, d_ws, event_between=ev_mid)
+        jpgx.blocks_gpu(fr, params, rgb_ptrs[nstep[0] % len(rgb_ptrs)], d_out, d_ws,
+                        event_between=ev_mid)
+        nstep[0] += 1
 
     # W warmup steps, each timed on its own (reported as the cold start), then untimed steps
     # until --settle-ms have passed: after idle the GPU's power management takes ~20 ms of load
@@ -363,7 +374,8 @@ def main():
                        "sample_ratio": args.sample_ratio, "parallelism": f"stripes{N}",
                        "collectives": ("none" if N == 1 else
                                        f"{backend}: barrier, max-time, output check"),
-                       "kernel_timing": "HIP events around the K launches on their stream"},
+                       "kernel_timing": "HIP events around the K launches on their stream",
+                       "input_sets": args.input_sets},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": (round(t_ratio * bytes_per_px * px_rank_step)

@@ -4,8 +4,8 @@ of input, under the 256 MiB Infinity Cache) to 16 and 24 frames (398 / 597 MB, o
 bench's 8-frame launch is not flattered by cache residency.
 
 Usage (GPU box): python tools/frames_sweep.py OUT.json [xform mx]
-HIP events around 10 back-to-back launches, 5 repetitions: min and median of the per-launch
-mean are reported."""
+After 200 ms of untimed launches (the GPU's ramp out of idle), HIP events around
+10 back-to-back launches, 5 repetitions: min and median of the per-launch mean are reported."""
 import json
 import os
 import statistics
@@ -31,9 +31,12 @@ def sweep(kernel, dev):
         out = torch.empty((F, 3, nb, 64), dtype=torch.int16, device=dev)
         fr = jpgx.frames(W, H, nframes=F)
         p = jpgx.default_params(W, H, q)
-        for _ in range(3):
-            jpgx.blocks_gpu(fr, p, d_in, out, 0)
-        torch.cuda.synchronize()
+        import time
+        t0 = time.perf_counter()                   # settle: the GPU's ramp out of idle (~20 ms)
+        while time.perf_counter() - t0 < 0.2:
+            for _ in range(5):
+                jpgx.blocks_gpu(fr, p, d_in, out, 0)
+            torch.cuda.synchronize()
         ts = []
         for _ in range(5):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -1,5 +1,5 @@
 // membench2.hip -- streaming ceilings for a 1:2 read:write byte mix (not product code).
-// 8 x 4K frames: 199 MB read (RGB) + 398 MB written (int16 coefficients), like k_xform.
+// F x 4K frames (argv[1], default 8): 3 B/px read (RGB) + 6 B/px written, like the kernels.
 //   ideal     : every lane reads 16 B and writes 2 x 16 B, all perfectly coalesced, persistent
 //   ideal_nt  : same with nontemporal stores
 //   ideal_np  : same, one element per thread (non-persistent grid)
@@ -55,9 +55,12 @@ __global__ void k_copy(const u32x4 *in, u32x4 *out, size_t n)
     for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) out[i] = in[i];
 }
 
-int main()
+int main(int argc, char **argv)
 {
-    const size_t in_bytes = 8ull * 3840 * 2160 * 3, out_bytes = 2 * in_bytes;
+    /* argv[1]: 4K frames of input (default 8 = 199 MB, under the 256 MiB Infinity Cache; 16+
+     * streams from HBM) */
+    const size_t frames = argc > 1 ? (size_t)atoi(argv[1]) : 8;
+    const size_t in_bytes = frames * 3840 * 2160 * 3, out_bytes = 2 * in_bytes;
     const size_t n = in_bytes / 16;
     u32x4 *din, *dout;
     CK(hipMalloc(&din, in_bytes));
@@ -70,7 +73,7 @@ int main()
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     auto run = [&](const char *name, auto launch, double bytes) {
-        for (int i = 0; i < 3; i++) launch();
+        for (int i = 0; i < 200; i++) launch();      /* settle: the GPU's ramp out of idle */
         CK(hipDeviceSynchronize());
         const int it = 20;
         CK(hipEventRecord(e0));
