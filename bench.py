@@ -220,6 +220,13 @@ def check_output(d_out, plan, W, H, q, subsample, world, device, jpgx):
             "against": "tests/golden/big_golden.json batch64_4k_q90 (frame 0, all stripes)"}
 
 
+def sub_kernel_name(sr):
+    """The kernels a true-subsampling launch runs (jpgx_blocks_gpu's dispatch)."""
+    if os.environ.get("JPGX_SUB422" if sr == 1 else "JPGX_SUB420") == "two-pass":
+        return f"k_xform(Y)+k_chroma<{sr}>"
+    return "k_sub422" if sr == 1 else "k_sub420"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -381,7 +388,7 @@ def main():
                          "traffic": (round(t_ratio * bytes_per_px * px_rank_step)
                                      if t_ratio else None),
                          "traffic_source": t_src,
-                         "kernel": kname if not args.subsample else ("k_sub422" if args.sample_ratio == 1 and os.environ.get("JPGX_SUB422") != "two-pass" else "k_xform(Y)+k_chroma"),
+                         "kernel": kname if not args.subsample else sub_kernel_name(args.sample_ratio),
                          "kernel_ms": round(xform_ms, 4),
                          "bytes_per_launch": bytes_per_px * px_rank_step},
             "cpu_baseline": cpu,

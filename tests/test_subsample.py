@@ -77,12 +77,13 @@ def _dev(a, cuda):
 
 @pytest.fixture(params=["fused", "two-pass"])
 def impl(request, monkeypatch):
-    """True 4:2:2 runs as k_sub422 (one pass, the default) or, with JPGX_SUB422=two-pass, as
-    k_xform's Y + k_chroma<1>; 4:2:0 always uses the latter."""
-    if request.param == "two-pass":
-        monkeypatch.setenv("JPGX_SUB422", "two-pass")
-    else:
-        monkeypatch.delenv("JPGX_SUB422", raising=False)
+    """True 4:2:2 / 4:2:0 run as k_sub422 / k_sub420 (one pass, the default) or, with
+    JPGX_SUB422 / JPGX_SUB420 = two-pass, as k_xform's Y + k_chroma<1> / <2>."""
+    for var in ("JPGX_SUB422", "JPGX_SUB420"):
+        if request.param == "two-pass":
+            monkeypatch.setenv(var, "two-pass")
+        else:
+            monkeypatch.delenv(var, raising=False)
     return request.param
 
 
@@ -190,6 +191,29 @@ def test_gpu_subsample_4k_batch_golden(cuda, impl, sr):
            if hashlib.sha256(got[i].astype("<i2").tobytes()).hexdigest()
            != ent[f"sr{sr}_coef_sha256"][i]]
     assert not bad, f"frames with wrong coefficients (seeds): {bad}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H", [(272, 48), (48, 32), (528, 16)])
+def test_gpu_sub420_partial_tiles_and_frames(cuda, impl, W, H):
+    """MCU rows of 17, 3 and 33 MCUs (partial 16-MCU tiles, a row's last block in the quirk
+    column), 3 frames in one launch, and a 2-block-row stripe pair through the device entry."""
+    import torch
+    F, q = 3, 70
+    frames = [O.gen_splitmix(300 + W + f, W, H) for f in range(F)]
+    S = jpgx.FLAG_SUBSAMPLE
+    nb = (H // 8) * (W // 8)
+    per = nb + 2 * jpgx.chroma_blocks(W, 0, H // 8, 2, S)
+    out = torch.zeros((F, per, 64), dtype=torch.int16, device=cuda)
+    fr = jpgx.frames(W, H, nframes=F, out_frame_stride=per * 64)
+    jpgx.blocks_gpu(fr, jpgx.default_params(W, H, q, 2, flags=S), _dev(np.stack(frames), cuda),
+                    out, 0)
+    got = out.cpu().numpy()
+    for f in range(F):
+        want = np.concatenate([O.blocks(frames[f], q, 2)[0],
+                               O.chroma_sub(frames[f], q, 2).reshape(-1, 64)])
+        bad = np.argwhere(got[f] != want)
+        assert len(bad) == 0, f"frame {f}: {len(bad)} mismatches, first {bad[:4].tolist()}"
 
 
 @pytest.mark.gpu
