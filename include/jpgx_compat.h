@@ -172,6 +172,17 @@ int jpgx_write_jfif_sub(const int16_t *coef, int width, int height, int quality,
 int jpgx_encode_bmp_to_jpeg_ex(const char *input, const char *output, int quality,
                                int sample_ratio, unsigned flags, int device);
 
+/* The reference's declared in-memory entry point (src/headers/jpg_encode.h:99,
+ * encode_rgb_to_jpeg(Byte *colours, output, quality, sample_ratio); declared, never defined
+ * there, and without the image size, which this one takes): interleaved top-down RGB rows
+ * `pitch` bytes apart -> the block transform on GPU `device` -> a JFIF file at `output`
+ * (truly subsampled with JPGX_FLAG_SUBSAMPLE and sample_ratio 1/2).  The x0 = -8 underflow
+ * bytes are jpgx_default_params's (those of a 54-byte-header BMP of this size).  Returns 0 or a
+ * JPGX_E* code. */
+int jpgx_encode_rgb_to_jpeg(const uint8_t *rgb, int width, int height, size_t pitch,
+                            const char *output, int quality, int sample_ratio, unsigned flags,
+                            int device);
+
 /* The reference's public entry point (src/headers/jpg_encode.h:85): BMP in, JPEG file out --
  * the block transform on GPU 0, then jpgx_write_jfif.  Returns 0 or a JPGX_E* code. */
 int jpgx_encode_bmp_to_jpeg(const char *input, const char *output, int quality,

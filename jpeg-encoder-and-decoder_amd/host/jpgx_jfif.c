@@ -280,6 +280,38 @@ int jpgx_write_jfif_sub(const int16_t *coef, int width, int height, int quality,
     return o.overflow ? JPGX_EARG : JPGX_OK;
 }
 
+int jpgx_encode_rgb_to_jpeg(const uint8_t *rgb, int width, int height, size_t pitch,
+                            const char *output, int quality, int sample_ratio, unsigned flags,
+                            int device)
+{
+    if (!rgb || !output) return JPGX_EARG;
+    jpgx_params p;
+    jpgx_default_params(&p, width, height, quality, sample_ratio);
+    p.flags = flags & JPGX_FLAG_SUBSAMPLE;
+    int rc = jpgx_validate(width, height, &p);
+    if (rc) return rc;
+    const int sub = (flags & JPGX_FLAG_SUBSAMPLE) && sample_ratio != 0;
+    const size_t nb = (size_t)(width / 8) * (height / 8);
+    const size_t nbc = jpgx_chroma_blocks(width, 0, height / 8, sample_ratio, p.flags);
+    int16_t *coef = (int16_t *)malloc((nb + 2 * nbc) * 64 * sizeof(int16_t));
+    const size_t cap = jpgx_jfif_bound(width, height);
+    uint8_t *buf = (uint8_t *)malloc(cap);
+    size_t len = 0;
+    rc = (coef && buf) ? JPGX_OK : JPGX_ENOMEM;
+    if (!rc) rc = jpgx_blocks(rgb, width, height, pitch, &p, coef, device);
+    if (!rc)
+        rc = sub ? jpgx_write_jfif_sub(coef, width, height, quality, sample_ratio, buf, cap, &len)
+                 : jpgx_write_jfif(coef, width, height, quality, buf, cap, &len);
+    if (!rc) {
+        FILE *f = fopen(output, "wb");
+        if (!f || fwrite(buf, 1, len, f) != len) rc = JPGX_EARG;
+        if (f && fclose(f)) rc = JPGX_EARG;
+    }
+    free(coef);
+    free(buf);
+    return rc;
+}
+
 int jpgx_encode_bmp_to_jpeg_ex(const char *input, const char *output, int quality,
                                int sample_ratio, unsigned flags, int device)
 {

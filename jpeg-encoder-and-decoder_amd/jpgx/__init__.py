@@ -49,6 +49,7 @@ COMPAT_EXPORTS = [
     "jpgx_fill_jpgdata", "jpgx_free_jpgdata", "jpgx_dpcm", "jpgx_dpcm_dc", "jpgx_bmp_read",
     "jpgx_free", "jpgx_encode_bmp", "jpgx_jfif_bound", "jpgx_write_jfif",
     "jpgx_encode_bmp_to_jpeg", "jpgx_write_jfif_sub", "jpgx_encode_bmp_to_jpeg_ex",
+    "jpgx_encode_rgb_to_jpeg",
 ]
 
 

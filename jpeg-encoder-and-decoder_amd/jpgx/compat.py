@@ -87,6 +87,8 @@ def _setup(L):
     L.jpgx_write_jfif.argtypes = [vp, i, i, i, vp, ctypes.c_size_t,
                                   ctypes.POINTER(ctypes.c_size_t)]
     L.jpgx_encode_bmp_to_jpeg.argtypes = [ctypes.c_char_p, ctypes.c_char_p, i, i]
+    L.jpgx_encode_rgb_to_jpeg.argtypes = [vp, i, i, ctypes.c_size_t, ctypes.c_char_p, i, i,
+                                          ctypes.c_uint, i]
 
 
 _setup(lib)
@@ -256,3 +258,14 @@ def encode_bmp_to_jpeg_ex(src: str, dst: str, quality: int, sample_ratio: int, f
 def encode_bmp_to_jpeg(src: str, dst: str, quality: int, sample_ratio: int = 0) -> None:
     _check(lib.jpgx_encode_bmp_to_jpeg(src.encode(), dst.encode(), quality, sample_ratio),
            "jpgx_encode_bmp_to_jpeg")
+
+
+def encode_rgb_to_jpeg(rgb: np.ndarray, dst: str, quality: int, sample_ratio: int = 0,
+                       flags: int = 0, device: int = 0) -> None:
+    """In-memory (H, W, 3) uint8 image -> JFIF file (jpgx_encode_rgb_to_jpeg)."""
+    if rgb.dtype != np.uint8 or rgb.ndim != 3 or rgb.strides[1:] != (3, 1):
+        raise ValueError("rgb must be (H, W, 3) uint8 with packed pixels")
+    H, W = rgb.shape[:2]
+    _check(lib.jpgx_encode_rgb_to_jpeg(rgb.ctypes.data, W, H, rgb.strides[0], dst.encode(),
+                                       quality, sample_ratio, ctypes.c_uint(flags), device),
+           "jpgx_encode_rgb_to_jpeg")

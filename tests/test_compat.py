@@ -272,3 +272,28 @@ def test_fill_jpgdata_refuses_to_leak():
     rc = C.lib.jpgx_fill_jpgdata(ctypes.byref(j), np.ascontiguousarray(coef, np.int16).ctypes.data)
     assert rc == jpgx.OK and np.array_equal(C.jpgdata_zigzag(j), coef)
     C.lib.jpgx_free_jpgdata(ctypes.byref(j))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sr,flags", [(0, 0), (1, 0), (1, jpgx.FLAG_SUBSAMPLE), (2, jpgx.FLAG_SUBSAMPLE)])
+def test_encode_rgb_to_jpeg_in_memory(tmp_path, sr, flags):
+    """jpgx_encode_rgb_to_jpeg (the reference's declared encode_rgb_to_jpeg,
+    src/headers/jpg_encode.h:99): an in-memory image, row-padded, to a JFIF file whose decoded
+    coefficients are the oracle's (4:4:4 parity output, or the true-subsampling extension)."""
+    from jfif_decode import decode
+    W, H, q = 96, 64, 80
+    big = O.gen_splitmix(61 + sr, W + 16, H)
+    rgb = big[:, :W]                                  # pitch (W + 16) * 3
+    dst = str(tmp_path / "m.jpg")
+    C.encode_rgb_to_jpeg(rgb, dst, q, sr, flags)
+    d = decode(open(dst, "rb").read())
+    img = np.ascontiguousarray(rgb)
+    if flags & jpgx.FLAG_SUBSAMPLE:
+        assert np.array_equal(d["coef"][0], O.blocks(img, q, sr)[0])
+        c = O.chroma_sub(img, q, sr)
+        assert np.array_equal(d["coef"][1], c[0]) and np.array_equal(d["coef"][2], c[1])
+    else:
+        assert np.array_equal(d["coef"].astype(np.int16), O.blocks(img, q))
+    with pytest.raises(jpgx.JpgxError) as e:
+        C.encode_rgb_to_jpeg(np.ascontiguousarray(rgb[:, :90]), dst, q)
+    assert e.value.rc == jpgx.EGEOMETRY
