@@ -185,3 +185,9 @@ def test_large_frames_hash(golden, cuda):
         for q, h in ent["coef_sha256"].items():
             out = jpgx.encode_blocks(d, int(q), underflow=ent["underflow"]).cpu().numpy()
             assert coef_sha(out) == h, (W, H, q)
+        if (W, H) == (3840, 2160):
+            # BASELINE configs[2] literally: 4K, sample_ratio 1 ("4:2:2"), q=75 -- the
+            # reference's chroma_subsample is a no-op (src/downsample.c:24-32), so its output is
+            # the 4:4:4 one (every sr1 golden above equals its sr0 hash)
+            out = jpgx.encode_blocks(d, 75, sample_ratio=1, underflow=ent["underflow"]).cpu().numpy()
+            assert coef_sha(out) == ent["coef_sha256"]["75"]
