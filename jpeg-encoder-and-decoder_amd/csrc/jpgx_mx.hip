@@ -94,9 +94,6 @@ struct MxLds {
 };
 static_assert(kSlot % 16 == 0 && kStageBytes % 16 == 0, "16-byte aligned LDS regions");
 
-#ifdef JX_MX_DBG_COUNT          /* measurement only: exact-pass calls and tasks per launch */
-__device__ unsigned long long g_mx_dbg[4];
-#endif
 __device__ mx_u4 g_mxB[3 * JX_MX_PARTS][64];     /* B operands: (part, which) x lane        */
 __device__ jx_mxtab g_mxtab[2][JX_MAXQ + 1];     /* [force][quality]                        */
 __constant__ double kMxCos[8][8] = JX_COS_INIT;
@@ -223,14 +220,6 @@ typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) void *mx_lp;
 typedef const __attribute__((address_space(1))) void *mx_gp;
 
-/* n 4-byte LDS-DMA operations of the input's first bytes into dst (timing experiments) */
-[[maybe_unused]] __device__ __forceinline__ void mx_pad_raw(const MxG &g, uint8_t *dst, int n)
-{
-    for (int i = 0; i < n; i++)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g.rgb,
-                                         (__attribute__((address_space(3))) void *)dst, 4, 0, 0);
-}
-
 /*
  * The pixels of the step starting at block b0 (position P) into `slot` ([y][24 jb + k]).
  * Simple steps: two LDS-DMA instructions of 16-byte pieces (piece p = lane, and 64 + lane for
@@ -246,12 +235,6 @@ typedef const __attribute__((address_space(1))) void *mx_gp;
 __device__ __forceinline__ void mx_issue(const MxG &g, const MxCur &P, unsigned b0, bool simple,
                                          uint32_t off0, uint32_t off1, uint8_t *slot)
 {
-#ifdef JX_MX_DBG_NOLOAD        /* timing experiments only: padding instead of the pixel DMA */
-    if (b0 != 0xffffffffu) {
-        mx_pad_raw(g, slot, 2);
-        return;
-    }
-#endif
     if (simple) {
         const uint8_t *base = P.src;
         __builtin_amdgcn_global_load_lds((mx_gp)(base + off0), (mx_lp)slot, 16, 0, 0);
@@ -354,9 +337,6 @@ __device__ __forceinline__ void mx_exact_inline(MxLds &L, const uint8_t *slot, u
 {
     const unsigned lane = mx_lane();
     mx_wave_sync();
-#ifdef JX_MX_DBG_COUNT
-    if (lane == 0) atomicAdd(&g_mx_dbg[2], 1ull);
-#endif
     for (;;) {
         const uint64_t act = __ballot(bits != 0);
         if (!act) break;
@@ -389,12 +369,6 @@ __device__ __forceinline__ void mx_flush(MxLds &L, int &nq, int &ns, const MxG &
     __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0): the tasks' blocks are stored */
     mx_wave_sync();
     const unsigned lane = mx_lane(), i = lane >> 3, x = lane & 7u;
-#ifdef JX_MX_DBG_COUNT
-    if (lane == 0) {
-        atomicAdd(&g_mx_dbg[0], 1ull);
-        atomicAdd(&g_mx_dbg[1], (unsigned long long)nq);
-    }
-#endif
     const bool live = (int)i < nq;
     const unsigned code = L.dtask[live ? i : 0u];
     const unsigned slot = code >> 8, ch = (code >> 6) & 3u, v = (code >> 3) & 7u, u = code & 7u;
@@ -486,15 +460,8 @@ __device__ __forceinline__ void mx_column(const mx_f2 (&R)[4], const mx_f2 (&W)[
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
-#ifdef JX_MX_DBG_NOSTAGE       /* timing experiments only: no zig-zag LDS writes */
-        emax += __uint_as_float((__float_as_uint(tm.x) ^ __float_as_uint(tm.y)) & 0x007fffffu);
-#else
         *(uint16_t *)(st + zo[jx_pk_k(p, 0)]) = (uint16_t)__float_as_uint(tm.x);
         *(uint16_t *)(st + zo[jx_pk_k(p, 1)]) = (uint16_t)__float_as_uint(tm.y);
-#endif
-#ifdef JX_MX_DBG_NOBAND        /* timing experiments only: no band test (NOT exact) */
-        continue;
-#endif
         const mx_f2 rr = tm - M2;
         const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
         const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
@@ -522,11 +489,6 @@ __device__ __forceinline__ uint32_t mx_flags(const mx_f2 (&F)[4], const mx_f2 (&
 /* R pairs (y, y+1) of one column from the lo (rows 0..3) and hi (rows 4..7) tiles */
 __device__ __forceinline__ void mx_combine(mx_f4 hl, mx_f4 ll, mx_f4 hh, mx_f4 lh, mx_f2 (&R)[4])
 {
-#ifdef JX_MX_DBG_NOPS          /* experiment: extra wait states between the MFMAs and their reads */
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 7\n\ts_nop 7");
-    __builtin_amdgcn_sched_barrier(0);
-#endif
     const mx_f2 s = {0x1p-12f, 0x1p-12f};
     R[0] = __builtin_elementwise_fma(mx_f2{ll.x, ll.y}, s, mx_f2{hl.x, hl.y});
     R[1] = __builtin_elementwise_fma(mx_f2{ll.z, ll.w}, s, mx_f2{hl.z, hl.w});
@@ -690,16 +652,9 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         column(2);
         (void)em;
         mx_wave_sync();
-#ifndef JX_MX_DBG_NOEXACT        /* measurement only: no exact pass (NOT bit-exact) */
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx_defer(L, sp, fl, b0, nq, ns, g, T);
-#endif
         /* stores: channel c's 8 blocks x 128 B; always three store instructions (the vmcnt
          * accounting above counts on it) */
-#ifdef JX_MX_DBG_NOSTORE       /* timing experiments only: padding instead of the stores */
-        if (b0 != 0xffffffffu) {
-            mx_pad(g, L, 3);
-        } else
-#endif
         if (mx_simple_store(P, g, b0)) {
             int16_t *ob = P.dst + lane * 8;
             const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
@@ -789,17 +744,6 @@ int mx_tables_for_current_device(int *waves)
 
 }  // namespace
 
-#ifdef JX_MX_DBG_COUNT
-/* measurement only: {exact passes, tasks, batches} since the last call (then reset) */
-extern "C" int jx_mx_dbg_read(unsigned long long out[4])
-{
-    hipDeviceSynchronize();
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mx_dbg), 4 * sizeof(unsigned long long)) != hipSuccess)
-        return JPGX_EHIP;
-    unsigned long long z[4] = {0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_mx_dbg), z, sizeof z) == hipSuccess ? JPGX_OK : JPGX_EHIP;
-}
-#endif
 
 /* k_mx over every frame of the stripe (4:4:4 / reference-parity output); no workspace. */
 extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)

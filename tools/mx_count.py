@@ -1,4 +1,7 @@
-"""Exact-pass statistics of k_mx (a -DJX_MX_DBG_COUNT build) on the bench workload."""
+"""Exact-pass statistics of k_mx (a -DJX_MX_DBG_COUNT build) on the bench workload.
+Needs the measurement hooks: git apply tools/probes/k_mx_debug_knobs.patch, then build the
+variant with -DJX_MX_DBG_COUNT (tools/build_variants.sh).
+"""
 import ctypes
 import os
 import sys
