@@ -192,3 +192,23 @@ def test_packed_transform_matches_scalar_bit_for_bit():
     f.argtypes = [ctypes.c_longlong, ctypes.c_ulonglong]
     assert f(20000, 1) == 0
     assert f(20000, 0x9E3779B97F4A7C15) == 0
+
+
+def test_product_entry_points_fail_loudly_without_a_gpu():
+    """No CPU fallback: without a GPU every compute entry point returns JPGX_ENODEV (or the HIP
+    error), never a result.  Skipped where a GPU is visible."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    import jpgx
+    rgb = np.zeros((16, 16, 3), np.uint8)
+    with pytest.raises(jpgx.JpgxError) as e:
+        jpgx.encode_blocks(rgb, 50)
+    assert e.value.rc == jpgx.ENODEV
+    with pytest.raises(jpgx.JpgxError) as e:
+        jpgx.encode_blocks_multi(rgb, 50, 1)
+    assert e.value.rc == jpgx.ENODEV
+    with pytest.raises(jpgx.JpgxError) as e:
+        jpgx.HostContext(2)
+    assert e.value.rc == jpgx.ENODEV
+    assert jpgx.device_count() == 0
