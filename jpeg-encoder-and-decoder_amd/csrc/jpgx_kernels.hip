@@ -937,7 +937,7 @@ __device__ __forceinline__ uint64_t cols_to_stage(int wch, float (&T)[8][NU], co
 #pragma unroll
         for (int v = 0; v < 8; v++) {
             wc[v] = hi ? tab.w[wch][uu + kHi][v] : tab.w[wch][uu][v];
-            lc[v] = hi ? band.lim[lch][uu + kHi][v] : band.lim[lch][uu][v];
+            lc[v] = band.lim[lch][uu][v];    /* wave-uniform: for NU = 4 the joint band */
         }
         float col[8], F[8];
 #pragma unroll
@@ -950,18 +950,11 @@ __device__ __forceinline__ uint64_t cols_to_stage(int wch, float (&T)[8][NU], co
             const unsigned zz = hi ? (unsigned)zz_of(v, uu + kHi) : (unsigned)zz_of(v, uu);
             ((uint16_t *)W.stage)[slot * 66 + zz] = (uint16_t)__float_as_uint(tm);
             uint64_t mk;
-            if (NU == 8)                     /* whole block: wave-uniform limits, in SGPRs */
-                asm("v_cmp_ge_f32_e64 %[m], |%[d]|, %[l]\n\t"
-                    "s_or_b64 %[seen], %[seen], %[m]"
-                    : [m] "=&s"(mk), [seen] "+s"(seen)
-                    : [d] "v"(d), [l] "s"(lc[v])
-                    : "scc");
-            else
-                asm("v_cmp_ge_f32_e64 %[m], |%[d]|, %[l]\n\t"
-                    "s_or_b64 %[seen], %[seen], %[m]"
-                    : [m] "=&s"(mk), [seen] "+s"(seen)
-                    : [d] "v"(d), [l] "v"(lc[v])
-                    : "scc");
+            asm("v_cmp_ge_f32_e64 %[m], |%[d]|, %[l]\n\t"
+                "s_or_b64 %[seen], %[seen], %[m]"
+                : [m] "=&s"(mk), [seen] "+s"(seen)
+                : [d] "v"(d), [l] "s"(lc[v])
+                : "scc");
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -1254,9 +1247,13 @@ int tables_for_current_device()
                     for (int u = 0; u < 8; u++)
                         for (int v = 0; v < 8; v++) {
                             /* slot 0 (luma is never averaged): the band both chroma channels
-                             * satisfy, for k_sub422's / k_sub420's mixed Cb / Cr lanes */
-                            const int k = v * 8 + u;
-                            bn.lim[ch][u][v] = ch ? lim[ch][k] : std::min(lim[1][k], lim[2][k]);
+                             * satisfy, for k_sub422's mixed Cb / Cr lanes; for 4:2:0 also both
+                             * column halves u, u ^ 4 (k_sub420's top / bottom lanes) */
+                            const int k = v * 8 + u, k2 = v * 8 + (u ^ 4);
+                            const float j = std::min(lim[1][k], lim[2][k]);
+                            bn.lim[ch][u][v] = ch ? lim[ch][k]
+                                                  : (sm == 2 ? std::min(j, std::min(lim[1][k2], lim[2][k2]))
+                                                             : j);
                             bf.lim[ch][u][v] = -1.0f;
                         }
             }
