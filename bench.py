@@ -140,7 +140,7 @@ def measured_traffic(kname):
     import glob
     sys.path.insert(0, os.path.join(REPO, "tools"))
     from pmc_summary import kernel_source_sha
-    sha = kernel_source_sha()
+    sha = kernel_source_sha(kname)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{kname}_pmc.json")),
                        reverse=True):
         with open(path) as f:

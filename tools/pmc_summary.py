@@ -16,14 +16,15 @@ from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "csrc")
-KSRCS = ("jpgx_kernels.hip", "jpgx_mx.hip", "jpgx_internal.h", "xform_math.h")
+KSRCS = {"k_mx": ("jpgx_mx.hip", "jpgx_internal.h", "xform_math.h", "jx_consts.h"),
+         "k_xform": ("jpgx_kernels.hip", "jpgx_internal.h", "xform_math.h", "jx_consts.h")}
 BYTES_PER_LAUNCH = 8 * 3840 * 2160 * 9          # bench.py workload, 9 B/px algorithmic
 
 
-def kernel_source_sha():
-    """sha256 over the device sources both 4:4:4 kernels are built from."""
+def kernel_source_sha(kernel="k_mx"):
+    """sha256 over the device sources the kernel is built from."""
     h = hashlib.sha256()
-    for name in KSRCS:
+    for name in KSRCS[kernel]:
         with open(os.path.join(CSRC, name), "rb") as f:
             h.update(f.read())
     return h.hexdigest()
@@ -60,7 +61,7 @@ def main(src, dst, kernel="k_xform"):
         if os.path.exists(f):
             for k, v in counters(f, kernel).items():
                 pmc[k] = mean(v)
-    res = {"kernel": kernel, "kernel_source_sha256": kernel_source_sha(),
+    res = {"kernel": kernel, "kernel_source_sha256": kernel_source_sha(kernel),
            "workload": "8 x 3840x2160 RGB, q=90 (bench.py)",
            "algorithmic_bytes_per_launch": BYTES_PER_LAUNCH, "pmc_mean_per_launch": pmc}
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
