@@ -297,3 +297,17 @@ def test_encode_rgb_to_jpeg_in_memory(tmp_path, sr, flags):
     with pytest.raises(jpgx.JpgxError) as e:
         C.encode_rgb_to_jpeg(np.ascontiguousarray(rgb[:, :90]), dst, q)
     assert e.value.rc == jpgx.EGEOMETRY
+
+
+@pytest.mark.gpu
+def test_config0_512_bmp_to_jpeg(golden, tmp_path):
+    """BASELINE configs[0] through the drop-in: a 512x512 BMP (the golden G frame, seed 1) ->
+    jpgx_encode_bmp_to_jpeg at q=90 (4:4:4) -> a JPEG whose decoded coefficients hash to the
+    real reference's zig_zag_* output for that BMP (tests/golden/golden.json)."""
+    from jfif_decode import decode
+    ent = next(e for e in golden["synthetic"] if (e["kind"], e["W"], e["H"]) == ("G", 512, 512))
+    src, dst = str(tmp_path / "in.bmp"), str(tmp_path / "out.jpg")
+    O.write_bmp(src, O.gen_splitmix(ent["seed"], 512, 512))
+    C.encode_bmp_to_jpeg(src, dst, 90)
+    d = decode(open(dst, "rb").read())
+    assert coef_sha(d["coef"].astype(np.int16)) == ent["coef_sha256"]["90"]
