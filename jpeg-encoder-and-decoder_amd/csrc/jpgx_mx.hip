@@ -9,7 +9,7 @@
  * JpgData.zig_zag_* arrays, [frame][Y|Cb|Cr][nb][64] int16.
  *
  * Work unit: a "step" of 8 consecutive blocks (launch-global block index, frames
- * concatenated); each wave walks a contiguous range of steps.
+ * concatenated); persistent waves take chunks of 4 steps grid-stride (mx_span_init).
  *   Input   the step's 8 pixel rows x 8 blocks x 24 B land in a 1.5-KiB LDS slot ([y][24 jb + k])
  *           by LDS-DMA (16-byte pieces), issued two steps ahead (3-slot ring).
  *   Rows    set s (blocks 4s..4s+3), half h (pixel rows 4h..4h+3): a 16 x 32 f16 A operand,
@@ -181,14 +181,20 @@ struct MxCur {
     int16_t *dst;
 };
 
+/* P's pixel and output pointers from its position */
+__device__ __forceinline__ void mx_ptrs(MxCur &P, const MxG &g)
+{
+    P.src = g.rgb + (long long)P.f * g.fstride + 8ll * P.r * g.pitch + 24ll * P.c;
+    P.dst = g.out + (long long)P.f * g.ofstride + 64ll * P.bi;
+}
+
 __device__ __forceinline__ void mx_seek(MxCur &P, const MxG &g, unsigned b0)
 {
     P.f = b0 / g.nb;
     P.bi = b0 - P.f * g.nb;
     P.r = P.bi / g.bpr;
     P.c = P.bi - P.r * g.bpr;
-    P.src = g.rgb + (long long)P.f * g.fstride + 8ll * P.r * g.pitch + 24ll * P.c;
-    P.dst = g.out + (long long)P.f * g.ofstride + 64ll * P.bi;
+    mx_ptrs(P, g);
 }
 
 /* to the next step (first block b0 + 8): pointer bumps inside a block-row, a seek otherwise */
@@ -213,6 +219,78 @@ __device__ __forceinline__ bool mx_simple_load(const MxCur &p, const MxG &g, uns
 __device__ __forceinline__ bool mx_simple_store(const MxCur &p, const MxG &g, unsigned b0)
 {
     return p.bi + 8u <= g.nb && b0 + 8u <= g.total;
+}
+
+/*
+ * Which steps a wave computes.  kChunk = 0: one contiguous range per wave, balanced to a step.
+ * kChunk = C > 0: the launch's steps cut into chunks of C; wave wv takes chunks wv, wv + nw,
+ * wv + 2 nw, ... (grid-stride over chunks), so the waves in flight stream through one window of
+ * about nw C steps of the frames at a time -- neighbouring waves read and write neighbouring
+ * bytes -- instead of each wave streaming through its own 1/nw of the batch.  From a chunk's
+ * last step to the wave's next chunk is a constant jb = 8 (nw C - C + 1) blocks, so the cursor
+ * moves there without a division.  s = nsteps once the wave is done.
+ */
+#ifndef JX_MX_CHUNK
+#define JX_MX_CHUNK 4
+#endif
+constexpr unsigned kChunk = JX_MX_CHUNK;
+struct MxSpan {
+    unsigned s, end;
+};
+struct MxJump {
+    unsigned nwC, jb, jr, jc, rows;     /* nw C; jb blocks = jr block-rows + jc blocks; rows/frame */
+};
+
+__device__ __forceinline__ void mx_span_init(MxSpan &R, MxJump &J, const MxG &g, unsigned nsteps,
+                                             unsigned nw, unsigned wv)
+{
+    if (kChunk == 0) {
+        R.s = (unsigned)(((unsigned long long)nsteps * wv) / nw);
+        R.end = (unsigned)(((unsigned long long)nsteps * (wv + 1)) / nw);
+        if (R.s >= R.end) R.s = R.end = nsteps;
+        J = MxJump{0u, 0u, 0u, 0u, 0u};
+        return;
+    }
+    R.s = wv * kChunk;
+    R.end = std::min(R.s + kChunk, nsteps);
+    if (R.s >= nsteps) R.s = R.end = nsteps;
+    J.nwC = nw * kChunk;
+    J.jb = 8u * (J.nwC - kChunk + 1u);
+    J.jr = J.jb / g.bpr;
+    J.jc = J.jb - J.jr * g.bpr;
+    J.rows = g.nb / g.bpr;
+}
+
+/* to the wave's next step, and the cursor with it */
+__device__ __forceinline__ void mx_step(MxSpan &R, MxCur &P, const MxG &g, unsigned nsteps,
+                                        const MxJump &J)
+{
+    if (R.s + 1u < R.end) {
+        mx_next(P, g, 8u * R.s);
+        R.s++;
+        return;
+    }
+    const unsigned ns = R.s + J.jb / 8u;
+    if (kChunk == 0 || R.end >= nsteps || ns >= nsteps) {
+        R.s = nsteps;
+        return;
+    }
+    /* P is at step R.s (a chunk's last): move it jb blocks on */
+    P.bi += J.jb;
+    P.c += J.jc;
+    P.r += J.jr;
+    if (P.c >= g.bpr) {
+        P.c -= g.bpr;
+        P.r++;
+    }
+    while (P.bi >= g.nb) {
+        P.bi -= g.nb;
+        P.r -= J.rows;
+        P.f++;
+    }
+    mx_ptrs(P, g);
+    R.s = ns;
+    R.end = std::min(ns + kChunk, nsteps);
 }
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -519,9 +597,10 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     const unsigned nsteps = (g.total + 7u) / 8u;
     const unsigned nw = gridDim.x * 4u;
     const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    const unsigned s_end = (unsigned)(((unsigned long long)nsteps * (wv + 1)) / nw);
-    unsigned s = (unsigned)(((unsigned long long)nsteps * wv) / nw);
-    if (s >= s_end) return;
+    MxSpan RC;                                     /* the step being computed */
+    MxJump J;
+    mx_span_init(RC, J, g, nsteps, nw, wv);
+    if (RC.s >= nsteps) return;
 
     /* A operand of this lane: row m = lane & 15 (block m >> 2 of the set, pixel row m & 3 of the
      * half), k-group q = lane >> 4 (bytes 8q..8q+7; q = 3: the bias) */
@@ -559,22 +638,23 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         for (int w = 0; w < 3; w++) B[p][w] = g_mxB[3 * p + w][lane];
 
     MxCur P;
-    mx_seek(P, g, 8u * s);
+    mx_seek(P, g, 8u * RC.s);
     /* prologue: the first kDist steps' DMA (ring slots 0..kDist-1), each followed by three
-     * padding operations in place of the stores of the (absent) steps before s */
+     * padding operations in place of the stores of the (absent) steps before the first */
     MxCur PN = P;                                  /* position of the next step to issue */
+    MxSpan RN = RC;
 #pragma unroll
     for (int k = 0; k < (int)kDist; k++) {
-        const unsigned sn = s + (unsigned)k;
-        if (sn < s_end) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[k]);
+        const unsigned sn = RN.s;
+        if (sn < nsteps) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[k]);
         else mx_pad(g, L, 2);
         mx_pad(g, L, 3);
-        mx_next(PN, g, 8u * sn);
+        mx_step(RN, PN, g, nsteps, J);
     }
     unsigned slot = 0;
     int nq = 0, ns = 0;                            /* deferred exact tasks, their blocks */
-    for (; s < s_end; s++) {
-        const unsigned b0 = 8u * s;
+    while (RC.s < nsteps) {
+        const unsigned b0 = 8u * RC.s;
         /* this step's DMA: younger VMEM operations are the next step's 2 pieces and the last
          * two steps' 3 stores each (vmcnt counts loads, LDS-DMA and stores in issue order) */
         /* VMEM operations younger than this step's DMA, in issue order: the three stores of each
@@ -586,10 +666,10 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         uint8_t *const sp = L.ring[slot];
         /* the step after next: its DMA into the slot step s-1 used */
         {
-            const unsigned sn = s + kDist, nslot = slot == 0 ? kRing - 1u : slot - 1u;
-            if (sn < s_end) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[nslot]);
+            const unsigned sn = RN.s, nslot = slot == 0 ? kRing - 1u : slot - 1u;
+            if (sn < nsteps) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[nslot]);
             else mx_pad(g, L, 2);
-            mx_next(PN, g, 8u * sn);
+            mx_step(RN, PN, g, nsteps, J);
         }
         /* A operands: set 0/1 x half lo/hi */
         const mx_u2 d00 = *(const mx_u2 *)(sp + aoff);
@@ -679,7 +759,7 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             }
         }
         mx_wave_sync();
-        mx_next(P, g, b0);
+        mx_step(RC, P, g, nsteps, J);
         slot = slot == kRing - 1u ? 0u : slot + 1u;
     }
     if (nq) mx_flush(L, nq, ns, g, T);
