@@ -15,6 +15,8 @@ for r in $(seq 1 "${REPS:-2}"); do
     JPGX_LIB=$lib timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} \
       > "$OUT/bench_${n}_$r.json" 2> "$OUT/bench_${n}_$r.err"; rc=$?
     echo "bench $n rep $r rc=$rc $(summ $OUT/bench_${n}_$r.json)"
+    # rc 3 = output differs from the goldens (accepted for timing-only builds with ALLOW_WRONG=1)
+    if [ $rc -eq 3 ] && [ "${ALLOW_WRONG:-0}" = "1" ]; then continue; fi
     [ $rc -eq 0 ] || { tail -5 "$OUT/bench_${n}_$r.err"; exit $rc; }
   done
 done
