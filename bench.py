@@ -10,9 +10,10 @@ Workload (BASELINE.json metric "Mpixels/sec RGB->quantised-coeff, 4K 4:4:4 q=90"
   exact path recomputes the guard-band coefficients).
   8 frames per GPU = 597 MB moved per step, more than the 256 MiB Infinity Cache.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
-(one process per GPU, RCCL only for the barrier and the max-time reduction: the stripes need
-no data exchange).  Rank 0 prints ONE JSON line.
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 one process per GPU, either
+under the driver's torch.distributed.run or started by bench.py itself (a child
+torch.distributed.run) when WORLD_SIZE is unset; RCCL carries only the barrier and the max-time
+reduction (the stripes need no data exchange).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -227,6 +228,31 @@ def sub_kernel_name(sr):
     return "k_sub422" if sr == 1 else "k_sub420"
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` (N > 1) started without torch.distributed.run: start the N ranks
+    here, one process per GPU, as a child torch.distributed.run (never an exec), before this
+    process makes any GPU call; its exit code is ours.  Refused when the node has fewer GPUs than
+    N, unless JPGX_BENCH_BACKEND=gloo asks for the rehearsal with ranks sharing the GPUs."""
+    import socket
+    import subprocess
+
+    import torch
+    ndev = torch.cuda.device_count()          # counts devices without initialising the GPU
+    rehearsal = os.environ.get("JPGX_BENCH_BACKEND") == "gloo"
+    if n > ndev and not rehearsal:
+        log(f"bench: --gpus {n} but this node has {ndev} GPU(s)")
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"bench: starting {n} ranks: {' '.join(cmd[2:])}")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -253,6 +279,10 @@ def main():
                     help="true 4:2:2 / 4:2:0 chroma (JPGX_FLAG_SUBSAMPLE, an extension; needs "
                          "--sample-ratio 1 or 2): not the headline metric")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     if args.kernel:
         os.environ["JPGX_KERNEL"] = args.kernel
     kname = "k_xform" if os.environ.get("JPGX_KERNEL") == "xform" else "k_mx"
@@ -263,6 +293,8 @@ def main():
     import jpgx
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU over RCCL ("nccl").  JPGX_BENCH_BACKEND=gloo (with ranks placed on

@@ -134,11 +134,27 @@ int shard_reserve(Shard &s, size_t in_bytes, size_t out_bytes, bool staged)
         s.cap_in = in_bytes;
         s.cap_out = out_bytes;
     }
-    if (staged && !s.h_in[0]) {
-        for (int b = 0; b < 2; b++) {
-            if (hipHostMalloc(&s.h_in[b], s.cap_in, hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc(&s.h_out[b], s.cap_out, hipHostMallocDefault) != hipSuccess)
-                return JPGX_EHIP;
+    if (staged && !(s.h_in[0] && s.h_in[1] && s.h_out[0] && s.h_out[1])) {
+        bool ok = true;
+        for (int b = 0; b < 2 && ok; b++) {
+            if (!s.h_in[b] && hipHostMalloc(&s.h_in[b], s.cap_in, hipHostMallocDefault) != hipSuccess) {
+                s.h_in[b] = nullptr;
+                ok = false;
+            }
+            if (ok && !s.h_out[b] && hipHostMalloc(&s.h_out[b], s.cap_out, hipHostMallocDefault) != hipSuccess) {
+                s.h_out[b] = nullptr;
+                ok = false;
+            }
+        }
+        if (!ok) {
+            /* never leave a partial set behind: the next call re-allocates all four */
+            for (int b = 0; b < 2; b++) {
+                (void)hipHostFree(s.h_in[b]);
+                (void)hipHostFree(s.h_out[b]);
+                s.h_in[b] = nullptr;
+                s.h_out[b] = nullptr;
+            }
+            return JPGX_EHIP;
         }
     }
     return JPGX_OK;

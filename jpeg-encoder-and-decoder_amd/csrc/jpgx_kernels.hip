@@ -1317,21 +1317,6 @@ bool sub420_two_pass()
 
 extern "C" {
 
-size_t jpgx_chroma_blocks(int width, int row_begin, int row_end, int sample_ratio, unsigned flags)
-{
-    if (width <= 0 || row_end < row_begin) return 0;
-    const size_t rows = (size_t)(row_end - row_begin);
-    if (!(flags & JPGX_FLAG_SUBSAMPLE) || sample_ratio == 0) return rows * (size_t)(width / 8);
-    return (sample_ratio == 2 ? rows / 2 : rows) * (size_t)(width / 16);
-}
-
-size_t jpgx_workspace_size(const jpgx_frames *fr)
-{
-    /* both 4:4:4 kernels and k_chroma keep their exact-pass queues in LDS */
-    (void)fr;
-    return 0;
-}
-
 int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
                     int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream)
 {

@@ -467,6 +467,15 @@ __device__ __forceinline__ void mx_defer(MxLds &L, const uint8_t *sp, uint32_t b
                                          int &nq, int &ns, const MxG &g, const jx_mxtab &T)
 {
     const unsigned lane = mx_lane();
+    /* a launch's last step fills its missing blocks with copies of the last block (mx_issue
+     * clamps): their flags are dropped here, the copies are never stored, and the real last
+     * block carries the same tasks */
+    if (b0 + 8u > g.total) {
+        const unsigned nvalid = g.total - b0;
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            if (mx_col_block((unsigned)k, lane) >= nvalid) bits &= ~(0xffu << (8 * k));
+    }
     /* flagged blocks of the step, and the task count */
     const uint64_t m0 = __ballot((bits & 0xffu) != 0), m1 = __ballot((bits & 0xff00u) != 0),
                    m2 = __ballot((bits & 0xff0000u) != 0);
@@ -744,8 +753,9 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
                 __builtin_nontemporal_store(val, (mx_u4 *)(ob + (long long)c * g.nb * 64));
             }
         } else {
-            /* lanes past the end rewrite the last block's chunk with its own bytes (the clamped
-             * blocks computed the last block) */
+            /* lanes past the launch's end (the clamped copies of the last block) store nothing;
+             * block b0 is always in range, so each store instruction still issues (the vmcnt
+             * accounting counts three per step) */
             const unsigned l = mx_lane();
             const unsigned bl = b0 + (l >> 3), b = bl < g.total ? bl : g.total - 1u;
             const unsigned f = b / g.nb, bi = b - f * g.nb;
@@ -753,9 +763,10 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
 #pragma unroll
             for (int c = 0; c < 3; c++) {
                 const mx_u4 val = *(const mx_u4 *)(L.stage + mx_sb((unsigned)c) + ro);
-                __builtin_nontemporal_store(
-                    val, (mx_u4 *)(g.out + (long long)f * g.ofstride +
-                                   ((long long)c * g.nb + bi) * 64 + (l & 7u) * 8));
+                if (bl < g.total)
+                    __builtin_nontemporal_store(
+                        val, (mx_u4 *)(g.out + (long long)f * g.ofstride +
+                                       ((long long)c * g.nb + bi) * 64 + (l & 7u) * 8));
             }
         }
         mx_wave_sync();
@@ -833,7 +844,11 @@ extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)
     if (rc) return rc;
     const size_t total = (size_t)xa->g.nb * (size_t)xa->g.nframes;
     const size_t nsteps = (total + 7) / 8;
-    const size_t w = std::min<size_t>(nsteps, (size_t)std::max(waves, 4));
+#ifndef JX_MX_NP
+#define JX_MX_NP 0
+#endif
+    const size_t w = JX_MX_NP ? (nsteps + JX_MX_NP - 1) / JX_MX_NP
+                              : std::min<size_t>(nsteps, (size_t)std::max(waves, 4));
     const unsigned grid = (unsigned)((w + 3) / 4);
     hipLaunchKernelGGL(k_mx, dim3(grid), dim3(256), 0, (hipStream_t)stream, *xa);
     return mx_rc(hipGetLastError());

@@ -239,6 +239,21 @@ void jpgx_stripe(int block_rows, int nshards, int k, int *row_begin, int *row_en
 
 const char *jpgx_version(void) { return "jpgx 0.1 (gfx950)"; }
 
+size_t jpgx_chroma_blocks(int width, int row_begin, int row_end, int sample_ratio, unsigned flags)
+{
+    if (width <= 0 || row_end < row_begin) return 0;
+    const size_t rows = (size_t)(row_end - row_begin);
+    if (!(flags & JPGX_FLAG_SUBSAMPLE) || sample_ratio == 0) return rows * (size_t)(width / 8);
+    return (sample_ratio == 2 ? rows / 2 : rows) * (size_t)(width / 16);
+}
+
+size_t jpgx_workspace_size(const jpgx_frames *fr)
+{
+    /* every kernel keeps its exact-pass queues in LDS */
+    (void)fr;
+    return 0;
+}
+
 }  /* extern "C" */
 
 /* ---- packed-pair equivalence (host) --------------------------------------------------------

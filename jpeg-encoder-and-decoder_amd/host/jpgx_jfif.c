@@ -287,10 +287,12 @@ int jpgx_encode_rgb_to_jpeg(const uint8_t *rgb, int width, int height, size_t pi
     if (!rgb || !output) return JPGX_EARG;
     jpgx_params p;
     jpgx_default_params(&p, width, height, quality, sample_ratio);
-    p.flags = flags & JPGX_FLAG_SUBSAMPLE;
+    /* true subsampling needs a ratio; with sample_ratio 0 the flag means plain 4:4:4 (as in
+     * jpgx_encode_bmp_to_jpeg_ex) */
+    const int sub = (flags & JPGX_FLAG_SUBSAMPLE) && sample_ratio != 0;
+    p.flags = sub ? JPGX_FLAG_SUBSAMPLE : 0u;
     int rc = jpgx_validate(width, height, &p);
     if (rc) return rc;
-    const int sub = (flags & JPGX_FLAG_SUBSAMPLE) && sample_ratio != 0;
     const size_t nb = (size_t)(width / 8) * (height / 8);
     const size_t nbc = jpgx_chroma_blocks(width, 0, height / 8, sample_ratio, p.flags);
     int16_t *coef = (int16_t *)malloc((nb + 2 * nbc) * 64 * sizeof(int16_t));

@@ -102,7 +102,8 @@ int jpgx_bmp_read(const char *path, uint8_t **rgb, int *width, int *height, size
     /* the reference reads 3 bytes per pixel at a row stride of W*(bpp/8): only 24-bit
      * files are meaningful; rows are taken backwards from the end of the file
      * (bitmap.c:127-137) and must lie inside it */
-    if (bpp != 24 || w <= 0 || h <= 0 || (long long)w * h * 3 > (long long)fs) {
+    /* W*H*3 <= fs, tested without forming a product that can overflow (hostile headers) */
+    if (bpp != 24 || w <= 0 || h <= 0 || (long long)w > fs / 3 || (long long)h > fs / 3 / w) {
         free(buf);
         return JPGX_EARG;
     }

@@ -329,6 +329,8 @@ class HostContext:
         if rgb.dtype != np.uint8 or rgb.ndim != 3 or rgb.shape[2] != 3 or rgb.strides[1:] != (3, 1):
             raise ValueError("rgb must be (H, W, 3) uint8 with packed pixels")
         H, W = rgb.shape[:2]
+        if rgb.strides[0] < 3 * W:                # flipped or overlapping rows: not a pitch
+            raise ValueError("rgb rows must be laid out top-down with a pitch >= 3 * width")
         p = default_params(W, H, quality, sample_ratio, underflow, flags)
         nb = (H // 8) * (W // 8)
         nbc = chroma_blocks(W, 0, H // 8, sample_ratio, flags)

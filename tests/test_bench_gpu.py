@@ -1,6 +1,6 @@
 """bench.py itself on the GPU: the N=1 line (contract keys, roofline, its own output check
 against the golden hashes) and the N>1 path rehearsed with two ranks on the box's one GPU
-(torch.distributed.run, gloo collectives: the stripes, per-rank seeds, barrier, max-over-ranks
+(`bench.py --gpus 2` starts them itself; gloo collectives: the stripes, per-rank seeds, barrier, max-over-ranks
 timing and the cross-rank output check all run; RCCL needs one GPU per rank)."""
 import json
 import os
@@ -33,10 +33,10 @@ def test_bench_single_gpu_line():
 
 
 def test_bench_two_ranks_rehearsal():
-    env = dict(os.environ, JPGX_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
-                        "29517", "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
+    """`bench.py --gpus 2` started directly: it launches its two ranks itself."""
+    env = dict(os.environ, JPGX_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
                         "--frames-per-gpu", "2"], cwd=REPO, env=env, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -44,3 +44,12 @@ def test_bench_two_ranks_rehearsal():
     assert d["n_gpus"] == 2 and d["config"]["global_batch_frames"] == 4
     assert d["cpu_baseline"] is None
     assert d["output_check"]["ok"] and "all stripes" in d["output_check"]["against"]
+
+
+def test_bench_refuses_more_gpus_than_the_node_has():
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("JPGX_BENCH_BACKEND", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "64", "--steps", "1"], cwd=REPO,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -93,6 +93,27 @@ def test_tie_frame_every_dc_is_a_tie(cuda):
     assert np.array_equal(_gpu(rgb, 50, cuda), O.blocks(rgb, 50))
 
 
+@pytest.mark.parametrize("W,F", [(8, 1), (24, 1), (520, 1), (24, 3), (40, 5)])
+def test_tail_step_guard_region(cuda, W, F):
+    """Launches whose block count is not a multiple of 8 (the last step's missing blocks are
+    clamped copies of the last one) on tie frames (flagged DCs, so the exact pass runs on the
+    last step): the output equals the oracle and a sentinel region after it stays untouched."""
+    import torch
+    H, q = 8, 50
+    frames = [O.gen_tie(W, H) for _ in range(F)]
+    nb = (H // 8) * (W // 8)
+    guard = 4096
+    buf = torch.full((F * 3 * nb * 64 + guard,), 0x7A7A, dtype=torch.int16, device=cuda)
+    fr = jpgx.frames(W, H, nframes=F)
+    ws = torch.empty(max(jpgx.workspace_size(fr), 1), dtype=torch.uint8, device=cuda)
+    jpgx.blocks_gpu(fr, jpgx.default_params(W, H, q), _dev(np.stack(frames), cuda), buf, ws)
+    got = buf.cpu().numpy()
+    assert (got[F * 3 * nb * 64:] == 0x7A7A).all(), "write past the end of the output"
+    for f in range(F):
+        assert np.array_equal(got[f * 3 * nb * 64:(f + 1) * 3 * nb * 64].reshape(3, nb, 64),
+                              O.blocks(frames[f], q)), f
+
+
 def test_batch_and_stripes(cuda):
     """A batch of frames in one launch, and block-row stripes with the one-row halo, give the
     same output as frame-by-frame whole images."""

@@ -1,0 +1,302 @@
+// membench3.hip -- the memory skeleton of k_mx with synthetic compute (not product code).
+// 8 x 4K frames, fresh input (two input sets alternating launch by launch), 9 B/px.
+// Per wave-step (8 blocks): 2 LDS-DMA pieces of the step's 8 pixel rows x 192 B issued DIST
+// steps ahead into a ring, one constant vmcnt wait, NV synthetic VALU instructions (v_pk_fma
+// chains), NM MFMAs, NL ds_write_b16 to a stage, then 3 x (ds_read_b128 + 1 KiB nt store) to the
+// Y/Cb/Cr planes.  Chunks of CH steps come from a static grid-stride (QM 0), one atomic counter
+// (QM 1), or static rounds then the counter (QM 3).  Occupancy is pinned by dynamic LDS.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/membench3.hip -o tools/membench3
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+constexpr unsigned kW = 3840, kH = 2160, kPitch = kW * 3;
+constexpr unsigned kStepsPerRow = kW / 64;                 /* 60 */
+constexpr unsigned kNb = (kW / 8) * (kH / 8);               /* blocks per frame */
+constexpr unsigned kStepsPerFrame = kNb / 8;
+constexpr unsigned kSlot = 1536, kStage = 3 * 1152;
+
+typedef __attribute__((address_space(3))) void *lp;
+typedef const __attribute__((address_space(1))) void *gp;
+
+struct Args {
+    const uint8_t *in;
+    int16_t *out;
+    unsigned nsteps;
+    unsigned *ctr;                 /* dynamic queue counter, monotonically increasing         */
+    unsigned base;                 /* this launch's first counter value                       */
+    unsigned long long *ts;        /* per-wave {start, end} s_memrealtime, or null            */
+    unsigned nstatic;              /* QM 3: chunks handed out statically before the queue     */
+};
+
+template <int DIST>
+__device__ __forceinline__ constexpr int wait_imm()
+{
+    return (int)(((5 * DIST - 2) & 15) | (((5 * DIST - 2) >> 4) << 14) | 0xF70);
+}
+
+/* the chunk source; fetch() starts a request whose value take() returns later */
+template <int QM>
+struct Q {
+    unsigned nw, wv, round, pend;
+    __device__ __forceinline__ void fetch(const Args &a)
+    {
+        if (QM == 0) { pend = wv + nw * (round++); return; }
+        if (QM == 3) {
+            const unsigned k = wv + nw * round;
+            if (k < a.nstatic) { round++; pend = k; return; }
+        }
+        unsigned v = 0xffffffffu;
+        if ((threadIdx.x & 63u) == 0) v = atomicAdd(a.ctr, 1u) - a.base + (QM == 3 ? a.nstatic : 0u);
+        pend = v;                                  /* a VGPR; read (and waited for) in take() */
+    }
+    __device__ __forceinline__ unsigned take() { return __builtin_amdgcn_readfirstlane(pend); }
+};
+
+template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM>
+__global__ __launch_bounds__(256) void k_skel(Args a)
+{
+    static_assert(CH > DIST, "the issue cursor is at most one chunk ahead");
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    const unsigned lane = threadIdx.x & 63u;
+    uint8_t *ring = dyn + (threadIdx.x >> 6) * ((DIST + 1) * kSlot + kStage + 256);
+    uint8_t *stage = ring + (DIST + 1) * kSlot;
+    uint8_t *dummy = stage + kStage;
+    const unsigned nw = gridDim.x * 4u;
+    const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned nchunks = a.nsteps / CH;
+    Q<QM> q{nw, wv, 0, 0};
+    q.fetch(a);
+    unsigned cc = q.take();                        /* compute chunk */
+    if (cc >= nchunks) {
+        if (a.ts && lane == 0) { a.ts[2 * wv] = t0; a.ts[2 * wv + 1] = t0; }
+        return;
+    }
+    q.fetch(a);                                    /* the chunk after: taken when the issue cursor gets there */
+    unsigned ic = cc, ik = 0;                      /* issue cursor: chunk, step in it */
+    unsigned ck = 0;                               /* compute step in cc */
+    const uint32_t off0 = (lane / 12u) * kPitch + 16u * (lane % 12u);
+    const uint32_t off1 = ((64u + lane) / 12u) * kPitch + 16u * ((64u + lane) % 12u);
+    auto issue = [&](uint8_t *slot) {
+        if (ic < nchunks) {
+            const unsigned s = ic * CH + ik;
+            const uint8_t *b = a.in + (size_t)(s / kStepsPerRow) * 8 * kPitch + (s % kStepsPerRow) * 192u;
+            __builtin_amdgcn_global_load_lds((gp)(b + off0), (lp)slot, 16, 0, 0);
+            if (lane < 32) __builtin_amdgcn_global_load_lds((gp)(b + off1), (lp)(slot + 1024), 16, 0, 0);
+        } else {
+            __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
+        }
+        if (ic < nchunks && ++ik == CH) {
+            ik = 0;
+            ic = q.take();
+            if (ic < nchunks) q.fetch(a);
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < DIST; k++) {
+        issue(ring + k * kSlot);
+        for (int i = 0; i < 3; i++) __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
+    }
+    f2 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc[i] = f2{(float)lane, (float)i};
+    const f2 k1 = {1.0001f, 0.9999f}, k2 = {0.5f, 0.25f};
+    f4 macc[4] = {};
+    unsigned slot = 0;
+    for (;;) {
+        const unsigned sc = cc * CH + ck;
+        __builtin_amdgcn_s_waitcnt(wait_imm<DIST>());
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        uint8_t *sp = ring + slot * kSlot;
+        issue(ring + (slot == 0 ? DIST : slot - 1) * kSlot);
+        const u4 d = *(const u4 *)(sp + (lane % 96) * 16);
+        acc[0].x += __uint_as_float(d.x & 0x3fffffffu);
+        acc[1].x += __uint_as_float(d.y & 0x3fffffffu);
+        h8 av = __builtin_bit_cast(h8, d);
+#pragma unroll
+        for (int i = 0; i < NM; i++)
+            macc[i & 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, av, macc[i & 3], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < NV; i++)
+            asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(acc[i & 7]) : "v"(k1), "v"(k2));
+        if (NM) acc[2].x += macc[0].x + macc[1].y + macc[2].z + macc[3].w;
+#pragma unroll
+        for (int i = 0; i < NL; i++)
+            *(uint16_t *)(stage + (i % 3) * 1152 + ((lane * 37u + (unsigned)i * 131u) & 511u) * 2u) =
+                (uint16_t)__float_as_uint(acc[i & 7].x);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        const unsigned f = sc / kStepsPerFrame, bi = (sc - f * kStepsPerFrame) * 8u;
+        int16_t *ob = a.out + (size_t)f * 3 * kNb * 64 + (size_t)bi * 64 + lane * 8;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            u4 v = *(const u4 *)(stage + c * 1152 + lane * 16);
+            if (NL == 0) v.x ^= __float_as_uint(acc[c].x + acc[c + 3].y);
+            if (NT) __builtin_nontemporal_store(v, (u4 *)(ob + (size_t)c * kNb * 64));
+            else *(u4 *)(ob + (size_t)c * kNb * 64) = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        slot = slot == DIST ? 0 : slot + 1;
+        if (++ck == CH) {
+            ck = 0;
+            cc = ic;                                /* the issue cursor is already in the next chunk */
+            if (cc >= nchunks) break;
+        }
+    }
+    if (acc[5].y == 3.0f) a.out[0] = 1;
+    if (a.ts && lane == 0) {
+        a.ts[2 * wv] = t0;
+        a.ts[2 * wv + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void k_ideal(const u4 *__restrict__ in, u4 *__restrict__ out, size_t n)
+{
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const u4 v = in[i];
+        const u4 x = v * 3u, y = v ^ 0x5a5a5a5au;
+        if (NT) {
+            __builtin_nontemporal_store(x, out + i);
+            __builtin_nontemporal_store(y, out + n + i);
+        } else {
+            out[i] = x;
+            out[n + i] = y;
+        }
+    }
+}
+
+static uint8_t *g_in[2];
+static int16_t *g_out;
+static unsigned *g_ctr;
+static unsigned long long *g_ts;
+static int g_cus;
+static hipEvent_t e0, e1;
+
+template <class L>
+static void timeit(const char *name, L launch)
+{
+    int which = 0;
+    for (int i = 0; i < 300; i++) launch(g_in[(which++) & 1], false);
+    CK(hipDeviceSynchronize());
+    std::vector<float> v;
+    for (int r = 0; r < 5; r++) {
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < 20; i++) launch(g_in[(which++) & 1], false);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        v.push_back(ms * 1e3f / 20);
+    }
+    std::sort(v.begin(), v.end());
+    const double bytes = 8.0 * kW * kH * 9;
+    printf("%-44s min %7.1f us  med %7.1f us  frac(min) %.3f", name, v[0], v[2], bytes / (v[0] * 1e-6) / 8e12);
+    /* one more launch with per-wave timestamps: spread of wave end times */
+    launch(g_in[(which++) & 1], true);
+    CK(hipDeviceSynchronize());
+    printf("\n");
+    fflush(stdout);
+}
+
+static unsigned g_ctr_val = 0;
+
+template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM>
+static void skel(int wpe, int grid_mult = 1, double static_frac = 0.0)
+{
+    char name[128];
+    snprintf(name, sizeof name, "skel v%d m%d l%d c%d d%d nt%d q%d w%d g%d sf%.2f", NV, NM, NL, CH, DIST, NT, QM,
+             wpe, grid_mult, static_frac);
+    const size_t per_wg = 4 * ((DIST + 1) * kSlot + kStage + 256);
+    const size_t lds = std::max(per_wg, (size_t)(160 * 1024 / wpe) & ~(size_t)15);
+    auto kern = k_skel<NV, NM, NL, CH, DIST, NT, QM>;
+    CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const unsigned nsteps = 8 * kStepsPerFrame, nchunks = nsteps / CH;
+    unsigned grid = g_cus * wpe * grid_mult;
+    if (grid_mult == 0) grid = (nchunks + 3) / 4;  /* non-persistent: one chunk per wave */
+    const unsigned nw = grid * 4;
+    const unsigned nstatic = (unsigned)(static_frac * nchunks) / nw * nw;
+    std::vector<unsigned long long> ts(2 * nw);
+    timeit(name, [&](uint8_t *in, bool stamp) {
+        if (stamp) CK(hipMemset(g_ts, 0, 2 * nw * sizeof(unsigned long long)));
+        Args a{in, g_out, nsteps, g_ctr, g_ctr_val, stamp ? g_ts : nullptr, nstatic};
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, 0, a);
+        /* every wave ends with one failing dequeue: the counter moves by the dynamic chunks + nw */
+        if (QM != 0) g_ctr_val += (nchunks - nstatic) + nw;
+        if (stamp) {
+            CK(hipMemcpy(ts.data(), g_ts, ts.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long mn = ~0ull;
+            std::vector<double> ends;
+            for (unsigned w = 0; w < nw; w++)
+                if (ts[2 * w]) mn = std::min(mn, ts[2 * w]);
+            for (unsigned w = 0; w < nw; w++)
+                if (ts[2 * w]) ends.push_back((ts[2 * w + 1] - mn) * 0.01);
+            std::sort(ends.begin(), ends.end());
+            const size_t m = ends.size();
+            printf("  | wave ends us: p1 %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f", ends[m / 100], ends[m / 10],
+                   ends[m / 2], ends[m * 9 / 10], ends[m - 1]);
+        }
+    });
+}
+
+int main(int argc, char **argv)
+{
+    const char *which = argc > 1 ? argv[1] : "all";
+    const size_t in_bytes = 8ull * kW * kH * 3;
+    CK(hipMalloc(&g_in[0], in_bytes + 4096));
+    CK(hipMalloc(&g_in[1], in_bytes + 4096));
+    CK(hipMalloc(&g_out, 2 * in_bytes));
+    CK(hipMalloc(&g_ctr, 256));
+    CK(hipMalloc(&g_ts, 2 * 1024 * 1024 * sizeof(unsigned long long)));
+    CK(hipMemset(g_ctr, 0, 256));
+    CK(hipMemset(g_in[0], 7, in_bytes));
+    CK(hipMemset(g_in[1], 9, in_bytes));
+    CK(hipMemset(g_out, 0, 2 * in_bytes));
+    CK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, 0));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const size_t n = in_bytes / 16;
+    timeit("ideal_np_nt", [&](uint8_t *in, bool) {
+        hipLaunchKernelGGL(k_ideal<1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, (const u4 *)in, (u4 *)g_out, n);
+    });
+    if (!strcmp(which, "all") || !strcmp(which, "a")) {
+        skel<0, 0, 0, 4, 2, 1, 0>(3);
+        skel<0, 0, 0, 4, 2, 1, 0>(3, 0);
+        skel<0, 0, 0, 4, 2, 1, 1>(3);
+        skel<0, 0, 0, 8, 2, 1, 1>(3);
+        skel<0, 0, 0, 16, 2, 1, 1>(3);
+        skel<0, 0, 0, 4, 2, 1, 3>(3, 1, 0.8);
+        skel<0, 0, 0, 4, 2, 1, 3>(3, 1, 0.5);
+        skel<0, 0, 0, 4, 2, 1, 1>(4);
+        skel<0, 0, 0, 8, 2, 1, 1>(4);
+    }
+    if (!strcmp(which, "all") || !strcmp(which, "b")) {
+        skel<192, 16, 24, 4, 2, 1, 0>(3);
+        skel<192, 16, 24, 4, 2, 1, 1>(3);
+        skel<192, 16, 24, 8, 2, 1, 1>(3);
+        skel<192, 16, 24, 4, 2, 1, 3>(3, 1, 0.8);
+        skel<128, 16, 24, 4, 2, 1, 0>(3);
+        skel<128, 16, 24, 4, 2, 1, 1>(3);
+        skel<128, 16, 24, 4, 2, 1, 1>(4);
+        skel<256, 16, 24, 4, 2, 1, 0>(3);
+        skel<256, 16, 24, 4, 2, 1, 1>(3);
+        skel<256, 16, 24, 8, 2, 1, 1>(3);
+        skel<256, 16, 24, 8, 2, 1, 1>(4);
+    }
+    return 0;
+}
