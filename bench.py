@@ -221,9 +221,17 @@ def check_output(d_out, plan, W, H, q, subsample, world, device, jpgx):
             "against": "tests/golden/big_golden.json batch64_4k_q90 (frame 0, all stripes)"}
 
 
+ALT_LIB = os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "lib", "libjpgx_alt.so")
+
+
+def alt_selected():
+    """--kernel xform: the test-only cross-check library (k_xform / two-pass 4:2:x)"""
+    return os.path.abspath(os.environ.get("JPGX_LIB", "")) == ALT_LIB
+
+
 def sub_kernel_name(sr):
     """The kernels a true-subsampling launch runs (jpgx_blocks_gpu's dispatch)."""
-    if os.environ.get("JPGX_SUB422" if sr == 1 else "JPGX_SUB420") == "two-pass":
+    if alt_selected():
         return f"k_xform(Y)+k_chroma<{sr}>"
     return "k_sub422" if sr == 1 else "k_sub420"
 
@@ -273,8 +281,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel", choices=["xform", "mx"], default=None,
-                    help="4:4:4 transform kernel (sets JPGX_KERNEL): k_mx (default: colour and "
-                         "row DCT on the matrix cores) or k_xform (all-VALU), DESIGN.md 4")
+                    help="4:4:4 transform kernel: k_mx (the product: colour and row DCT on the "
+                         "matrix cores) or k_xform (all-VALU, from the test-only cross-check "
+                         "library lib/libjpgx_alt.so), DESIGN.md 4")
     ap.add_argument("--subsample", action="store_true",
                     help="true 4:2:2 / 4:2:0 chroma (JPGX_FLAG_SUBSAMPLE, an extension; needs "
                          "--sample-ratio 1 or 2): not the headline metric")
@@ -283,9 +292,9 @@ def main():
         raise SystemExit("--gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
-    if args.kernel:
-        os.environ["JPGX_KERNEL"] = args.kernel
-    kname = "k_xform" if os.environ.get("JPGX_KERNEL") == "xform" else "k_mx"
+    if args.kernel == "xform":
+        os.environ["JPGX_LIB"] = ALT_LIB
+    kname = "k_xform" if alt_selected() else "k_mx"
 
     import torch
     import torch.distributed as dist

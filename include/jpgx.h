@@ -24,7 +24,10 @@
  *   - callers own every buffer; the device path keeps no global mutable state (reentrant);
  *     the host-buffer path keeps its device buffers, streams and pinned staging in explicit
  *     contexts (jpgx_host_*), which jpgx_blocks / jpgx_blocks_multi take from a thread-safe
- *     process-wide pool (jpgx_host_release frees it);
+ *     process-wide pool (jpgx_host_release frees it).  One jpgx_host_ctx serves ONE caller at
+ *     a time: its shards' buffers are reused call to call, so two threads must not call
+ *     jpgx_host_blocks on the same context concurrently (use one context per thread, or the
+ *     pooled jpgx_blocks, which hands each concurrent call its own context);
  *   - quantisation tables are rebuilt from the pristine base tables on every call
  *     (the reference rescales its globals in place, src/quantise.c:34-35).
  */

@@ -65,11 +65,6 @@ struct jx_xform_args {
     int sub;                /* k_chroma: 1 = true 4:2:2, 2 = true 4:2:0                   */
 };
 
-/* the 4:4:4 kernel used when JPGX_KERNEL is unset: 1 = k_mx, 0 = k_xform */
-#ifndef JX_DEFAULT_MX
-#define JX_DEFAULT_MX 1
-#endif
-
 
 #ifdef __cplusplus
 extern "C" {

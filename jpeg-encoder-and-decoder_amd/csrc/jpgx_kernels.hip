@@ -1289,29 +1289,14 @@ int resident_waves()
     return g_resident_waves[dev];
 }
 
-/* the 4:4:4 transform kernel: JPGX_KERNEL=xform / mx selects k_xform (all-VALU) or k_mx
- * (matrix-core row pass, csrc/jpgx_mx.hip); unset: the default */
-bool mx_selected()
-{
-    const char *e = getenv("JPGX_KERNEL");
-    if (e && strcmp(e, "mx") == 0) return true;
-    if (e && strcmp(e, "xform") == 0) return false;
-    return JX_DEFAULT_MX != 0;
-}
-
-/* JPGX_SUB422=two-pass: true 4:2:2 as k_xform (Y) + k_chroma<1>, the pre-fusion path (for
- * A/B measurements and as a second implementation in the parity tests) */
-bool sub422_two_pass()
-{
-    const char *e = getenv("JPGX_SUB422");
-    return e && strcmp(e, "two-pass") == 0;
-}
-/* JPGX_SUB420=two-pass: true 4:2:0 as k_xform (Y) + k_chroma<2> */
-bool sub420_two_pass()
-{
-    const char *e = getenv("JPGX_SUB420");
-    return e && strcmp(e, "two-pass") == 0;
-}
+/* Dispatch.  The product library (libjpgx.so) runs one kernel per mode: k_mx for 4:4:4,
+ * k_sub422 / k_sub420 for true 4:2:2 / 4:2:0.  The test-only cross-check library
+ * (libjpgx_alt.so, built from the same sources with -DJPGX_ALT_DISPATCH) runs the second
+ * implementations instead: k_xform for 4:4:4 and k_xform (Y) + k_chroma<1|2> for true 4:2:x. */
+#ifndef JPGX_ALT_DISPATCH
+#define JPGX_ALT_DISPATCH 0
+#endif
+constexpr bool kAltDispatch = JPGX_ALT_DISPATCH != 0;
 
 }  // namespace
 
@@ -1373,7 +1358,7 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     xa.force_exact = (p->flags & JPGX_FLAG_FORCE_EXACT) ? 1 : 0;
     hipStream_t s = (hipStream_t)stream;
     xa.luma_only = sub ? 1 : 0;
-    if (!sub && mx_selected()) {
+    if (!sub && !kAltDispatch) {
         /* k_mx: colour + row DCT on the matrix cores, exact pass inside (csrc/jpgx_mx.hip) */
         rc = jx_launch_mx(&xa, stream);
         if (rc) return rc;
@@ -1384,7 +1369,7 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     const size_t ntiles = (total + 63) / 64;
     const size_t waves = std::min<size_t>(ntiles, (size_t)std::max(resident_waves(), 4));
     const unsigned grid = (unsigned)((waves + JX_WG / 64 - 1) / (JX_WG / 64));
-    if (sub && p->sample_ratio == 2 && !sub420_two_pass()) {
+    if (sub && p->sample_ratio == 2 && !kAltDispatch) {
         /* true 4:2:0 in one pass (k_sub420): tiles of 16 MCUs */
         jx_geom gc = xa.g;
         gc.bpr = fr->width / 16;
@@ -1399,7 +1384,7 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
         if (!rc && event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
         return rc;
     }
-    if (sub && p->sample_ratio == 1 && !sub422_two_pass()) {
+    if (sub && p->sample_ratio == 1 && !kAltDispatch) {
         /* true 4:2:2 in one pass (k_sub422): chroma geometry as k_chroma's below */
         jx_geom gc = xa.g;
         gc.bpr = fr->width / 16;

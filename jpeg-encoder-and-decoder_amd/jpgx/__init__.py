@@ -71,16 +71,19 @@ class Frames(ctypes.Structure):
                 ("in_frame_stride", ctypes.c_size_t), ("out_frame_stride", ctypes.c_size_t)]
 
 
-def _load() -> ctypes.CDLL:
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"libjpgx.so not built ({LIB_PATH}); run __graft_entry__.build()")
+ALT_LIB_PATH = os.path.join(PKG_ROOT, "lib", "libjpgx_alt.so")
+
+
+def _load(path: str = LIB_PATH) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(f"{os.path.basename(path)} not built ({path}); run __graft_entry__.build()")
     # libjpgx.so and torch both need libamdhip64.so.7 (same soname): load torch first so the
     # process has ONE HIP runtime and device pointers/streams are shared.
     try:
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     vp, sz, i, u8p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p
     P, Fp = ctypes.POINTER(Params), ctypes.POINTER(Frames)
     L.jpgx_validate.argtypes = [i, i, P]
@@ -119,6 +122,17 @@ def _load() -> ctypes.CDLL:
 
 
 lib = _load()
+_alt = None
+
+
+def alt_library() -> ctypes.CDLL:
+    """The TEST-ONLY cross-check build (lib/libjpgx_alt.so: k_xform for 4:4:4, k_xform +
+    k_chroma for true 4:2:x), loaded on first use.  Tests swap it in for `lib` to run every
+    parity check on the second implementation; the product never loads it."""
+    global _alt
+    if _alt is None:
+        _alt = _load(ALT_LIB_PATH)
+    return _alt
 
 
 def _check(rc: int, what: str) -> None:

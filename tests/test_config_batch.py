@@ -34,7 +34,9 @@ def batch():
 
 @pytest.fixture(params=["xform", "mx"])
 def kernel(request, monkeypatch):
-    monkeypatch.setenv("JPGX_KERNEL", request.param)
+    """k_mx (the product library) and k_xform (the test-only libjpgx_alt.so)"""
+    if request.param == "xform":
+        monkeypatch.setattr(jpgx, "lib", jpgx.alt_library())
     return request.param
 
 

@@ -14,10 +14,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True, params=["xform", "mx"])
 def kernel(request, monkeypatch):
-    """Every parity test runs on both 4:4:4 kernels: k_xform (all-VALU, the default) and k_mx
-    (colour + row DCT on the matrix cores, csrc/jpgx_mx.hip), selected per call by the
-    library through JPGX_KERNEL."""
-    monkeypatch.setenv("JPGX_KERNEL", request.param)
+    """Every parity test runs on both 4:4:4 kernels: k_mx (colour + row DCT on the matrix
+    cores, csrc/jpgx_mx.hip: the product library's kernel) and k_xform (all-VALU), which only
+    the test-only cross-check library libjpgx_alt.so dispatches."""
+    if request.param == "xform":
+        monkeypatch.setattr(jpgx, "lib", jpgx.alt_library())
     return request.param
 
 

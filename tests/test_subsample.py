@@ -77,13 +77,10 @@ def _dev(a, cuda):
 
 @pytest.fixture(params=["fused", "two-pass"])
 def impl(request, monkeypatch):
-    """True 4:2:2 / 4:2:0 run as k_sub422 / k_sub420 (one pass, the default) or, with
-    JPGX_SUB422 / JPGX_SUB420 = two-pass, as k_xform's Y + k_chroma<1> / <2>."""
-    for var in ("JPGX_SUB422", "JPGX_SUB420"):
-        if request.param == "two-pass":
-            monkeypatch.setenv(var, "two-pass")
-        else:
-            monkeypatch.delenv(var, raising=False)
+    """True 4:2:2 / 4:2:0 run as k_sub422 / k_sub420 (one pass: the product library) or as
+    k_xform's Y + k_chroma<1> / <2> (the test-only cross-check library libjpgx_alt.so)."""
+    if request.param == "two-pass":
+        monkeypatch.setattr(jpgx, "lib", jpgx.alt_library())
     return request.param
 
 

@@ -21,7 +21,8 @@ W, H, q = 3840, 2160, 90
 
 
 def sweep(kernel, dev):
-    os.environ["JPGX_KERNEL"] = kernel
+    if kernel == "xform":
+        os.environ["JPGX_LIB"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "jpeg-encoder-and-decoder_amd", "lib", "libjpgx_alt.so")
     rows = []
     for F in (1, 2, 4, 8, 16, 24):
         d_in = torch.empty(F * W * H * 3, dtype=torch.uint8, device=dev)

@@ -18,11 +18,11 @@ for r in $(seq 1 "$REPS"); do
 done
 for v in "1 fused" "1 two-pass" "2 fused" "2 two-pass"; do
   set -- $v
-  if [ "$2" = two-pass ]; then export JPGX_SUB422=two-pass JPGX_SUB420=two-pass; else unset JPGX_SUB422 JPGX_SUB420; fi
+  if [ "$2" = two-pass ]; then export JPGX_LIB="$ROOT/jpeg-encoder-and-decoder_amd/lib/libjpgx_alt.so"; else unset JPGX_LIB; fi
   timeout -k 10 300 python bench.py --subsample --sample-ratio $1 --quality 75 --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/bench_sr$1_$2.json" 2> "$OUT/bench_sr$1_$2.err"; rc=$?
   echo "bench sr$1 $2 rc=$rc $(summ $OUT/bench_sr$1_$2.json)"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench_sr$1_$2.err"; exit $rc; }
 done
-unset JPGX_SUB422 JPGX_SUB420
+unset JPGX_LIB
 if [ "${SWEEP:-1}" = "1" ]; then
   timeout -k 10 400 python tools/frames_sweep.py "$OUT/frames_sweep.json" xform mx > "$OUT/frames_sweep.log" 2>&1; rc=$?
   echo "sweep rc=$rc"; tail -12 "$OUT/frames_sweep.log"; [ $rc -eq 0 ] || exit $rc

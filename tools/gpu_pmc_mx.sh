@@ -1,11 +1,11 @@
 #!/bin/bash
-# PMC passes for k_mx (JPGX_KERNEL=mx) and k_xform side by side (kernel trace + one counter group per run).
+# PMC passes for k_mx and k_xform (the test-only libjpgx_alt.so) side by side (kernel trace + one counter group per run).
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
 cd /tmp
 for k in mx xform; do
-  export JPGX_KERNEL=$k
+  if [ "$k" = xform ]; then export JPGX_LIB="$ROOT/jpeg-encoder-and-decoder_amd/lib/libjpgx_alt.so"; else unset JPGX_LIB; fi
   OUT="$ROOT/gpurun_out/pmc_$k"; mkdir -p "$OUT"
   i=0
   for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC" "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_FLAT SQ_INSTS_FLAT"; do

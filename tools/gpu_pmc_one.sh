@@ -1,8 +1,9 @@
 #!/bin/bash
-# PMC passes for one kernel selection (JPGX_KERNEL=$1), one counter group per rocprofv3 run.
+# PMC passes for one kernel ($1 = mx, or xform from the test-only libjpgx_alt.so), one counter group per rocprofv3 run.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-export TMPDIR=/tmp JPGX_KERNEL=$1
+export TMPDIR=/tmp
+if [ "$1" = xform ]; then export JPGX_LIB="$ROOT/jpeg-encoder-and-decoder_amd/lib/libjpgx_alt.so"; fi
 OUT="$ROOT/gpurun_out/pmc1_$1"; mkdir -p "$OUT"
 cd /tmp
 i=0

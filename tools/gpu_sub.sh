@@ -11,7 +11,7 @@ echo "pytest rc=$rc"; grep -E "FAIL|passed|failed|Error" "$OUT/pytest.log" | tai
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for v in "1 fused" "1 two-pass" "2 two-pass"; do
   set -- $v
-  if [ "$2" = two-pass ]; then export JPGX_SUB422=two-pass; else unset JPGX_SUB422; fi
+  if [ "$2" = two-pass ]; then export JPGX_LIB="$ROOT/jpeg-encoder-and-decoder_amd/lib/libjpgx_alt.so"; else unset JPGX_LIB; fi
   timeout -k 10 300 python bench.py --subsample --sample-ratio $1 --quality 75 --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/bench_sr$1_$2.json" 2> "$OUT/bench_sr$1_$2.err"; rc=$?
   echo "bench sr$1 $2 rc=$rc $(cat $OUT/bench_sr$1_$2.json)"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench_sr$1_$2.err"; exit $rc; }
 done

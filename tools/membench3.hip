@@ -46,42 +46,79 @@ __device__ __forceinline__ constexpr int wait_imm()
     return (int)(((5 * DIST - 2) & 15) | (((5 * DIST - 2) >> 4) << 14) | 0xF70);
 }
 
-/* the chunk source; fetch() starts a request whose value take() returns later */
+/* the chunk source; fetch() starts a request whose value take() returns later.  QM 4: the
+ * workgroup's chunk sequence is super-chunks blockIdx.x, blockIdx.x + gridDim.x, ... of
+ * a.nstatic chunks each; its waves take the next one from an LDS counter */
 template <int QM>
 struct Q {
     unsigned nw, wv, round, pend;
+    unsigned *lq;
     __device__ __forceinline__ void fetch(const Args &a)
     {
         if (QM == 0) { pend = wv + nw * (round++); return; }
+        if (QM == 4) {
+            unsigned t0 = 0;
+            if ((threadIdx.x & 63u) == 0) t0 = atomicAdd(lq, 1u);
+            const unsigned t = __builtin_amdgcn_readfirstlane(t0);
+            const unsigned sc = a.nstatic, r = t / sc;
+            pend = (blockIdx.x + gridDim.x * r) * sc + (t - r * sc);
+            return;
+        }
         if (QM == 3) {
             const unsigned k = wv + nw * round;
             if (k < a.nstatic) { round++; pend = k; return; }
         }
-        unsigned v = 0xffffffffu;
-        if ((threadIdx.x & 63u) == 0) v = atomicAdd(a.ctr, 1u) - a.base + (QM == 3 ? a.nstatic : 0u);
-        pend = v;                                  /* a VGPR; read (and waited for) in take() */
+        unsigned v = 0;
+        if (QM == 5) {
+            const unsigned x = (unsigned)__builtin_amdgcn_s_getreg((2 << 11) | 20) & 7u;
+            if ((threadIdx.x & 63u) == 0) v = atomicAdd(a.ctr + 32 * x, 1u);
+            pend = v;
+            return;
+        }
+        if ((threadIdx.x & 63u) == 0) v = atomicAdd(a.ctr, 1u);
+        pend = v;                                  /* raw: decoded (and waited for) in take() */
     }
-    __device__ __forceinline__ unsigned take() { return __builtin_amdgcn_readfirstlane(pend); }
+    __device__ __forceinline__ unsigned take(const Args &a)
+    {
+        if (QM == 0 || QM == 4) return pend;
+        const unsigned t = __builtin_amdgcn_readfirstlane(pend);
+        if (QM == 5) {
+            const unsigned x = (unsigned)__builtin_amdgcn_s_getreg((2 << 11) | 20) & 7u, G = a.nstatic;
+            return t == 0xffffffffu ? t : (t / G) * 8u * G + x * G + (t % G);
+        }
+        return t - a.base + (QM == 3 ? a.nstatic : 0u);
+    }
 };
 
-template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM>
-__global__ __launch_bounds__(256) void k_skel(Args a)
+template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM, int WPG = 4>
+__global__ __launch_bounds__(WPG * 64) void k_skel(Args a)
 {
     static_assert(CH > DIST, "the issue cursor is at most one chunk ahead");
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    __shared__ unsigned s_q;
+    if (QM == 4) {
+        if (threadIdx.x == 0) s_q = 0;
+        __syncthreads();
+    }
     const unsigned lane = threadIdx.x & 63u;
     uint8_t *ring = dyn + (threadIdx.x >> 6) * ((DIST + 1) * kSlot + kStage + 256);
     uint8_t *stage = ring + (DIST + 1) * kSlot;
     uint8_t *dummy = stage + kStage;
-    const unsigned nw = gridDim.x * 4u;
-    const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const unsigned nw = gridDim.x * WPG;
+    const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * WPG + (threadIdx.x >> 6));
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
     const unsigned nchunks = a.nsteps / CH;
-    Q<QM> q{nw, wv, 0, 0};
+    Q<QM> q{nw, wv, 0, 0, &s_q};
     q.fetch(a);
-    unsigned cc = q.take();                        /* compute chunk */
+    unsigned cc = q.take(a);                        /* compute chunk */
     if (cc >= nchunks) {
-        if (a.ts && lane == 0) { a.ts[2 * wv] = t0; a.ts[2 * wv + 1] = t0; }
+        if (a.ts && lane == 0) { a.ts[6 * wv] = 0; a.ts[6 * wv + 1] = 0; }
+        if (QM == 5) {
+            unsigned last = 0;
+            if (lane == 0) last = atomicAdd(a.ctr + 256, 1u) == nw - 1;
+            if (__builtin_amdgcn_readfirstlane(last) && lane < 9) atomicExch(a.ctr + (lane == 8 ? 256 : 32 * lane), 0u);
+        }
         return;
     }
     q.fetch(a);                                    /* the chunk after: taken when the issue cursor gets there */
@@ -101,7 +138,7 @@ __global__ __launch_bounds__(256) void k_skel(Args a)
         }
         if (ic < nchunks && ++ik == CH) {
             ik = 0;
-            ic = q.take();
+            ic = q.take(a);
             if (ic < nchunks) q.fetch(a);
         }
     };
@@ -113,7 +150,11 @@ __global__ __launch_bounds__(256) void k_skel(Args a)
     f2 acc[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) acc[i] = f2{(float)lane, (float)i};
-    const f2 k1 = {1.0001f, 0.9999f}, k2 = {0.5f, 0.25f};
+    const f2 k1 = NT == 2 ? f2{0.0f, 0.0f} : f2{1.0001f, 0.9999f}, k2 = NT == 2 ? f2{0.0f, 0.0f} : f2{0.5f, 0.25f};
+    if (NT == 2) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) acc[i] = f2{0.0f, 0.0f};
+    }
     f4 macc[4] = {};
     unsigned slot = 0;
     for (;;) {
@@ -124,9 +165,11 @@ __global__ __launch_bounds__(256) void k_skel(Args a)
         uint8_t *sp = ring + slot * kSlot;
         issue(ring + (slot == 0 ? DIST : slot - 1) * kSlot);
         const u4 d = *(const u4 *)(sp + (lane % 96) * 16);
-        acc[0].x += __uint_as_float(d.x & 0x3fffffffu);
-        acc[1].x += __uint_as_float(d.y & 0x3fffffffu);
-        h8 av = __builtin_bit_cast(h8, d);
+        if (NT != 2) {
+            acc[0].x += __uint_as_float(d.x & 0x3fffffffu);
+            acc[1].x += __uint_as_float(d.y & 0x3fffffffu);
+        }
+        h8 av = __builtin_bit_cast(h8, NT == 2 ? u4{0, 0, 0, 0} : d);
 #pragma unroll
         for (int i = 0; i < NM; i++)
             macc[i & 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, av, macc[i & 3], 0, 0, 0);
@@ -137,7 +180,7 @@ __global__ __launch_bounds__(256) void k_skel(Args a)
 #pragma unroll
         for (int i = 0; i < NL; i++)
             *(uint16_t *)(stage + (i % 3) * 1152 + ((lane * 37u + (unsigned)i * 131u) & 511u) * 2u) =
-                (uint16_t)__float_as_uint(acc[i & 7].x);
+                (uint16_t)(__float_as_uint(acc[i & 7].x) ^ (d.z >> (i & 15)));
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
         const unsigned f = sc / kStepsPerFrame, bi = (sc - f * kStepsPerFrame) * 8u;
@@ -159,9 +202,20 @@ __global__ __launch_bounds__(256) void k_skel(Args a)
         }
     }
     if (acc[5].y == 3.0f) a.out[0] = 1;
+    if (QM == 5) {
+        /* the last wave to finish resets the counters for the next launch (stream order) */
+        __builtin_amdgcn_s_waitcnt(0);
+        unsigned last = 0;
+        if (lane == 0) last = atomicAdd(a.ctr + 256, 1u) == nw - 1;
+        if (__builtin_amdgcn_readfirstlane(last) && lane < 9) atomicExch(a.ctr + (lane == 8 ? 256 : 32 * lane), 0u);
+    }
     if (a.ts && lane == 0) {
-        a.ts[2 * wv] = t0;
-        a.ts[2 * wv + 1] = __builtin_amdgcn_s_memrealtime();
+        a.ts[6 * wv] = t0;
+        a.ts[6 * wv + 1] = __builtin_amdgcn_s_memrealtime();
+        a.ts[6 * wv + 2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+        a.ts[6 * wv + 3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        a.ts[6 * wv + 4] = c0;
+        a.ts[6 * wv + 5] = __builtin_amdgcn_s_memtime();
     }
 }
 
@@ -216,40 +270,81 @@ static void timeit(const char *name, L launch)
 
 static unsigned g_ctr_val = 0;
 
-template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM>
-static void skel(int wpe, int grid_mult = 1, double static_frac = 0.0)
+template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM, int WPG = 4>
+static void skel(int wpe, int grid_mult = 1, double static_frac = 0.0, int superchunk = 0)
 {
-    char name[128];
-    snprintf(name, sizeof name, "skel v%d m%d l%d c%d d%d nt%d q%d w%d g%d sf%.2f", NV, NM, NL, CH, DIST, NT, QM,
-             wpe, grid_mult, static_frac);
-    const size_t per_wg = 4 * ((DIST + 1) * kSlot + kStage + 256);
-    const size_t lds = std::max(per_wg, (size_t)(160 * 1024 / wpe) & ~(size_t)15);
-    auto kern = k_skel<NV, NM, NL, CH, DIST, NT, QM>;
+    char name[160];
+    snprintf(name, sizeof name, "skel v%d m%d l%d c%d d%d nt%d q%d w%d g%d sf%.2f wg%d sc%d", NV, NM, NL, CH, DIST,
+             NT, QM, wpe, grid_mult, static_frac, WPG, superchunk);
+    const size_t per_wg = WPG * ((DIST + 1) * kSlot + kStage + 256);
+    /* wpe waves per SIMD: wpe * 4 / WPG workgroups per CU */
+    const size_t lds = std::max(per_wg, (size_t)(160 * 1024 * WPG / (4 * wpe) - 64) & ~(size_t)15);
+    auto kern = k_skel<NV, NM, NL, CH, DIST, NT, QM, WPG>;
     CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const unsigned nsteps = 8 * kStepsPerFrame, nchunks = nsteps / CH;
-    unsigned grid = g_cus * wpe * grid_mult;
-    if (grid_mult == 0) grid = (nchunks + 3) / 4;  /* non-persistent: one chunk per wave */
-    const unsigned nw = grid * 4;
-    const unsigned nstatic = (unsigned)(static_frac * nchunks) / nw * nw;
-    std::vector<unsigned long long> ts(2 * nw);
+    unsigned grid = g_cus * wpe * 4 / WPG * grid_mult;
+    if (grid_mult == 0) grid = (nchunks + WPG - 1) / WPG;  /* non-persistent: one chunk per wave */
+    const unsigned nw = grid * WPG;
+    unsigned nstatic = (unsigned)(static_frac * nchunks) / nw * nw;
+    if (QM == 4 || QM == 5) {
+        nstatic = superchunk;                       /* chunks per super-chunk / XCD interleave */
+    }
+    std::vector<unsigned long long> ts(6 * nw);
     timeit(name, [&](uint8_t *in, bool stamp) {
-        if (stamp) CK(hipMemset(g_ts, 0, 2 * nw * sizeof(unsigned long long)));
+        if (stamp) CK(hipMemset(g_ts, 0, 6 * nw * sizeof(unsigned long long)));
         Args a{in, g_out, nsteps, g_ctr, g_ctr_val, stamp ? g_ts : nullptr, nstatic};
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, 0, a);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(WPG * 64), lds, 0, a);
         /* every wave ends with one failing dequeue: the counter moves by the dynamic chunks + nw */
-        if (QM != 0) g_ctr_val += (nchunks - nstatic) + nw;
+        if (QM == 1 || QM == 3) g_ctr_val += (nchunks - nstatic) + nw;
         if (stamp) {
             CK(hipMemcpy(ts.data(), g_ts, ts.size() * 8, hipMemcpyDeviceToHost));
             unsigned long long mn = ~0ull;
             std::vector<double> ends;
+            std::vector<double> clk;
             for (unsigned w = 0; w < nw; w++)
-                if (ts[2 * w]) mn = std::min(mn, ts[2 * w]);
-            for (unsigned w = 0; w < nw; w++)
-                if (ts[2 * w]) ends.push_back((ts[2 * w + 1] - mn) * 0.01);
+                if (ts[6 * w]) {
+                    mn = std::min(mn, ts[6 * w]);
+                    const double dr = (double)(ts[6 * w + 1] - ts[6 * w]);
+                    if (dr > 500) clk.push_back((double)(ts[6 * w + 5] - ts[6 * w + 4]) / dr * 100.0);
+                }
+            std::sort(clk.begin(), clk.end());
+            double xsum[8] = {}, xn[8] = {};
+            /* per CU (xcc, se, cu): spread of its waves' ends */
+            std::vector<std::pair<unsigned, double>> cu;
+            for (unsigned w = 0; w < nw; w++) {
+                if (!ts[6 * w]) continue;
+                const double e = (ts[6 * w + 1] - mn) * 0.01;
+                ends.push_back(e);
+                const unsigned x = (unsigned)ts[6 * w + 2] & 7u, hw = (unsigned)ts[6 * w + 3];
+                xsum[x] += e;
+                xn[x] += 1;
+                cu.push_back({x << 16 | ((hw >> 13) & 7u) << 8 | ((hw >> 8) & 15u), e});
+            }
             std::sort(ends.begin(), ends.end());
             const size_t m = ends.size();
-            printf("  | wave ends us: p1 %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f", ends[m / 100], ends[m / 10],
+            printf("  | ends p1 %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f", ends[m / 100], ends[m / 10],
                    ends[m / 2], ends[m * 9 / 10], ends[m - 1]);
+            if (!clk.empty()) printf(" | clk MHz p50 %.0f", clk[clk.size() / 2]);
+            printf(" | xcd means");
+            for (int x = 0; x < 8; x++) printf(" %.0f", xn[x] ? xsum[x] / xn[x] : -1.0);
+            std::sort(cu.begin(), cu.end());
+            double spread = 0, cmax_lo = 1e30, cmax_hi = 0;
+            int ncu = 0;
+            for (size_t i = 0; i < cu.size();) {
+                size_t j = i;
+                double lo = 1e30, hi = 0;
+                while (j < cu.size() && cu[j].first == cu[i].first) {
+                    lo = std::min(lo, cu[j].second);
+                    hi = std::max(hi, cu[j].second);
+                    j++;
+                }
+                spread += hi - lo;
+                cmax_lo = std::min(cmax_lo, hi);
+                cmax_hi = std::max(cmax_hi, hi);
+                ncu++;
+                i = j;
+            }
+            printf(" | %d CUs: mean in-CU spread %.1f, CU last-end %.1f..%.1f", ncu, spread / ncu, cmax_lo, cmax_hi);
         }
     });
 }
@@ -262,10 +357,22 @@ int main(int argc, char **argv)
     CK(hipMalloc(&g_in[1], in_bytes + 4096));
     CK(hipMalloc(&g_out, 2 * in_bytes));
     CK(hipMalloc(&g_ctr, 256));
-    CK(hipMalloc(&g_ts, 2 * 1024 * 1024 * sizeof(unsigned long long)));
+    CK(hipMalloc(&g_ts, 6 * 1024 * 1024 * sizeof(unsigned long long)));
     CK(hipMemset(g_ctr, 0, 256));
-    CK(hipMemset(g_in[0], 7, in_bytes));
-    CK(hipMemset(g_in[1], 9, in_bytes));
+    {
+        std::vector<uint8_t> h(in_bytes);
+        uint64_t z = 12345;
+        for (size_t i = 0; i < in_bytes; i += 8) {
+            z += 0x9E3779B97F4A7C15ULL;
+            uint64_t t = z;
+            t = (t ^ (t >> 30)) * 0xBF58476D1CE4E5B9ULL;
+            t = (t ^ (t >> 27)) * 0x94D049BB133111EBULL;
+            t ^= t >> 31;
+            memcpy(&h[i], &t, std::min<size_t>(8, in_bytes - i));
+        }
+        CK(hipMemcpy(g_in[0], h.data(), in_bytes, hipMemcpyHostToDevice));
+        CK(hipMemcpy(g_in[1], h.data(), in_bytes, hipMemcpyHostToDevice));
+    }
     CK(hipMemset(g_out, 0, 2 * in_bytes));
     CK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, 0));
     CK(hipEventCreate(&e0));
@@ -280,23 +387,19 @@ int main(int argc, char **argv)
         skel<0, 0, 0, 4, 2, 1, 1>(3);
         skel<0, 0, 0, 8, 2, 1, 1>(3);
         skel<0, 0, 0, 16, 2, 1, 1>(3);
-        skel<0, 0, 0, 4, 2, 1, 3>(3, 1, 0.8);
-        skel<0, 0, 0, 4, 2, 1, 3>(3, 1, 0.5);
-        skel<0, 0, 0, 4, 2, 1, 1>(4);
-        skel<0, 0, 0, 8, 2, 1, 1>(4);
+        skel<0, 0, 0, 4, 2, 1, 5>(3, 1, 0, 1);
+        skel<0, 0, 0, 4, 2, 1, 5>(3, 1, 0, 4);
+        skel<0, 0, 0, 8, 2, 1, 5>(3, 1, 0, 1);
+        skel<0, 0, 0, 4, 2, 1, 5>(4, 1, 0, 1);
+        skel<0, 0, 0, 4, 2, 1, 5>(2, 1, 0, 1);
     }
     if (!strcmp(which, "all") || !strcmp(which, "b")) {
         skel<192, 16, 24, 4, 2, 1, 0>(3);
-        skel<192, 16, 24, 4, 2, 1, 1>(3);
+        skel<192, 16, 24, 4, 2, 1, 0>(3, 0);
+        skel<192, 16, 24, 4, 2, 1, 5>(3, 1, 0, 1);
+        skel<192, 16, 24, 8, 2, 1, 5>(3, 1, 0, 1);
         skel<192, 16, 24, 8, 2, 1, 1>(3);
-        skel<192, 16, 24, 4, 2, 1, 3>(3, 1, 0.8);
-        skel<128, 16, 24, 4, 2, 1, 0>(3);
-        skel<128, 16, 24, 4, 2, 1, 1>(3);
-        skel<128, 16, 24, 4, 2, 1, 1>(4);
-        skel<256, 16, 24, 4, 2, 1, 0>(3);
-        skel<256, 16, 24, 4, 2, 1, 1>(3);
-        skel<256, 16, 24, 8, 2, 1, 1>(3);
-        skel<256, 16, 24, 8, 2, 1, 1>(4);
+        skel<192, 16, 24, 4, 2, 1, 5>(4, 1, 0, 1);
     }
     return 0;
 }

@@ -11,7 +11,6 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["JPGX_LIB"] = os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "lib", "variants",
                                       "libjpgx_mxCount.so")
-os.environ["JPGX_KERNEL"] = "mx"
 sys.path.insert(0, os.path.join(REPO, "jpeg-encoder-and-decoder_amd"))
 import jpgx  # noqa: E402
 

@@ -7,7 +7,6 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "jpeg-encoder-and-decoder_amd"), os.path.join(REPO, "oracle")]
-os.environ["JPGX_KERNEL"] = "mx"
 import jpgx  # noqa: E402
 import oracle as O  # noqa: E402
 

@@ -30,7 +30,8 @@ def sample(stop, out):
 def main():
     dst = sys.argv[1]
     if len(sys.argv) > 2:
-        os.environ["JPGX_KERNEL"] = sys.argv[2]
+        if sys.argv[2] == "xform":
+            os.environ["JPGX_LIB"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "jpeg-encoder-and-decoder_amd", "lib", "libjpgx_alt.so")
     W, H, F, q = 3840, 2160, 8, 90
     dev = torch.device("cuda:0")
     d_in = torch.empty(F * W * H * 3, dtype=torch.uint8, device=dev)
@@ -63,7 +64,7 @@ def main():
         ms.append((time.time() - t0, e0.elapsed_time(e1) / 50))
     stop.set()
     th.join()
-    res = {"kernel": os.environ.get("JPGX_KERNEL", "default"), "launch_ms": ms, "idle": idle,
+    res = {"kernel": ("xform" if os.environ.get("JPGX_LIB", "").endswith("_alt.so") else "mx"), "launch_ms": ms, "idle": idle,
            "load": samples}
     with open(dst, "w") as f:
         json.dump(res, f, indent=1)

@@ -1,0 +1,282 @@
+// spec_bench.hip -- wave-specialised memory skeleton of the block transform (not product code).
+// One workgroup per CU: NLD loader waves (LDS-DMA of the pixel rows into an input ring, waiting
+// only on their own loads), NST storer waves (ds_read_b128 of the coefficient stage + 1 KiB
+// nontemporal stores, never waiting on them), NC compute waves (synthetic compute: NV packed
+// FMAs, NM MFMAs, NL ds_write_b16, reading the input ring and writing the output ring).  One
+// s_barrier per round; a round = NC steps of 8 blocks (one per compute wave).  Rounds of a
+// workgroup: r-th round = global round blockIdx.x + gridDim.x * r (static), or NP mode (one
+// launch-time range per workgroup of RPW rounds).  8 x 4K frames, fresh input (2 sets), 9 B/px.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/spec_bench.hip -o tools/spec_bench
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+constexpr unsigned kW = 3840, kH = 2160, kPitch = kW * 3;
+constexpr unsigned kStepsPerRow = kW / 64;
+constexpr unsigned kNb = (kW / 8) * (kH / 8);
+constexpr unsigned kStepsPerFrame = kNb / 8;
+constexpr unsigned kSlot = 1536, kOut = 3072;     /* per step: pixels, coefficients (3 x 1 KiB) */
+
+typedef __attribute__((address_space(3))) void *lp;
+
+/* workgroup barrier for LDS hand-offs only: no vmcnt drain (a __syncthreads() fence may wait for
+ * the storers' outstanding global stores) */
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+typedef const __attribute__((address_space(1))) void *gp;
+
+struct Args {
+    const uint8_t *in;
+    int16_t *out;
+    unsigned nsteps;
+    unsigned long long *ts;
+    unsigned rounds_per_wg;        /* NP mode: consecutive rounds per workgroup (0 = static stride) */
+};
+
+template <int NLD, int NST, int NC, int NV, int NM, int NL, int ZERO>
+__global__ __launch_bounds__((NLD + NST + NC) * 64) void k_spec(Args a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *in_ring = lds;                        /* [3][NC][kSlot]  */
+    uint8_t *out_ring = lds + 3 * NC * kSlot;      /* [2][NC][kOut]   */
+    uint8_t *dummy = out_ring + 2 * NC * kOut;
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const unsigned nrounds_total = a.nsteps / NC;  /* global rounds (steps in multiples of NC) */
+    unsigned r0, rstride, nr;
+    if (a.rounds_per_wg) {
+        r0 = blockIdx.x * a.rounds_per_wg;
+        rstride = 1;
+        nr = r0 < nrounds_total ? std::min(a.rounds_per_wg, nrounds_total - r0) : 0;
+    } else {
+        r0 = blockIdx.x;
+        rstride = gridDim.x;
+        nr = r0 < nrounds_total ? (nrounds_total - r0 + rstride - 1) / rstride : 0;
+    }
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+    auto gstep = [&](unsigned r, unsigned k) { return (r0 + rstride * r) * NC + k; };
+    /* loader: steps of round r, k = wave, wave + NLD, ...; 2 DMA pieces each */
+    const uint32_t off0 = (lane / 12u) * kPitch + 16u * (lane % 12u);
+    const uint32_t off1 = ((64u + lane) / 12u) * kPitch + 16u * ((64u + lane) % 12u);
+    constexpr int kLdPer = (NC + NLD - 1) / NLD;   /* steps per loader per round */
+    auto load_round = [&](unsigned r) {
+        uint8_t *slot = in_ring + (r % 3) * NC * kSlot;
+#pragma unroll
+        for (int i = 0; i < kLdPer; i++) {
+            const unsigned k = wave + NLD * i;
+            if (r < nr && k < NC) {
+                const unsigned s = gstep(r, k);
+                const uint8_t *b = a.in + (size_t)(s / kStepsPerRow) * 8 * kPitch + (s % kStepsPerRow) * 192u;
+                __builtin_amdgcn_global_load_lds((gp)(b + off0), (lp)(slot + k * kSlot), 16, 0, 0);
+                if (lane < 32) __builtin_amdgcn_global_load_lds((gp)(b + off1), (lp)(slot + k * kSlot + 1024), 16, 0, 0);
+            } else {
+                __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
+            }
+        }
+    };
+    constexpr int kLdWait = 2 * kLdPer;            /* one round of DMA younger than the awaited one */
+    constexpr int kLdImm = (kLdWait & 15) | ((kLdWait >> 4) << 14) | 0xF70;
+    /* storer: the 3 NC KiB pieces of round r, piece p = wave - NLD + NST * i */
+    constexpr int kStPer = (3 * NC + NST - 1) / NST;
+    auto store_round = [&](unsigned r) {
+        const uint8_t *slot = out_ring + (r % 2) * NC * kOut;
+#pragma unroll
+        for (int i = 0; i < kStPer; i++) {
+            const unsigned pc = (wave - NLD) + NST * i;
+            if (pc < 3 * NC) {
+                const unsigned k = pc / 3, c = pc - 3 * k;
+                const u4 v = *(const u4 *)(slot + k * kOut + c * 1024 + lane * 16);
+                const unsigned s = gstep(r, k), f = s / kStepsPerFrame, bi = (s - f * kStepsPerFrame) * 8u;
+                int16_t *o = a.out + (size_t)f * 3 * kNb * 64 + (size_t)c * kNb * 64 + (size_t)bi * 64 + lane * 8;
+                __builtin_nontemporal_store(v, (u4 *)o);
+            }
+        }
+    };
+    f2 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc[i] = ZERO ? f2{0.0f, 0.0f} : f2{(float)lane, (float)i};
+    const f2 k1 = ZERO ? f2{0.0f, 0.0f} : f2{1.0001f, 0.9999f}, k2 = ZERO ? f2{0.0f, 0.0f} : f2{0.5f, 0.25f};
+    f4 macc[4] = {};
+    const bool is_ld = wave < NLD, is_st = wave >= NLD && wave < NLD + NST;
+    const unsigned cw = wave - NLD - NST;          /* compute wave index */
+    /* prologue: rounds 0 and 1 loaded */
+    if (is_ld) {
+        load_round(0);
+        load_round(1);
+        __builtin_amdgcn_s_waitcnt(kLdImm);        /* round 0 landed */
+    }
+    lds_barrier();
+    for (unsigned r = 0; r < nr + 1; r++) {
+        /* round r: loaders issue round r+2, storers store round r-1, computers compute round r */
+        if (is_ld) {
+            load_round(r + 2);
+        } else if (is_st) {
+            if (r >= 1) store_round(r - 1);
+        } else if (r < nr) {
+            const uint8_t *sp = in_ring + (r % 3) * NC * kSlot + cw * kSlot;
+            uint8_t *op = out_ring + (r % 2) * NC * kOut + cw * kOut;
+            const u4 d = *(const u4 *)(sp + (lane % 96) * 16);
+            if (!ZERO) {
+                acc[0].x += __uint_as_float(d.x & 0x3fffffffu);
+                acc[1].x += __uint_as_float(d.y & 0x3fffffffu);
+            }
+            h8 av = __builtin_bit_cast(h8, ZERO ? u4{0, 0, 0, 0} : d);
+#pragma unroll
+            for (int i = 0; i < NM; i++)
+                macc[i & 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, av, macc[i & 3], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < NV; i++)
+                asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(acc[i & 7]) : "v"(k1), "v"(k2));
+            if (NM) acc[2].x += macc[0].x + macc[1].y + macc[2].z + macc[3].w;
+#pragma unroll
+            for (int i = 0; i < NL; i++)
+                *(uint16_t *)(op + (i % 3) * 1024 + ((lane * 37u + (unsigned)i * 131u) & 511u) * 2u) =
+                    (uint16_t)(__float_as_uint(acc[i & 7].x) ^ (d.z >> (i & 15)));
+            if (NL == 0) *(u4 *)(op + lane * 16) = d;
+        }
+        if (is_ld) __builtin_amdgcn_s_waitcnt(kLdImm);   /* round r+1 landed (round r+2 in flight) */
+        lds_barrier();
+    }
+    if (acc[5].y == 3.0f) a.out[0] = 1;
+    if (a.ts && lane == 0) {
+        const unsigned wg = blockIdx.x * (NLD + NST + NC) + wave;
+        a.ts[4 * wg] = t0;
+        a.ts[4 * wg + 1] = __builtin_amdgcn_s_memrealtime();
+        a.ts[4 * wg + 2] = c0;
+        a.ts[4 * wg + 3] = __builtin_amdgcn_s_memtime();
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void k_ideal(const u4 *__restrict__ in, u4 *__restrict__ out, size_t n)
+{
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const u4 v = in[i];
+        __builtin_nontemporal_store(v * 3u, out + i);
+        __builtin_nontemporal_store(v ^ 0x5a5a5a5au, out + n + i);
+    }
+}
+
+static uint8_t *g_in[2];
+static int16_t *g_out;
+static unsigned long long *g_ts;
+static int g_cus;
+static hipEvent_t e0, e1;
+
+template <class L>
+static void timeit(const char *name, L launch)
+{
+    int which = 0;
+    for (int i = 0; i < 300; i++) launch(g_in[(which++) & 1], false);
+    CK(hipDeviceSynchronize());
+    std::vector<float> v;
+    for (int r = 0; r < 5; r++) {
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < 20; i++) launch(g_in[(which++) & 1], false);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        v.push_back(ms * 1e3f / 20);
+    }
+    std::sort(v.begin(), v.end());
+    const double bytes = 8.0 * kW * kH * 9;
+    printf("%-44s min %7.1f us  med %7.1f us  frac(min) %.3f", name, v[0], v[2], bytes / (v[0] * 1e-6) / 8e12);
+    launch(g_in[(which++) & 1], true);
+    CK(hipDeviceSynchronize());
+    printf("\n");
+    fflush(stdout);
+}
+
+template <int NLD, int NST, int NC, int NV, int NM, int NL, int ZERO>
+static void spec(unsigned rounds_per_wg = 0)
+{
+    constexpr int NWV = NLD + NST + NC;
+    char name[128];
+    snprintf(name, sizeof name, "spec ld%d st%d c%d v%d m%d l%d z%d rpw%u", NLD, NST, NC, NV, NM, NL, ZERO, rounds_per_wg);
+    const size_t lds = 3 * NC * kSlot + 2 * NC * kOut + 256;
+    if (lds > 160 * 1024) { printf("%s: LDS %zu too big\n", name, lds); return; }
+    auto kern = k_spec<NLD, NST, NC, NV, NM, NL, ZERO>;
+    CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024)));
+    const unsigned nsteps = 8 * kStepsPerFrame / NC * NC, nrt = nsteps / NC;
+    const unsigned grid = rounds_per_wg ? (nrt + rounds_per_wg - 1) / rounds_per_wg : g_cus;
+    std::vector<unsigned long long> ts(4 * (size_t)grid * NWV);
+    timeit(name, [&](uint8_t *in, bool stamp) {
+        Args a{in, g_out, nsteps, stamp ? g_ts : nullptr, rounds_per_wg};
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(NWV * 64), 160 * 1024, 0, a);
+        if (stamp) {
+            CK(hipMemcpy(ts.data(), g_ts, ts.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long mn = ~0ull;
+            std::vector<double> clk, ends;
+            for (size_t w = 0; w < (size_t)grid * NWV; w++) mn = std::min(mn, ts[4 * w]);
+            for (size_t w = 0; w < (size_t)grid * NWV; w++) {
+                ends.push_back((ts[4 * w + 1] - mn) * 0.01);
+                const double dr = (double)(ts[4 * w + 1] - ts[4 * w]);
+                if (dr > 500) clk.push_back((double)(ts[4 * w + 3] - ts[4 * w + 2]) / dr * 100.0);
+            }
+            std::sort(ends.begin(), ends.end());
+            std::sort(clk.begin(), clk.end());
+            printf("  | ends p1 %.1f p50 %.1f max %.1f | clk p50 %.0f", ends[ends.size() / 100], ends[ends.size() / 2],
+                   ends.back(), clk.empty() ? 0.0 : clk[clk.size() / 2]);
+        }
+    });
+}
+
+int main(int argc, char **argv)
+{
+    const size_t in_bytes = 8ull * kW * kH * 3;
+    CK(hipMalloc(&g_in[0], in_bytes + 4096));
+    CK(hipMalloc(&g_in[1], in_bytes + 4096));
+    CK(hipMalloc(&g_out, 2 * in_bytes));
+    CK(hipMalloc(&g_ts, 4 * 1024 * 1024 * sizeof(unsigned long long)));
+    {
+        std::vector<uint8_t> h(in_bytes);
+        uint64_t z = 12345;
+        for (size_t i = 0; i < in_bytes; i += 8) {
+            z += 0x9E3779B97F4A7C15ULL;
+            uint64_t t = z;
+            t = (t ^ (t >> 30)) * 0xBF58476D1CE4E5B9ULL;
+            t = (t ^ (t >> 27)) * 0x94D049BB133111EBULL;
+            t ^= t >> 31;
+            memcpy(&h[i], &t, std::min<size_t>(8, in_bytes - i));
+        }
+        CK(hipMemcpy(g_in[0], h.data(), in_bytes, hipMemcpyHostToDevice));
+        CK(hipMemcpy(g_in[1], h.data(), in_bytes, hipMemcpyHostToDevice));
+    }
+    CK(hipMemset(g_out, 0, 2 * in_bytes));
+    CK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, 0));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const size_t n = in_bytes / 16;
+    timeit("ideal_np_nt", [&](uint8_t *in, bool) {
+        hipLaunchKernelGGL(k_ideal<1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, (const u4 *)in, (u4 *)g_out, n);
+    });
+    /* memory only */
+    spec<1, 2, 9, 0, 0, 0, 0>();
+    spec<2, 2, 8, 0, 0, 0, 0>();
+    spec<2, 4, 10, 0, 0, 0, 0>();
+    spec<1, 2, 9, 0, 0, 0, 0>(4);
+    spec<1, 2, 9, 0, 0, 0, 0>(16);
+    /* with compute */
+    spec<1, 2, 9, 192, 16, 24, 0>();
+    spec<1, 2, 9, 192, 16, 24, 1>();
+    spec<2, 2, 8, 192, 16, 24, 0>();
+    spec<2, 4, 10, 192, 16, 24, 0>();
+    spec<1, 2, 9, 128, 16, 24, 0>();
+    spec<1, 2, 9, 192, 16, 24, 0>(16);
+    return 0;
+}

@@ -50,9 +50,10 @@ print(json.dumps({"hash": h, "ms": sorted(ts)}))
 
 def run(lib):
     env = dict(os.environ, JPGX_LIB=lib)
-    if "#" in lib:                         # the default library with JPGX_KERNEL=<kernel>
-        lib, kern = lib.split("#")
-        env.update(JPGX_LIB=lib, JPGX_KERNEL=kern)
+    if lib.endswith("#xform"):             # the test-only cross-check library (k_xform)
+        env.update(JPGX_LIB=os.path.join(os.path.dirname(lib.split("#")[0]), "libjpgx_alt.so"))
+    elif "#" in lib:
+        env.update(JPGX_LIB=lib.split("#")[0])
     r = subprocess.run([sys.executable, "-c", CHILD % {"repo": REPO}], env=env, capture_output=True,
                        text=True, timeout=300)
     if r.returncode:
