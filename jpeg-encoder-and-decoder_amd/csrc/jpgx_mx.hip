@@ -65,7 +65,7 @@ constexpr unsigned kSlot = 1536;        /* one step's pixels: [y][8 blocks x 24 
 #define JX_MX_DIST 2                    /* DMA issued this many steps ahead                  */
 #endif
 constexpr unsigned kDist = JX_MX_DIST;
-constexpr unsigned kRing = kDist + 1;   /* LDS input slots                                   */
+constexpr unsigned kRing = 4;           /* LDS input slots: one chunk (step k in slot k)      */
 /* s_waitcnt immediate for vmcnt(5 kDist - 2): the VMEM operations younger than a step's DMA
  * (kDist steps' 3 stores each, kDist - 1 steps' 2 DMA pieces each) */
 constexpr unsigned kVmWait = 5 * kDist - 2;
@@ -170,6 +170,7 @@ struct MxG {
     long long pitch, fstride, ofstride;
     unsigned bpr, nb, total;
     int row0, quality, force;
+    bool lin_store;                     /* plane offsets fit the stores' 32-bit lane offsets */
     uint32_t u[6];                      /* the underflow pixel row (jx_geom.under) */
 };
 
@@ -197,100 +198,75 @@ __device__ __forceinline__ void mx_seek(MxCur &P, const MxG &g, unsigned b0)
     mx_ptrs(P, g);
 }
 
-/* to the next step (first block b0 + 8): pointer bumps inside a block-row, a seek otherwise */
-__device__ __forceinline__ void mx_next(MxCur &P, const MxG &g, unsigned b0)
-{
-    if (__builtin_expect(P.c + 8u < g.bpr && P.bi + 8u < g.nb, 1)) {
-        P.c += 8u;
-        P.bi += 8u;
-        P.src += 192;
-        P.dst += 512;
-    } else {
-        mx_seek(P, g, b0 + 8u);
-    }
-}
-
 /* the step's 8 blocks lie in one block-row of one frame, none is the row's last block, all in
  * range: lane-linear source addresses */
 __device__ __forceinline__ bool mx_simple_load(const MxCur &p, const MxG &g, unsigned b0)
 {
     return p.c + 8u < g.bpr && b0 + 8u <= g.total;
 }
-__device__ __forceinline__ bool mx_simple_store(const MxCur &p, const MxG &g, unsigned b0)
-{
-    return p.bi + 8u <= g.nb && b0 + 8u <= g.total;
-}
 
 /*
- * Which steps a wave computes.  kChunk = 0: one contiguous range per wave, balanced to a step.
- * kChunk = C > 0: the launch's steps cut into chunks of C; wave wv takes chunks wv, wv + nw,
- * wv + 2 nw, ... (grid-stride over chunks), so the waves in flight stream through one window of
- * about nw C steps of the frames at a time -- neighbouring waves read and write neighbouring
- * bytes -- instead of each wave streaming through its own 1/nw of the batch.  From a chunk's
- * last step to the wave's next chunk is a constant jb = 8 (nw C - C + 1) blocks, so the cursor
- * moves there without a division.  s = nsteps once the wave is done.
+ * Which steps a wave computes: the launch's blocks cut into chunks of kChunk steps (32 blocks);
+ * wave wv takes chunks wv, wv + nw, wv + 2 nw, ... (grid-stride), so the waves in flight stream
+ * through one window of about nw chunks at a time -- neighbouring waves on neighbouring bytes.
+ * All the bookkeeping is per chunk: its position (one division at the wave's start, then a
+ * constant jump of 32 nw blocks), its base pointers, and whether all its steps are "simple"
+ * (one block-row of one frame, not the row's last block, in range): then every step of it is
+ * two LDS-DMA instructions and three stores off SGPR bases with loop-invariant lane offsets.
+ * The rare other chunks (a row's last 32 blocks, frame / stripe / launch ends) take the general
+ * per-step path.
  */
 #ifndef JX_MX_CHUNK
 #define JX_MX_CHUNK 4
 #endif
 constexpr unsigned kChunk = JX_MX_CHUNK;
-struct MxSpan {
-    unsigned s, end;
+static_assert(kChunk == 4 && kDist == 2, "the ring holds one chunk: step k of a chunk in slot k");
+struct MxChunk {
+    unsigned b0;                        /* first block (launch-global); >= total: none        */
+    unsigned f, bi, r, c;               /* frame, block in frame, block-row, column of b0      */
+    const uint8_t *src;                 /* pixel (8c, 8r) of frame f                           */
+    int16_t *dst;                       /* frame f's channel-0 output of block bi              */
+    bool simple;
 };
 struct MxJump {
-    unsigned nwC, jb, jr, jc, rows;     /* nw C; jb blocks = jr block-rows + jc blocks; rows/frame */
+    unsigned jb, jr, jc, rows;          /* 32 nw blocks = jr block-rows + jc blocks; rows/frame */
 };
 
-__device__ __forceinline__ void mx_span_init(MxSpan &R, MxJump &J, const MxG &g, unsigned nsteps,
-                                             unsigned nw, unsigned wv)
+__device__ __forceinline__ void mx_chunk_ptrs(MxChunk &C, const MxG &g)
 {
-    if (kChunk == 0) {
-        R.s = (unsigned)(((unsigned long long)nsteps * wv) / nw);
-        R.end = (unsigned)(((unsigned long long)nsteps * (wv + 1)) / nw);
-        if (R.s >= R.end) R.s = R.end = nsteps;
-        J = MxJump{0u, 0u, 0u, 0u, 0u};
-        return;
-    }
-    R.s = wv * kChunk;
-    R.end = std::min(R.s + kChunk, nsteps);
-    if (R.s >= nsteps) R.s = R.end = nsteps;
-    J.nwC = nw * kChunk;
-    J.jb = 8u * (J.nwC - kChunk + 1u);
-    J.jr = J.jb / g.bpr;
-    J.jc = J.jb - J.jr * g.bpr;
-    J.rows = g.nb / g.bpr;
+    C.src = g.rgb + (long long)C.f * g.fstride + 8ll * C.r * g.pitch + 24ll * C.c;
+    C.dst = g.out + (long long)C.f * g.ofstride + 64ll * C.bi;
+    C.simple = C.b0 + 32u <= g.total && C.c + 32u < g.bpr && g.lin_store;
 }
 
-/* to the wave's next step, and the cursor with it */
-__device__ __forceinline__ void mx_step(MxSpan &R, MxCur &P, const MxG &g, unsigned nsteps,
-                                        const MxJump &J)
+__device__ __forceinline__ void mx_chunk_at(MxChunk &C, const MxG &g, unsigned b0)
 {
-    if (R.s + 1u < R.end) {
-        mx_next(P, g, 8u * R.s);
-        R.s++;
-        return;
+    C.b0 = b0;
+    C.f = b0 / g.nb;
+    C.bi = b0 - C.f * g.nb;
+    C.r = C.bi / g.bpr;
+    C.c = C.bi - C.r * g.bpr;
+    mx_chunk_ptrs(C, g);
+}
+
+/* the wave's next chunk, 32 nw blocks on: no division */
+__device__ __forceinline__ void mx_chunk_next(MxChunk &C, const MxG &g, const MxJump &J)
+{
+    C.b0 += J.jb;
+    if (C.b0 >= g.total) return;
+    C.bi += J.jb;
+    C.c += J.jc;
+    C.r += J.jr;
+    if (C.c >= g.bpr) {
+        C.c -= g.bpr;
+        C.r++;
     }
-    const unsigned ns = R.s + J.jb / 8u;
-    if (kChunk == 0 || R.end >= nsteps || ns >= nsteps) {
-        R.s = nsteps;
-        return;
+    while (C.bi >= g.nb) {
+        C.bi -= g.nb;
+        C.r -= J.rows;
+        C.f++;
     }
-    /* P is at step R.s (a chunk's last): move it jb blocks on */
-    P.bi += J.jb;
-    P.c += J.jc;
-    P.r += J.jr;
-    if (P.c >= g.bpr) {
-        P.c -= g.bpr;
-        P.r++;
-    }
-    while (P.bi >= g.nb) {
-        P.bi -= g.nb;
-        P.r -= J.rows;
-        P.f++;
-    }
-    mx_ptrs(P, g);
-    R.s = ns;
-    R.end = std::min(ns + kChunk, nsteps);
+    mx_chunk_ptrs(C, g);
 }
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -549,10 +525,12 @@ __device__ __forceinline__ void mx_column(const mx_f2 (&R)[4], const mx_f2 (&W)[
         const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
         *(uint16_t *)(st + zo[jx_pk_k(p, 0)]) = (uint16_t)__float_as_uint(tm.x);
         *(uint16_t *)(st + zo[jx_pk_k(p, 1)]) = (uint16_t)__float_as_uint(tm.y);
+#ifndef JX_MX_DBG_NOBAND               /* timing experiments only: no band test (NOT exact) */
         const mx_f2 rr = tm - M2;
         const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
         const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
         emax = __builtin_fmaxf(__builtin_fmaxf(emax, e.x), e.y);          /* v_max3_f32 */
+#endif
     }
 }
 
@@ -598,18 +576,16 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     g.row0 = a.g.row0;
     g.quality = a.quality;
     g.force = a.force_exact;
+    /* the stores' lane offsets (lane * 16 + plane * nb * 128 bytes) fit 32 bits */
+    g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
 #pragma unroll
     for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
 
     const unsigned lane = threadIdx.x & 63u;
     MxLds &L = s_lds[threadIdx.x >> 6];
-    const unsigned nsteps = (g.total + 7u) / 8u;
     const unsigned nw = gridDim.x * 4u;
     const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    MxSpan RC;                                     /* the step being computed */
-    MxJump J;
-    mx_span_init(RC, J, g, nsteps, nw, wv);
-    if (RC.s >= nsteps) return;
+    if (32u * wv >= g.total) return;
 
     /* A operand of this lane: row m = lane & 15 (block m >> 2 of the set, pixel row m & 3 of the
      * half), k-group q = lane >> 4 (bytes 8q..8q+7; q = 3: the bias) */
@@ -621,6 +597,9 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     /* DMA pieces p = lane, 64 + lane: pixel row p / 12, bytes 16 (p % 12) of the step's row */
     const uint32_t off0 = (uint32_t)((lane / 12u) * (unsigned)g.pitch + 16u * (lane % 12u));
     const uint32_t off1 = (uint32_t)(((64u + lane) / 12u) * (unsigned)g.pitch + 16u * ((64u + lane) % 12u));
+    /* stores: lane's 16 bytes of channel c's 8 blocks, as byte offsets from the step's block 0 */
+    const uint32_t so0 = lane * 16u, so1 = so0 + g.nb * 128u, so2 = so1 + g.nb * 128u;
+    const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
 
     /* C layout: lane (gq = lane >> 4, j = lane & 15) holds column j of rows 4 gq..4 gq + 3 */
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
@@ -646,39 +625,56 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
 #pragma unroll
         for (int w = 0; w < 3; w++) B[p][w] = g_mxB[3 * p + w][lane];
 
-    MxCur P;
-    mx_seek(P, g, 8u * RC.s);
-    /* prologue: the first kDist steps' DMA (ring slots 0..kDist-1), each followed by three
-     * padding operations in place of the stores of the (absent) steps before the first */
-    MxCur PN = P;                                  /* position of the next step to issue */
-    MxSpan RN = RC;
-#pragma unroll
-    for (int k = 0; k < (int)kDist; k++) {
-        const unsigned sn = RN.s;
-        if (sn < nsteps) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[k]);
-        else mx_pad(g, L, 2);
-        mx_pad(g, L, 3);
-        mx_step(RN, PN, g, nsteps, J);
-    }
-    unsigned slot = 0;
+    /* chunks: cc (computed now), nc2 (the next one; its first two steps are issued during cc's
+     * last two) */
+    MxJump J;
+    J.jb = 32u * nw;
+    J.jr = J.jb / g.bpr;
+    J.jc = J.jb - J.jr * g.bpr;
+    J.rows = g.nb / g.bpr;
+    MxChunk cc;
+    mx_chunk_at(cc, g, 32u * wv);
+    MxChunk nx = cc;
+
+    /* DMA of step k of chunk C into ring slot k (the slot the step computes from) */
+    const auto issue = [&](const MxChunk &C, unsigned k) {
+        uint8_t *const slot = L.ring[k];
+        const unsigned b = C.b0 + 8u * k;
+        if (b >= g.total) {
+            mx_pad(g, L, 2);
+        } else if (C.simple) {
+            const uint8_t *base = C.src + 192u * k;
+            __builtin_amdgcn_global_load_lds((mx_gp)(base + off0), (mx_lp)slot, 16, 0, 0);
+            if (lane < 32) __builtin_amdgcn_global_load_lds((mx_gp)(base + off1), (mx_lp)(slot + 1024u), 16, 0, 0);
+        } else {
+            MxCur P;
+            mx_seek(P, g, b);
+            mx_issue(g, P, b, mx_simple_load(P, g, b), off0, off1, slot);
+        }
+    };
+    /* prologue: steps 0 and 1, each followed by three padding operations in place of the stores
+     * of the (absent) steps before the first */
+    issue(cc, 0);
+    mx_pad(g, L, 3);
+    issue(cc, 1);
+    mx_pad(g, L, 3);
     int nq = 0, ns = 0;                            /* deferred exact tasks, their blocks */
-    while (RC.s < nsteps) {
-        const unsigned b0 = 8u * RC.s;
-        /* this step's DMA: younger VMEM operations are the next step's 2 pieces and the last
-         * two steps' 3 stores each (vmcnt counts loads, LDS-DMA and stores in issue order) */
+    unsigned k = 0;                                /* step of cc */
+    for (;;) {
+        const unsigned b0 = cc.b0 + 8u * k;
         /* VMEM operations younger than this step's DMA, in issue order: the three stores of each
-         * of steps s-kDist..s-1 and the two DMA pieces of each of steps s+1..s+kDist-1 (padding
-         * operations stand in for the ones that do not exist; a general step's loads and the
-         * exact flush wait for themselves, which only makes this count conservative) */
+         * of steps s-2, s-1 and the two DMA pieces of step s+1 (padding operations stand in for
+         * the ones that do not exist; a general step's loads and the exact flush wait for
+         * themselves, which only makes this count conservative) */
         __builtin_amdgcn_s_waitcnt(kWaitImm);
         mx_wave_sync();
-        uint8_t *const sp = L.ring[slot];
-        /* the step after next: its DMA into the slot step s-1 used */
-        {
-            const unsigned sn = RN.s, nslot = slot == 0 ? kRing - 1u : slot - 1u;
-            if (sn < nsteps) mx_issue(g, PN, 8u * sn, mx_simple_load(PN, g, 8u * sn), off0, off1, L.ring[nslot]);
-            else mx_pad(g, L, 2);
-            mx_step(RN, PN, g, nsteps, J);
+        const uint8_t *const sp = L.ring[k];
+        /* the step after next: step k + 2 of this chunk, or step k - 2 of the next */
+        if (k < 2) {
+            issue(cc, k + 2);
+        } else {
+            if (k == 2) mx_chunk_next(nx, g, J);
+            issue(nx, k - 2);
         }
         /* A operands: set 0/1 x half lo/hi */
         const mx_u2 d00 = *(const mx_u2 *)(sp + aoff);
@@ -699,20 +695,25 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         const auto mma_set = [&](mx_f4(&o)[4], const mx_h8 &Alo, const mx_h8 &Ahi) {
             o[0] = mx_mma(Alo, B[0][0], z);
             o[2] = mx_mma(Ahi, B[0][0], z);
+#ifdef JX_MX_DBG_NOLO               /* timing experiments only: no lo-part MFMAs (NOT exact) */
+            o[1] = z;
+            o[3] = z;
+#else
             o[1] = mx_mma(Alo, B[1][0], z);
             o[3] = mx_mma(Ahi, B[1][0], z);
+#endif
             if (kParts == 3) {
                 o[1] = mx_mma(Alo, B[kParts - 1][0], o[1]);
                 o[3] = mx_mma(Ahi, B[kParts - 1][0], o[3]);
             }
         };
-        const auto column = [&](int k) {
-            mx_combine(acc[k][0], acc[k][1], acc[k][2], acc[k][3], R);
+        const auto column = [&](int kc) {
+            mx_combine(acc[kc][0], acc[kc][1], acc[kc][2], acc[kc][3], R);
             float e = -1.0f;
-            const mx_f2(&W)[4] = k < 2 ? Wy : Wc;
-            const mx_f2(&Lq)[4] = k < 2 ? Ly : Lc;
-            mx_column(R, W, Lq, k == 0 ? st1 : (k == 1 ? st1 + 4u * kBS : st3), zo, e, F);
-            if (__builtin_expect(__ballot(e >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * k);
+            const mx_f2(&W)[4] = kc < 2 ? Wy : Wc;
+            const mx_f2(&Lq)[4] = kc < 2 ? Ly : Lc;
+            mx_column(R, W, Lq, kc == 0 ? st1 : (kc == 1 ? st1 + 4u * kBS : st3), zo, e, F);
+            if (__builtin_expect(__ballot(e >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * kc);
             em = __builtin_fmaxf(em, e);
         };
         mma_set(acc[0], A00, A01);
@@ -723,12 +724,19 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         __builtin_amdgcn_sched_barrier(0);
         acc[2][0] = mx_mma(A00, B[0][1], z);
         acc[2][2] = mx_mma(A01, B[0][1], z);
+#ifdef JX_MX_DBG_NOLO
+        acc[2][1] = z;
+        acc[2][3] = z;
+        acc[2][0] = mx_mma(A10, B[0][2], acc[2][0]);
+        acc[2][2] = mx_mma(A11, B[0][2], acc[2][2]);
+#else
         acc[2][1] = mx_mma(A00, B[1][1], z);
         acc[2][3] = mx_mma(A01, B[1][1], z);
         acc[2][0] = mx_mma(A10, B[0][2], acc[2][0]);
         acc[2][2] = mx_mma(A11, B[0][2], acc[2][2]);
         acc[2][1] = mx_mma(A10, B[1][2], acc[2][1]);
         acc[2][3] = mx_mma(A11, B[1][2], acc[2][3]);
+#endif
         if (kParts == 3) {
             acc[2][1] = mx_mma(A00, B[kParts - 1][1], acc[2][1]);
             acc[2][3] = mx_mma(A01, B[kParts - 1][1], acc[2][3]);
@@ -744,13 +752,12 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx_defer(L, sp, fl, b0, nq, ns, g, T);
         /* stores: channel c's 8 blocks x 128 B; always three store instructions (the vmcnt
          * accounting above counts on it) */
-        if (mx_simple_store(P, g, b0)) {
-            int16_t *ob = P.dst + lane * 8;
-            const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
+        if (cc.simple) {
+            const uint8_t *const ob = (const uint8_t *)(cc.dst + 512u * k);
 #pragma unroll
             for (int c = 0; c < 3; c++) {
                 const mx_u4 val = *(const mx_u4 *)(L.stage + mx_sb((unsigned)c) + ro);
-                __builtin_nontemporal_store(val, (mx_u4 *)(ob + (long long)c * g.nb * 64));
+                __builtin_nontemporal_store(val, (mx_u4 *)(ob + (c == 0 ? so0 : (c == 1 ? so1 : so2))));
             }
         } else {
             /* lanes past the launch's end (the clamped copies of the last block) store nothing;
@@ -759,10 +766,10 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             const unsigned l = mx_lane();
             const unsigned bl = b0 + (l >> 3), b = bl < g.total ? bl : g.total - 1u;
             const unsigned f = b / g.nb, bi = b - f * g.nb;
-            const uint32_t ro = (l >> 3) * kBS + (l & 7u) * 16u;
+            const uint32_t rl = (l >> 3) * kBS + (l & 7u) * 16u;
 #pragma unroll
             for (int c = 0; c < 3; c++) {
-                const mx_u4 val = *(const mx_u4 *)(L.stage + mx_sb((unsigned)c) + ro);
+                const mx_u4 val = *(const mx_u4 *)(L.stage + mx_sb((unsigned)c) + rl);
                 if (bl < g.total)
                     __builtin_nontemporal_store(
                         val, (mx_u4 *)(g.out + (long long)f * g.ofstride +
@@ -770,8 +777,13 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             }
         }
         mx_wave_sync();
-        mx_step(RC, P, g, nsteps, J);
-        slot = slot == kRing - 1u ? 0u : slot + 1u;
+        if (++k == kChunk) {
+            k = 0;
+            cc = nx;
+            if (cc.b0 >= g.total) break;
+        } else if (b0 + 8u >= g.total) {
+            break;
+        }
     }
     if (nq) mx_flush(L, nq, ns, g, T);
 }

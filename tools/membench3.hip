@@ -55,23 +55,37 @@ struct Q {
     unsigned *lq;
     __device__ __forceinline__ void fetch(const Args &a)
     {
-        if (QM == 0) { pend = wv + nw * (round++); return; }
-        if (QM == 4) {
+        if (QM == 0 || QM == 6 || QM == 8 || QM == 9) { pend = wv + nw * (round++); return; }
+        if (QM == 4 || QM == 10) {
             unsigned t0 = 0;
             if ((threadIdx.x & 63u) == 0) t0 = atomicAdd(lq, 1u);
             const unsigned t = __builtin_amdgcn_readfirstlane(t0);
+            if (QM == 10) {
+                /* the workgroup's t-th chunk: round r = t / W, m = t % W; the W chunks of a round
+                 * spread like W/4 four-wave workgroups' (groups of 4 consecutive chunks, 4 G apart) */
+                const unsigned W = nw / gridDim.x, r = t / W, mm = t - r * W;
+                pend = r * nw + (mm >> 2) * (4u * gridDim.x) + 4u * blockIdx.x + (mm & 3u);
+                return;
+            }
             const unsigned sc = a.nstatic, r = t / sc;
             pend = (blockIdx.x + gridDim.x * r) * sc + (t - r * sc);
             return;
         }
-        if (QM == 3) {
+        if (QM == 3 || QM == 7) {
             const unsigned k = wv + nw * round;
             if (k < a.nstatic) { round++; pend = k; return; }
+        }
+        if (QM == 7) {
+            const unsigned x = (unsigned)__builtin_amdgcn_s_getreg((2 << 11) | 20) & 7u;
+            unsigned v7 = 0;
+            if ((threadIdx.x & 63u) == 0) v7 = 0x80000000u | atomicAdd(a.ctr + 32 * x, 1u);
+            pend = v7;                              /* bit 31: a dynamic ticket */
+            return;
         }
         unsigned v = 0;
         if (QM == 5) {
             const unsigned x = (unsigned)__builtin_amdgcn_s_getreg((2 << 11) | 20) & 7u;
-            if ((threadIdx.x & 63u) == 0) v = atomicAdd(a.ctr + 32 * x, 1u);
+            if ((threadIdx.x & 63u) == 0) v = atomicAdd(a.ctr + a.base * x, 1u);
             pend = v;
             return;
         }
@@ -80,7 +94,13 @@ struct Q {
     }
     __device__ __forceinline__ unsigned take(const Args &a)
     {
-        if (QM == 0 || QM == 4) return pend;
+        if (QM == 0 || QM == 4 || QM == 6 || QM == 8 || QM == 9 || QM == 10) return pend;
+        if (QM == 7) {
+            const unsigned t = __builtin_amdgcn_readfirstlane(pend);
+            if (!(t & 0x80000000u)) return t;
+            const unsigned x = (unsigned)__builtin_amdgcn_s_getreg((2 << 11) | 20) & 7u;
+            return a.nstatic + 8u * (t & 0x7fffffffu) + x;
+        }
         const unsigned t = __builtin_amdgcn_readfirstlane(pend);
         if (QM == 5) {
             const unsigned x = (unsigned)__builtin_amdgcn_s_getreg((2 << 11) | 20) & 7u, G = a.nstatic;
@@ -96,7 +116,7 @@ __global__ __launch_bounds__(WPG * 64) void k_skel(Args a)
     static_assert(CH > DIST, "the issue cursor is at most one chunk ahead");
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
     __shared__ unsigned s_q;
-    if (QM == 4) {
+    if (QM == 4 || QM == 10) {
         if (threadIdx.x == 0) s_q = 0;
         __syncthreads();
     }
@@ -114,10 +134,10 @@ __global__ __launch_bounds__(WPG * 64) void k_skel(Args a)
     unsigned cc = q.take(a);                        /* compute chunk */
     if (cc >= nchunks) {
         if (a.ts && lane == 0) { a.ts[6 * wv] = 0; a.ts[6 * wv + 1] = 0; }
-        if (QM == 5) {
+        if (QM == 5 || QM == 7) {
             unsigned last = 0;
             if (lane == 0) last = atomicAdd(a.ctr + 256, 1u) == nw - 1;
-            if (__builtin_amdgcn_readfirstlane(last) && lane < 9) atomicExch(a.ctr + (lane == 8 ? 256 : 32 * lane), 0u);
+            if (__builtin_amdgcn_readfirstlane(last) && lane < 9) atomicExch(a.ctr + (lane == 8 ? 256 : a.base * lane), 0u);
         }
         return;
     }
@@ -194,6 +214,17 @@ __global__ __launch_bounds__(WPG * 64) void k_skel(Args a)
         }
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
+        if (QM == 6) asm volatile("s_barrier" ::: "memory");   /* lock-step within the workgroup */
+        if (QM == 8 || QM == 9) {
+            /* rotating priority: each wave of a CU gets the top priority a quarter of the time */
+            const unsigned ph = (QM == 8 ? (cc * CH + ck) : cc) + (wv >> 2) + (wv & 3);
+            switch (ph & 3) {
+            case 0: __builtin_amdgcn_s_setprio(0); break;
+            case 1: __builtin_amdgcn_s_setprio(1); break;
+            case 2: __builtin_amdgcn_s_setprio(2); break;
+            default: __builtin_amdgcn_s_setprio(3); break;
+            }
+        }
         slot = slot == DIST ? 0 : slot + 1;
         if (++ck == CH) {
             ck = 0;
@@ -202,12 +233,12 @@ __global__ __launch_bounds__(WPG * 64) void k_skel(Args a)
         }
     }
     if (acc[5].y == 3.0f) a.out[0] = 1;
-    if (QM == 5) {
+    if (QM == 5 || QM == 7) {
         /* the last wave to finish resets the counters for the next launch (stream order) */
         __builtin_amdgcn_s_waitcnt(0);
         unsigned last = 0;
         if (lane == 0) last = atomicAdd(a.ctr + 256, 1u) == nw - 1;
-        if (__builtin_amdgcn_readfirstlane(last) && lane < 9) atomicExch(a.ctr + (lane == 8 ? 256 : 32 * lane), 0u);
+        if (__builtin_amdgcn_readfirstlane(last) && lane < 9) atomicExch(a.ctr + (lane == 8 ? 256 : a.base * lane), 0u);
     }
     if (a.ts && lane == 0) {
         a.ts[6 * wv] = t0;
@@ -268,7 +299,7 @@ static void timeit(const char *name, L launch)
     fflush(stdout);
 }
 
-static unsigned g_ctr_val = 0;
+static unsigned g_ctr_val = 0, g_stride = 32;
 
 template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM, int WPG = 4>
 static void skel(int wpe, int grid_mult = 1, double static_frac = 0.0, int superchunk = 0)
@@ -292,7 +323,7 @@ static void skel(int wpe, int grid_mult = 1, double static_frac = 0.0, int super
     std::vector<unsigned long long> ts(6 * nw);
     timeit(name, [&](uint8_t *in, bool stamp) {
         if (stamp) CK(hipMemset(g_ts, 0, 6 * nw * sizeof(unsigned long long)));
-        Args a{in, g_out, nsteps, g_ctr, g_ctr_val, stamp ? g_ts : nullptr, nstatic};
+        Args a{in, g_out, nsteps, g_ctr, QM == 5 ? g_stride : (QM == 7 ? 32u : g_ctr_val), stamp ? g_ts : nullptr, nstatic};
         hipLaunchKernelGGL(kern, dim3(grid), dim3(WPG * 64), lds, 0, a);
         /* every wave ends with one failing dequeue: the counter moves by the dynamic chunks + nw */
         if (QM == 1 || QM == 3) g_ctr_val += (nchunks - nstatic) + nw;
@@ -345,6 +376,38 @@ static void skel(int wpe, int grid_mult = 1, double static_frac = 0.0, int super
                 i = j;
             }
             printf(" | %d CUs: mean in-CU spread %.1f, CU last-end %.1f..%.1f", ncu, spread / ncu, cmax_lo, cmax_hi);
+            /* by SIMD id, and by the wave's rank (by block index) among the CU's workgroups */
+            double ss[4] = {}, sn[4] = {};
+            std::vector<std::pair<unsigned long long, std::pair<unsigned, double>>> byc;   /* (cu key, (block, end)) */
+            for (unsigned w = 0; w < nw; w++) {
+                if (!ts[6 * w]) continue;
+                const unsigned hw = (unsigned)ts[6 * w + 3], x = (unsigned)ts[6 * w + 2] & 7u;
+                const double e = (ts[6 * w + 1] - mn) * 0.01;
+                ss[(hw >> 4) & 3] += e;
+                sn[(hw >> 4) & 3] += 1;
+                const unsigned long long key = (unsigned long long)x << 16 | ((hw >> 13) & 7u) << 8 | ((hw >> 8) & 15u);
+                byc.push_back({key, {w / WPG, e}});
+            }
+            printf(" | simd means");
+            for (int i = 0; i < 4; i++) printf(" %.0f", sn[i] ? ss[i] / sn[i] : -1.0);
+            std::sort(byc.begin(), byc.end());
+            double rs[8] = {}, rn[8] = {};
+            for (size_t i = 0; i < byc.size();) {
+                size_t j = i;
+                while (j < byc.size() && byc[j].first == byc[i].first) j++;
+                /* rank workgroups of this CU by block index */
+                std::vector<unsigned> blks;
+                for (size_t k = i; k < j; k++) blks.push_back(byc[k].second.first);
+                std::sort(blks.begin(), blks.end());
+                blks.erase(std::unique(blks.begin(), blks.end()), blks.end());
+                for (size_t k = i; k < j; k++) {
+                    const int rk = (int)(std::lower_bound(blks.begin(), blks.end(), byc[k].second.first) - blks.begin());
+                    if (rk < 8) { rs[rk] += byc[k].second.second; rn[rk] += 1; }
+                }
+                i = j;
+            }
+            printf(" | wg-rank means");
+            for (int i = 0; i < 8 && rn[i]; i++) printf(" %.0f", rs[i] / rn[i]);
         }
     });
 }
@@ -356,9 +419,9 @@ int main(int argc, char **argv)
     CK(hipMalloc(&g_in[0], in_bytes + 4096));
     CK(hipMalloc(&g_in[1], in_bytes + 4096));
     CK(hipMalloc(&g_out, 2 * in_bytes));
-    CK(hipMalloc(&g_ctr, 256));
+    CK(hipMalloc(&g_ctr, 8 << 20));          /* counters up to 1 MiB apart (8 XCDs) */
     CK(hipMalloc(&g_ts, 6 * 1024 * 1024 * sizeof(unsigned long long)));
-    CK(hipMemset(g_ctr, 0, 256));
+    CK(hipMemset(g_ctr, 0, 8 << 20));
     {
         std::vector<uint8_t> h(in_bytes);
         uint64_t z = 12345;
@@ -384,22 +447,12 @@ int main(int argc, char **argv)
     if (!strcmp(which, "all") || !strcmp(which, "a")) {
         skel<0, 0, 0, 4, 2, 1, 0>(3);
         skel<0, 0, 0, 4, 2, 1, 0>(3, 0);
-        skel<0, 0, 0, 4, 2, 1, 1>(3);
-        skel<0, 0, 0, 8, 2, 1, 1>(3);
-        skel<0, 0, 0, 16, 2, 1, 1>(3);
-        skel<0, 0, 0, 4, 2, 1, 5>(3, 1, 0, 1);
-        skel<0, 0, 0, 4, 2, 1, 5>(3, 1, 0, 4);
-        skel<0, 0, 0, 8, 2, 1, 5>(3, 1, 0, 1);
-        skel<0, 0, 0, 4, 2, 1, 5>(4, 1, 0, 1);
-        skel<0, 0, 0, 4, 2, 1, 5>(2, 1, 0, 1);
-    }
-    if (!strcmp(which, "all") || !strcmp(which, "b")) {
+        skel<0, 0, 0, 4, 2, 1, 10, 12>(3);
+        skel<0, 0, 0, 4, 2, 1, 10, 8>(2);
+        skel<0, 0, 0, 4, 2, 1, 10, 16>(4);
         skel<192, 16, 24, 4, 2, 1, 0>(3);
-        skel<192, 16, 24, 4, 2, 1, 0>(3, 0);
-        skel<192, 16, 24, 4, 2, 1, 5>(3, 1, 0, 1);
-        skel<192, 16, 24, 8, 2, 1, 5>(3, 1, 0, 1);
-        skel<192, 16, 24, 8, 2, 1, 1>(3);
-        skel<192, 16, 24, 4, 2, 1, 5>(4, 1, 0, 1);
+        skel<192, 16, 24, 4, 2, 1, 10, 12>(3);
+        skel<192, 16, 24, 4, 2, 1, 10, 16>(4);
     }
     return 0;
 }

@@ -46,7 +46,7 @@ struct Args {
     unsigned rounds_per_wg;        /* NP mode: consecutive rounds per workgroup (0 = static stride) */
 };
 
-template <int NLD, int NST, int NC, int NV, int NM, int NL, int ZERO>
+template <int NLD, int NST, int NC, int NV, int NM, int NL, int ZERO, int P4 = 0>
 __global__ __launch_bounds__((NLD + NST + NC) * 64) void k_spec(Args a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -80,15 +80,26 @@ __global__ __launch_bounds__((NLD + NST + NC) * 64) void k_spec(Args a)
             if (r < nr && k < NC) {
                 const unsigned s = gstep(r, k);
                 const uint8_t *b = a.in + (size_t)(s / kStepsPerRow) * 8 * kPitch + (s % kStepsPerRow) * 192u;
-                __builtin_amdgcn_global_load_lds((gp)(b + off0), (lp)(slot + k * kSlot), 16, 0, 0);
-                if (lane < 32) __builtin_amdgcn_global_load_lds((gp)(b + off1), (lp)(slot + k * kSlot + 1024), 16, 0, 0);
+                if (P4) {
+                    /* 4-byte pieces with per-lane source addresses: piece p = 64 j + lane is row
+                     * p / 48, dword p % 48 (the general-geometry form) */
+#pragma unroll
+                    for (int j = 0; j < 6; j++) {
+                        const unsigned pc = 64u * j + lane, y = pc / 48u, w = pc - 48u * y;
+                        __builtin_amdgcn_global_load_lds((gp)(b + y * kPitch + 4u * w), (lp)(slot + k * kSlot + 256 * j), 4, 0, 0);
+                    }
+                } else {
+                    __builtin_amdgcn_global_load_lds((gp)(b + off0), (lp)(slot + k * kSlot), 16, 0, 0);
+                    if (lane < 32) __builtin_amdgcn_global_load_lds((gp)(b + off1), (lp)(slot + k * kSlot + 1024), 16, 0, 0);
+                }
             } else {
-                __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
-                __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
+#pragma unroll
+                for (int j = 0; j < (P4 ? 6 : 2); j++)
+                    __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
             }
         }
     };
-    constexpr int kLdWait = 2 * kLdPer;            /* one round of DMA younger than the awaited one */
+    constexpr int kLdWait = (P4 ? 6 : 2) * kLdPer; /* one round of DMA younger than the awaited one */
     constexpr int kLdImm = (kLdWait & 15) | ((kLdWait >> 4) << 14) | 0xF70;
     /* storer: the 3 NC KiB pieces of round r, piece p = wave - NLD + NST * i */
     constexpr int kStPer = (3 * NC + NST - 1) / NST;
@@ -161,6 +172,146 @@ __global__ __launch_bounds__((NLD + NST + NC) * 64) void k_spec(Args a)
     }
 }
 
+/* Decoupled variant: no workgroup barrier; LDS sequence words hand the rings over.
+ *   ld_seq[i]   rounds loader i has landed          (computer k waits on loader k % NLD)
+ *   cp_seq[k]   rounds computer k has finished       (storers; loaders before reusing a slot)
+ *   st_seq[j]   rounds storer j has read out          (computers before reusing an output slot)
+ * Input ring NR slots (loaders run up to NR-1 rounds ahead), output ring NO slots. */
+__device__ __forceinline__ unsigned lds_ld(const unsigned *p)
+{
+    return __atomic_load_n(p, __ATOMIC_RELAXED);
+}
+__device__ __forceinline__ void lds_st(unsigned *p, unsigned v)
+{
+    __atomic_store_n(p, v, __ATOMIC_RELAXED);
+}
+
+template <int NLD, int NST, int NC, int NV, int NM, int NL, int ZERO, int NR, int NO, int AHEAD>
+__global__ __launch_bounds__((NLD + NST + NC) * 64) void k_spec2(Args a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *in_ring = lds;                        /* [NR][NC][kSlot] */
+    uint8_t *out_ring = lds + NR * NC * kSlot;     /* [NO][NC][kOut]  */
+    unsigned *seq = (unsigned *)(out_ring + NO * NC * kOut);   /* ld[NLD] cp[NC] st[NST] */
+    uint8_t *dummy = (uint8_t *)(seq + 64);
+    unsigned *ld_seq = seq, *cp_seq = seq + NLD, *st_seq = seq + NLD + NC;
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    if (threadIdx.x < 64) seq[threadIdx.x] = 0;
+    __syncthreads();
+    const unsigned nrounds_total = a.nsteps / NC;
+    const unsigned r0 = blockIdx.x, rstride = gridDim.x;
+    const unsigned nr = r0 < nrounds_total ? (nrounds_total - r0 + rstride - 1) / rstride : 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+    auto gstep = [&](unsigned r, unsigned k) { return (r0 + rstride * r) * NC + k; };
+    /* bounded spin: a protocol bug ends the kernel (garbage timing) instead of hanging it */
+    auto wait_ge = [&](const unsigned *p, unsigned n, unsigned target) {
+        for (unsigned it = 0; it < (1u << 21); it++) {
+            unsigned m = 0xffffffffu;
+            for (unsigned i = 0; i < n; i++) m = min(m, lds_ld(p + i));
+            if (m >= target) return;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (lane == 0) a.out[1] = 0x7777;              /* timed out: marks the output */
+    };
+    if (wave < NLD) {
+        /* loader: steps k = wave + NLD i of every round */
+        constexpr int kPer = (NC + NLD - 1) / NLD;
+        const uint32_t off0 = (lane / 12u) * kPitch + 16u * (lane % 12u);
+        const uint32_t off1 = ((64u + lane) / 12u) * kPitch + 16u * ((64u + lane) % 12u);
+        constexpr int kWait = 2 * kPer * (AHEAD - 1);
+        constexpr int kImm = (kWait & 15) | ((kWait >> 4) << 14) | 0xF70;
+        for (unsigned r = 0; r < nr + AHEAD - 1; r++) {
+            if (r < nr) {
+                if (r >= NR) wait_ge(cp_seq, NC, r - NR + 1);          /* slot r % NR free */
+                uint8_t *slot = in_ring + (r % NR) * NC * kSlot;
+#pragma unroll
+                for (int i = 0; i < kPer; i++) {
+                    const unsigned k = wave + NLD * i;
+                    if (k < NC) {
+                        const unsigned s = gstep(r, k);
+                        const uint8_t *b = a.in + (size_t)(s / kStepsPerRow) * 8 * kPitch + (s % kStepsPerRow) * 192u;
+                        __builtin_amdgcn_global_load_lds((gp)(b + off0), (lp)(slot + k * kSlot), 16, 0, 0);
+                        if (lane < 32) __builtin_amdgcn_global_load_lds((gp)(b + off1), (lp)(slot + k * kSlot + 1024), 16, 0, 0);
+                    } else {
+                        __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
+                        __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 2 * kPer; i++) __builtin_amdgcn_global_load_lds((gp)a.in, (lp)dummy, 4, 0, 0);
+            }
+            if (r + 1 >= AHEAD) {
+                __builtin_amdgcn_s_waitcnt(kImm);                   /* round r - AHEAD + 1 landed */
+                if (lane == 0) lds_st(ld_seq + wave, r - AHEAD + 2);
+            }
+        }
+    } else if (wave < NLD + NST) {
+        /* storer j: pieces pc = j + NST i of every round (3 per step) */
+        const unsigned j = wave - NLD;
+        constexpr int kPer = (3 * NC + NST - 1) / NST;
+        for (unsigned r = 0; r < nr; r++) {
+            wait_ge(cp_seq, NC, r + 1);
+            const uint8_t *slot = out_ring + (r % NO) * NC * kOut;
+#pragma unroll
+            for (int i = 0; i < kPer; i++) {
+                const unsigned pc = j + NST * i;
+                if (pc < 3 * NC) {
+                    const unsigned k = pc / 3, c = pc - 3 * k;
+                    const u4 v = *(const u4 *)(slot + k * kOut + c * 1024 + lane * 16);
+                    const unsigned s = gstep(r, k), f = s / kStepsPerFrame, bi = (s - f * kStepsPerFrame) * 8u;
+                    int16_t *o = a.out + (size_t)f * 3 * kNb * 64 + (size_t)c * kNb * 64 + (size_t)bi * 64 + lane * 8;
+                    __builtin_nontemporal_store(v, (u4 *)o);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);                   /* lgkmcnt(0): slot read out */
+            if (lane == 0) lds_st(st_seq + j, r + 1);
+        }
+    } else {
+        const unsigned cw = wave - NLD - NST, ldw = cw % NLD;
+        f2 acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) acc[i] = ZERO ? f2{0.0f, 0.0f} : f2{(float)lane, (float)i};
+        const f2 k1 = ZERO ? f2{0.0f, 0.0f} : f2{1.0001f, 0.9999f}, k2 = ZERO ? f2{0.0f, 0.0f} : f2{0.5f, 0.25f};
+        f4 macc[4] = {};
+        for (unsigned r = 0; r < nr; r++) {
+            wait_ge(ld_seq + ldw, 1, r + 1);
+            if (r >= NO) wait_ge(st_seq, NST, r - NO + 1);
+            const uint8_t *sp = in_ring + (r % NR) * NC * kSlot + cw * kSlot;
+            uint8_t *op = out_ring + (r % NO) * NC * kOut + cw * kOut;
+            const u4 d = *(const u4 *)(sp + (lane % 96) * 16);
+            if (!ZERO) {
+                acc[0].x += __uint_as_float(d.x & 0x3fffffffu);
+                acc[1].x += __uint_as_float(d.y & 0x3fffffffu);
+            }
+            h8 av = __builtin_bit_cast(h8, ZERO ? u4{0, 0, 0, 0} : d);
+#pragma unroll
+            for (int i = 0; i < NM; i++)
+                macc[i & 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, av, macc[i & 3], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < NV; i++)
+                asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(acc[i & 7]) : "v"(k1), "v"(k2));
+            if (NM) acc[2].x += macc[0].x + macc[1].y + macc[2].z + macc[3].w;
+#pragma unroll
+            for (int i = 0; i < NL; i++)
+                *(uint16_t *)(op + (i % 3) * 1024 + ((lane * 37u + (unsigned)i * 131u) & 511u) * 2u) =
+                    (uint16_t)(__float_as_uint(acc[i & 7].x) ^ (d.z >> (i & 15)));
+            if (NL == 0) *(u4 *)(op + lane * 16) = d;
+            __builtin_amdgcn_s_waitcnt(0xC07F);                   /* lgkmcnt(0) */
+            if (lane == 0) lds_st(cp_seq + cw, r + 1);
+        }
+        if (acc[5].y == 3.0f) a.out[0] = 1;
+    }
+    if (a.ts && lane == 0) {
+        const unsigned wg = blockIdx.x * (NLD + NST + NC) + wave;
+        a.ts[4 * wg] = t0;
+        a.ts[4 * wg + 1] = __builtin_amdgcn_s_memrealtime();
+        a.ts[4 * wg + 2] = c0;
+        a.ts[4 * wg + 3] = __builtin_amdgcn_s_memtime();
+    }
+}
+
 template <int NT>
 __global__ __launch_bounds__(256) void k_ideal(const u4 *__restrict__ in, u4 *__restrict__ out, size_t n)
 {
@@ -202,15 +353,15 @@ static void timeit(const char *name, L launch)
     fflush(stdout);
 }
 
-template <int NLD, int NST, int NC, int NV, int NM, int NL, int ZERO>
+template <int NLD, int NST, int NC, int NV, int NM, int NL, int ZERO, int P4 = 0>
 static void spec(unsigned rounds_per_wg = 0)
 {
     constexpr int NWV = NLD + NST + NC;
     char name[128];
-    snprintf(name, sizeof name, "spec ld%d st%d c%d v%d m%d l%d z%d rpw%u", NLD, NST, NC, NV, NM, NL, ZERO, rounds_per_wg);
+    snprintf(name, sizeof name, "spec ld%d st%d c%d v%d m%d l%d z%d p4%d rpw%u", NLD, NST, NC, NV, NM, NL, ZERO, P4, rounds_per_wg);
     const size_t lds = 3 * NC * kSlot + 2 * NC * kOut + 256;
     if (lds > 160 * 1024) { printf("%s: LDS %zu too big\n", name, lds); return; }
-    auto kern = k_spec<NLD, NST, NC, NV, NM, NL, ZERO>;
+    auto kern = k_spec<NLD, NST, NC, NV, NM, NL, ZERO, P4>;
     CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024)));
     const unsigned nsteps = 8 * kStepsPerFrame / NC * NC, nrt = nsteps / NC;
     const unsigned grid = rounds_per_wg ? (nrt + rounds_per_wg - 1) / rounds_per_wg : g_cus;
@@ -232,6 +383,44 @@ static void spec(unsigned rounds_per_wg = 0)
             std::sort(clk.begin(), clk.end());
             printf("  | ends p1 %.1f p50 %.1f max %.1f | clk p50 %.0f", ends[ends.size() / 100], ends[ends.size() / 2],
                    ends.back(), clk.empty() ? 0.0 : clk[clk.size() / 2]);
+        }
+    });
+}
+
+template <int NLD, int NST, int NC, int NV, int NM, int NL, int ZERO, int NR, int NO, int AHEAD>
+static void spec2()
+{
+    constexpr int NWV = NLD + NST + NC;
+    char name[128];
+    snprintf(name, sizeof name, "spec2 ld%d st%d c%d v%d m%d l%d z%d nr%d no%d ah%d", NLD, NST, NC, NV, NM, NL, ZERO,
+             NR, NO, AHEAD);
+    const size_t lds = NR * NC * kSlot + NO * NC * kOut + 256 + 256;
+    if (lds > 160 * 1024) { printf("%s: LDS %zu too big\n", name, lds); return; }
+    auto kern = k_spec2<NLD, NST, NC, NV, NM, NL, ZERO, NR, NO, AHEAD>;
+    CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024)));
+    const unsigned nsteps = 8 * kStepsPerFrame / NC * NC;
+    const unsigned grid = g_cus;
+    std::vector<unsigned long long> ts(4 * (size_t)grid * NWV);
+    timeit(name, [&](uint8_t *in, bool stamp) {
+        Args a{in, g_out, nsteps, stamp ? g_ts : nullptr, 0};
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(NWV * 64), 160 * 1024, 0, a);
+        if (stamp) {
+            CK(hipMemcpy(ts.data(), g_ts, ts.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long mn = ~0ull;
+            std::vector<double> clk, ends;
+            for (size_t w = 0; w < (size_t)grid * NWV; w++) mn = std::min(mn, ts[4 * w]);
+            for (size_t w = 0; w < (size_t)grid * NWV; w++) {
+                ends.push_back((ts[4 * w + 1] - mn) * 0.01);
+                const double dr = (double)(ts[4 * w + 1] - ts[4 * w]);
+                if (dr > 500) clk.push_back((double)(ts[4 * w + 3] - ts[4 * w + 2]) / dr * 100.0);
+            }
+            std::sort(ends.begin(), ends.end());
+            std::sort(clk.begin(), clk.end());
+            printf("  | ends p1 %.1f p50 %.1f max %.1f | clk p50 %.0f", ends[ends.size() / 100], ends[ends.size() / 2],
+                   ends.back(), clk.empty() ? 0.0 : clk[clk.size() / 2]);
+            int16_t mark = 0;
+            CK(hipMemcpy(&mark, g_out + 1, 2, hipMemcpyDeviceToHost));
+            if (mark == 0x7777) printf(" | SPIN TIMEOUT");
         }
     });
 }
@@ -265,18 +454,17 @@ int main(int argc, char **argv)
     timeit("ideal_np_nt", [&](uint8_t *in, bool) {
         hipLaunchKernelGGL(k_ideal<1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, (const u4 *)in, (u4 *)g_out, n);
     });
-    /* memory only */
-    spec<1, 2, 9, 0, 0, 0, 0>();
-    spec<2, 2, 8, 0, 0, 0, 0>();
-    spec<2, 4, 10, 0, 0, 0, 0>();
-    spec<1, 2, 9, 0, 0, 0, 0>(4);
-    spec<1, 2, 9, 0, 0, 0, 0>(16);
-    /* with compute */
-    spec<1, 2, 9, 192, 16, 24, 0>();
-    spec<1, 2, 9, 192, 16, 24, 1>();
-    spec<2, 2, 8, 192, 16, 24, 0>();
-    spec<2, 4, 10, 192, 16, 24, 0>();
-    spec<1, 2, 9, 128, 16, 24, 0>();
-    spec<1, 2, 9, 192, 16, 24, 0>(16);
+    const char *which = argc > 1 ? argv[1] : "all";
+    if (!strcmp(which, "all") || !strcmp(which, "a")) {
+        spec<2, 2, 8, 0, 0, 0, 0>();
+        spec2<2, 2, 8, 0, 0, 0, 0, 4, 3, 3>();
+        spec2<1, 3, 8, 0, 0, 0, 0, 4, 3, 3>();
+        spec2<2, 2, 8, 192, 16, 24, 0, 4, 3, 3>();
+        spec2<2, 2, 8, 192, 16, 24, 1, 4, 3, 3>();
+        spec2<2, 2, 8, 128, 16, 24, 0, 4, 3, 3>();
+        spec2<2, 2, 12, 192, 16, 24, 0, 3, 2, 2>();
+        spec2<1, 3, 12, 192, 16, 24, 0, 3, 2, 2>();
+        spec2<2, 2, 8, 192, 16, 24, 0, 5, 3, 4>();
+    }
     return 0;
 }
