@@ -1385,13 +1385,8 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
         return rc;
     }
     if (sub && p->sample_ratio == 1 && !kAltDispatch) {
-        /* true 4:2:2 in one pass (k_sub422): chroma geometry as k_chroma's below */
-        jx_geom gc = xa.g;
-        gc.bpr = fr->width / 16;
-        gc.nb = (int)nbc;
-        gc.out = d_out + (long long)nb * 64 - (long long)nbc * 64;
-        hipLaunchKernelGGL(k_sub422, dim3(grid), dim3(JX_WG), 0, s, xa, gc);
-        rc = hip_rc(hipGetLastError());
+        /* true 4:2:2 in one pass on the matrix cores (k_mx422, csrc/jpgx_mx.hip) */
+        rc = jx_launch_mx422(&xa, stream);
         if (!rc && event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
         return rc;
     }

@@ -13,8 +13,8 @@
  *   Input   the step's 8 pixel rows x 8 blocks x 24 B land in a 1.5-KiB LDS slot ([y][24 jb + k])
  *           by LDS-DMA (16-byte pieces), issued two steps ahead (3-slot ring).
  *   Rows    set s (blocks 4s..4s+3), half h (pixel rows 4h..4h+3): a 16 x 32 f16 A operand,
- *           row m = 4 jb + y, k = byte k of the pixel row (b - 128, exact in f16; k = 24 the
- *           bias 1.0).  One product with B = colour x cosine gives, in C row m, column j, the
+ *           row m = 4 jb + y, k = byte k of the pixel row (zero-extended: the f16 b 2^-24,
+ *           exact, one v_perm per two bytes; k = 24 the bias 1.0).  One product with B = colour x cosine gives, in C row m, column j, the
  *           row transform of channel j/8 (Y, Cb), frequency u = j%8.  Cr: the two sets
  *           concatenated along K (B zero outside its set's columns), so column j of the Cr tile
  *           is set j/8's Cr at u = j%8.  B = Bh + 2^-12 Bl (JX_MX_PARTS = 2 f16 parts; 3 adds a
@@ -130,15 +130,18 @@ __device__ __forceinline__ unsigned mx_lane()
     return l;
 }
 
-/* Two pixel bytes -> two f16 (b - 128): perm makes 0x64bb (= 1024 + b) from each byte of d
- * (K = 0x64806481 supplies 0x64, and for the bias lanes 0x81 / 0x80 = 1153 / 1152, i.e. 1.0 /
- * 0.0 after the subtraction), then one packed subtraction, exact. */
+/* Two pixel bytes -> two f16: one perm zero-extends each selected byte of d to 16 bits, the
+ * f16 subnormal b 2^-24 (exact; jpgx_plan.cpp stores B's byte rows x 2^15, so the products are
+ * b B 2^-9).  Selector byte 0x0c gives 0x00; for the bias lanes 0x05 picks 0x3C from K, i.e.
+ * the f16 1.0 (0x3C00).  Data: 0x0c010c00 (bytes 0, 1) / 0x0c030c02 (2, 3); bias 1.0, 0.0:
+ * 0x0c0c050c; zeros 0x0c0c0c0c. */
 __device__ __forceinline__ uint32_t mx_cvt2(uint32_t d, uint32_t sel)
 {
-    const mx_h2 v = __builtin_bit_cast(mx_h2, __builtin_amdgcn_perm(0x64806481u, d, sel)) -
-                    (mx_h2){(_Float16)1152.0f, (_Float16)1152.0f};
-    return __builtin_bit_cast(uint32_t, v);
+    return __builtin_amdgcn_perm(0x00003C00u, d, sel);
 }
+constexpr uint32_t kSelLo = 0x0c010c00u, kSelHi = 0x0c030c02u, kSelOne = 0x0c0c050cu, kSelZero = 0x0c0c0c0cu;
+/* the MFMA results are R 2^-9 (jpgx_plan.cpp kMxBiasExp): the quantiser's w carries 2^9 */
+constexpr float kRScale = 512.0f;
 
 __device__ __forceinline__ mx_h8 mx_aop(mx_u2 d, uint32_t s0, uint32_t s1, uint32_t s2)
 {
@@ -220,12 +223,14 @@ __device__ __forceinline__ bool mx_simple_load(const MxCur &p, const MxG &g, uns
 #define JX_MX_CHUNK 4
 #endif
 constexpr unsigned kChunk = JX_MX_CHUNK;
-static_assert(kChunk == 4 && kDist == 2, "the ring holds one chunk: step k of a chunk in slot k");
+static_assert(kChunk == 4 && (kDist == 2 || kDist == 3),
+              "the ring holds one chunk: step k of a chunk in slot k, at most 3 steps ahead");
 struct MxChunk {
     unsigned b0;                        /* first block (launch-global); >= total: none        */
     unsigned f, bi, r, c;               /* frame, block in frame, block-row, column of b0      */
     const uint8_t *src;                 /* pixel (8c, 8r) of frame f                           */
     int16_t *dst;                       /* frame f's channel-0 output of block bi              */
+    int16_t *cdst;                      /* k_mx422: frame f's Cb output of chroma block bi / 2 */
     bool simple;
 };
 struct MxJump {
@@ -236,6 +241,7 @@ __device__ __forceinline__ void mx_chunk_ptrs(MxChunk &C, const MxG &g)
 {
     C.src = g.rgb + (long long)C.f * g.fstride + 8ll * C.r * g.pitch + 24ll * C.c;
     C.dst = g.out + (long long)C.f * g.ofstride + 64ll * C.bi;
+    C.cdst = g.out + (long long)C.f * g.ofstride + 64ll * (g.nb + C.bi / 2u);
     C.simple = C.b0 + 32u <= g.total && C.c + 32u < g.bpr && g.lin_store;
 }
 
@@ -331,7 +337,8 @@ __device__ __forceinline__ double mx_shr1(double s)
 /* n padding VMEM operations (4-byte LDS-DMA of the input's first bytes into L.dummy): they keep
  * the number of VMEM operations per step constant, so that one vmcnt(8) always waits for exactly
  * the step's own DMA */
-__device__ __forceinline__ void mx_pad(const MxG &g, MxLds &L, int n)
+template <class Lds>
+__device__ __forceinline__ void mx_pad(const MxG &g, Lds &L, int n)
 {
     for (int i = 0; i < n; i++)
         __builtin_amdgcn_global_load_lds((mx_gp)g.rgb, (mx_lp)L.dummy, 4, 0, 0);
@@ -345,6 +352,25 @@ __device__ __forceinline__ void mx_pad(const MxG &g, MxLds &L, int n)
  * transposed divisor (quantise.c:58).  px = the block's pixel row 0, rows rs bytes apart.  The
  * result is valid in lane x == 7.
  */
+/* the x-outer / y-inner sum of the products (lane x holds the 8 of its x), F and round(F / Q):
+ * valid in lane x == 7 */
+__device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch, unsigned u, unsigned v,
+                                            unsigned x, const jx_mxtab &T)
+{
+    double sum = 0.0;
+#pragma unroll
+    for (int xx = 0; xx < 8; xx++) {
+        if ((int)x == xx) {
+#pragma unroll
+            for (int y = 0; y < 8; y++) sum += prod[y];
+        }
+        if (xx < 7) sum = mx_shr1(sum);
+    }
+    const double F = kMxQuarterAlpha[u] * kMxAlpha[v] * sum;
+    const int q = T.q[ch == 0 ? 0 : 1][u * 8 + v];
+    return (int)round(F / (double)q);
+}
+
 __device__ __forceinline__ int mx_exact_coef(const lds_u8 *px, unsigned rs, unsigned ch, unsigned u,
                                              unsigned v, unsigned x, const jx_mxtab &T)
 {
@@ -360,18 +386,7 @@ __device__ __forceinline__ int mx_exact_coef(const lds_u8 *px, unsigned rs, unsi
         const double X = (Ac + Sc * tt) - 128.0;
         prod[y] = X * cu * kMxCos[v][y];
     }
-    double sum = 0.0;
-#pragma unroll
-    for (int xx = 0; xx < 8; xx++) {
-        if ((int)x == xx) {
-#pragma unroll
-            for (int y = 0; y < 8; y++) sum += prod[y];
-        }
-        if (xx < 7) sum = mx_shr1(sum);
-    }
-    const double F = kMxQuarterAlpha[u] * kMxAlpha[v] * sum;
-    const int q = T.q[ch == 0 ? 0 : 1][u * 8 + v];
-    return (int)round(F / (double)q);
+    return mx_exact_sum(prod, ch, u, v, x, T);
 }
 
 __device__ __forceinline__ lds_u8 *mx_lds(void *p) { return (lds_u8 *)p; }
@@ -591,9 +606,9 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
      * half), k-group q = lane >> 4 (bytes 8q..8q+7; q = 3: the bias) */
     const unsigned m = lane & 15u, q = lane >> 4;
     const uint32_t aoff = 192u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 0u);
-    const uint32_t s0 = q < 3 ? 0x05010500u : 0x07060504u;
-    const uint32_t s1 = q < 3 ? 0x05030502u : 0x07060706u;
-    const uint32_t s2 = q < 3 ? 0x05010500u : 0x07060706u;
+    const uint32_t s0 = q < 3 ? kSelLo : kSelOne;
+    const uint32_t s1 = q < 3 ? kSelHi : kSelZero;
+    const uint32_t s2 = q < 3 ? kSelLo : kSelZero;
     /* DMA pieces p = lane, 64 + lane: pixel row p / 12, bytes 16 (p % 12) of the step's row */
     const uint32_t off0 = (uint32_t)((lane / 12u) * (unsigned)g.pitch + 16u * (lane % 12u));
     const uint32_t off1 = (uint32_t)(((64u + lane) / 12u) * (unsigned)g.pitch + 16u * ((64u + lane) % 12u));
@@ -624,6 +639,7 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     for (int p = 0; p < kParts; p++)
 #pragma unroll
         for (int w = 0; w < 3; w++) B[p][w] = g_mxB[3 * p + w][lane];
+    __builtin_amdgcn_s_waitcnt(0xF70);              /* see k_mx422 */
 
     /* chunks: cc (computed now), nc2 (the next one; its first two steps are issued during cc's
      * last two) */
@@ -654,10 +670,10 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     };
     /* prologue: steps 0 and 1, each followed by three padding operations in place of the stores
      * of the (absent) steps before the first */
-    issue(cc, 0);
-    mx_pad(g, L, 3);
-    issue(cc, 1);
-    mx_pad(g, L, 3);
+    for (unsigned d = 0; d < kDist; d++) {
+        issue(cc, d);
+        mx_pad(g, L, 3);
+    }
     int nq = 0, ns = 0;                            /* deferred exact tasks, their blocks */
     unsigned k = 0;                                /* step of cc */
     for (;;) {
@@ -669,12 +685,12 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         __builtin_amdgcn_s_waitcnt(kWaitImm);
         mx_wave_sync();
         const uint8_t *const sp = L.ring[k];
-        /* the step after next: step k + 2 of this chunk, or step k - 2 of the next */
-        if (k < 2) {
-            issue(cc, k + 2);
+        /* the step kDist ahead: step k + kDist of this chunk, or of the next */
+        if (k + kDist < kChunk) {
+            issue(cc, k + kDist);
         } else {
-            if (k == 2) mx_chunk_next(nx, g, J);
-            issue(nx, k - 2);
+            if (k + kDist == kChunk) mx_chunk_next(nx, g, J);
+            issue(nx, k + kDist - kChunk);
         }
         /* A operands: set 0/1 x half lo/hi */
         const mx_u2 d00 = *(const mx_u2 *)(sp + aoff);
@@ -788,6 +804,511 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     if (nq) mx_flush(L, nq, ns, g, T);
 }
 
+/* ==== k_mx422: true 4:2:2 (extension, JPGX_FLAG_SUBSAMPLE, sample_ratio 1) ==================
+ *
+ * The same persistent chunk loop, LDS-DMA ring and per-step bookkeeping as k_mx; a step is 8 Y
+ * blocks = 4 MCUs (chroma block cb of the step = Y blocks 2 cb, 2 cb + 1: W is a multiple of 16
+ * and steps start at multiples of 8, so an MCU never straddles a step or a block-row).
+ *   Y       k_mx's Y row transform with the two sets concatenated along K (B_Y0 zero in columns
+ *           8..15, B_Y1 in 0..7): column j of the C tile is set j / 8's Y at u = j % 8.
+ *   Chroma  A row m = chroma block m >> 2, pixel row m & 3 of the half, K = the 48 bytes of the
+ *           MCU's pixel row + the bias, over two K = 32 products; B (jpgx_plan.cpp
+ *           jx_mx422_operands) holds 0.5 a[c][p] cos((2 floor(x/2) + 1) u pi/16), so column j is
+ *           the row transform of the pair-averaged level-shifted chroma: Cb (j < 8) or Cr of
+ *           chroma block gq at u = j % 8.  Same hi / lo split and rigorous band
+ *           (jx_plan_tables_mx422: 65 fp32 additions per lo part instead of 33).
+ *   Columns each lane holds two: Y and chroma -> 16 MFMAs and 2 x 8 column DCTs per step (k_mx:
+ *           16 and 3 x 8), output 1 KiB Y + 512 B Cb + 512 B Cr in two stores (lanes 0..31 Cb,
+ *           32..63 Cr).
+ *   Quirk   the x0 = -8 quirk shifts a row-last Y block's rows by one (Y only); a general step
+ *           holding such a block loads the block's true rows into L.qtrue for its chroma block.
+ *   Exact   deferred / inline as k_mx; a chroma task carries the MCU's 8 x 48 bytes (two side
+ *           slots) and follows the oracle's definition (oracle/cpu_ref.c cpuref_chroma_sample,
+ *           dct_coef): X = (ls(2X) + ls(2X+1)) * 0.5, ls = the level-shifted chroma in
+ *           preprocess.c's operation order.
+ */
+#ifndef JX_DBG_NOQ
+#define JX_DBG_NOQ 0
+#endif
+constexpr unsigned kVmWait422 = 4 * kDist - 2;    /* 2 stores x kDist steps + 2 DMA x (kDist - 1) */
+constexpr int kWaitImm422 = (int)((kVmWait422 & 15u) | ((kVmWait422 >> 4) << 14) | 0xF70u);
+
+struct Mx422Lds {
+    uint8_t ring[kRing][kSlot];
+    uint8_t stage[kStageBytes];         /* Cb block cb at mx_sb(0) + 144 cb, Cr at mx_sb(1) + ..,
+                                           Y block jb at mx_sb(2) + 144 jb                       */
+    uint8_t qtrue[4][192];              /* general step: true rows [y][24] of row-last block 2cb+1 */
+    uint8_t pix[kSide][192];            /* deferred blocks: Y [y][24] in one slot, an MCU [y][48]
+                                           in two                                                */
+    uint32_t sblk[kSide];               /* launch-global Y block (an MCU: its left block)        */
+    uint16_t dtask[kSide];              /* slot << 8 | ch << 6 | v << 3 | u                      */
+    uint16_t task[8];
+    uint32_t dummy[64];
+};
+static_assert(sizeof(Mx422Lds) * 4 * 3 <= 160 * 1024, "3 workgroups of 4 waves per CU");
+
+__device__ mx_u4 g_mx422B[JX_MX_PARTS * 4][64];  /* [part * 4 + which][lane] */
+__device__ jx_mxtab g_mx422tab[2][JX_MAXQ + 1];  /* n = 8 c + u: c = 0 Y, 1 Cb, 2 Cr */
+
+/* Y block of a lane's Y column (lane (gq, j): set j / 8) */
+__device__ __forceinline__ unsigned mx422_yblock(unsigned sl)
+{
+    return (sl & 15u) < 8 ? (sl >> 4) : 4u + (sl >> 4);
+}
+
+/*
+ * One exact coefficient per 8-lane group from pixel pairs: lane x's samples are the averages
+ * (X(p) + X(p + d1)) * 0.5 over rows y of p = row0 + rs y, X = the level-shifted channel value
+ * in the reference's colour arithmetic.  Chroma (4:2:2): p = pixel 2x, d1 = 3 (the extension's
+ * definition, oracle/cpu_ref.c cpuref_chroma_sample); Y: p = pixel x, d1 = 0 ((X + X) * 0.5 == X
+ * exactly, so Y tasks share the code).  Valid in lane x == 7.
+ */
+__device__ __forceinline__ int mx_exact_pair(const lds_u8 *row0, unsigned rs, unsigned d1, unsigned ch,
+                                             unsigned u, unsigned v, unsigned x, const jx_mxtab &T)
+{
+    const double cu = kMxCos[u][x];
+    const double k0c = kMxColour[ch][0], k1c = kMxColour[ch][1], k2c = kMxColour[ch][2];
+    const double Ac = kMxColour[ch][3], Sc = kMxColour[ch][4];
+    double prod[8];
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+        const lds_u8 *p = row0 + rs * (unsigned)y, *p1 = p + d1;
+        const double t0 = (k0c * (double)p[0] + k1c * (double)p[1]) + k2c * (double)p[2];
+        const double t1 = (k0c * (double)p1[0] + k1c * (double)p1[1]) + k2c * (double)p1[2];
+        const double X = (((Ac + Sc * t0) - 128.0) + ((Ac + Sc * t1) - 128.0)) * 0.5;
+        prod[y] = X * cu * kMxCos[v][y];
+    }
+    return mx_exact_sum(prod, ch, u, v, x, T);
+}
+
+/* lane x's first pixel (row 0) and row stride of chroma block cb in a step's slot; the right
+ * Y block's rows come from L.qtrue when it is a row-last block (bit cb of qmask) */
+__device__ __forceinline__ const lds_u8 *mx422_mcu_row0(Mx422Lds &L, const uint8_t *sp, uint32_t qmask,
+                                                        unsigned cb, unsigned x, unsigned &rs)
+{
+    const bool q = ((qmask >> cb) & 1u) && x >= 4;
+    rs = q ? 24u : 192u;
+    return q ? mx_lds(L.qtrue[cb]) + 6u * (x - 4u) : mx_lds((void *)sp) + 48u * cb + 6u * x;
+}
+
+/* Inline exact pass of one step: bit 8 col + v of a lane's bits (col 0 Y, 1 chroma) */
+__device__ __forceinline__ void mx422_exact_inline(Mx422Lds &L, const uint8_t *sp, uint32_t qmask,
+                                                   uint32_t bits, const jx_mxtab &T)
+{
+    const unsigned lane = mx_lane();
+    mx_wave_sync();
+    for (;;) {
+        const uint64_t act = __ballot(bits != 0);
+        if (!act) break;
+        const int rk = mx_rank(act);
+        if (bits != 0 && rk < 8) {
+            const unsigned b = (unsigned)__builtin_ctz(bits);
+            bits &= bits - 1u;
+            L.task[rk] = (uint16_t)(lane << 8 | b);
+        }
+        mx_wave_sync();
+        const int nt = std::min((int)__popcll(act), 8);
+        const unsigned i = lane >> 3, x = lane & 7u;
+        const bool live = (int)i < nt;
+        const unsigned code = L.task[live ? i : 0u];
+        const unsigned sl = code >> 8, k = (code >> 3) & 1u, v = code & 7u;
+        const unsigned jj = sl & 15u, u = jj & 7u;
+        unsigned ch, rs, d1, st;
+        const lds_u8 *row0;
+        if (k == 0) {
+            const unsigned jb = mx422_yblock(sl);
+            ch = 0;
+            rs = 192u;
+            d1 = 0;
+            row0 = mx_lds((void *)sp) + 24u * jb + 3u * x;
+            st = mx_sb(2) + kBS * jb;
+        } else {
+            const unsigned cb = sl >> 4;
+            ch = 1u + (jj >> 3);
+            d1 = 3;
+            row0 = mx422_mcu_row0(L, sp, qmask, cb, x, rs);
+            st = mx_sb(jj >> 3) + kBS * cb;
+        }
+        const int val = mx_exact_pair(row0, rs, d1, ch, u, v, x, T);
+        if (live && x == 7)
+            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + st +
+                                                           2u * (unsigned)kMxScan[v][u]) = (int16_t)val;
+        mx_wave_sync();
+    }
+}
+
+__device__ __forceinline__ void mx422_flush(Mx422Lds &L, int &nq, int &ns, const MxG &g, const jx_mxtab &T)
+{
+    __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0): the tasks' blocks are stored */
+    mx_wave_sync();
+    const unsigned lane = mx_lane(), i = lane >> 3, x = lane & 7u;
+    const bool live = (int)i < nq;
+    const unsigned code = L.dtask[live ? i : 0u];
+    const unsigned slot = code >> 8, ch = (code >> 6) & 3u, v = (code >> 3) & 7u, u = code & 7u;
+    const lds_u8 *px = mx_lds(L.pix[slot]);
+    const int val = ch == 0 ? mx_exact_pair(px + 3u * x, 24u, 0u, 0u, u, v, x, T)
+                            : mx_exact_pair(px + 6u * x, 48u, 3u, ch, u, v, x, T);
+    if (live && x == 7) {
+        const unsigned b = L.sblk[slot], f = b / g.nb, bi = b - f * g.nb;
+        const long long blk = ch == 0 ? (long long)bi : (long long)g.nb + (ch - 1u) * (g.nb / 2u) + bi / 2u;
+        g.out[(long long)f * g.ofstride + blk * 64 + kMxScan[v][u]] = (int16_t)val;
+    }
+    mx_wave_sync();
+    nq = 0;
+    ns = 0;
+}
+
+/* A step with flagged coefficients: queue them with their blocks' pixels (Y: one side slot per
+ * block; an MCU: two), flushing first if the queue would overflow; inline if the step alone
+ * would. */
+__device__ __forceinline__ void mx422_defer(Mx422Lds &L, const uint8_t *sp, uint32_t qmask, uint32_t bits,
+                                            unsigned b0, int &nq, int &ns, const MxG &g, const jx_mxtab &T)
+{
+    const unsigned lane = mx_lane();
+    if (b0 + 8u > g.total) {                           /* clamped copies past the end (even count) */
+        const unsigned nvalid = g.total - b0;
+        if (mx422_yblock(lane) >= nvalid) bits &= ~0xffu;
+        if (2u * (lane >> 4) >= nvalid) bits &= ~0xff00u;
+    }
+    const uint64_t m0 = __ballot((bits & 0xffu) != 0), m1 = __ballot((bits & 0xff00u) != 0);
+    uint32_t yblk = 0, cblk = 0;
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) {
+        yblk |= (((m0 >> (16 * gq)) & 0xffu) ? 1u : 0u) << gq;
+        yblk |= (((m0 >> (16 * gq + 8)) & 0xffu) ? 1u : 0u) << (4 + gq);
+        cblk |= (((m1 >> (16 * gq)) & 0xffffu) ? 1u : 0u) << gq;
+    }
+    const unsigned cnt = (unsigned)__popc(bits);
+    unsigned incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned o = __shfl_up(incl, d, 64);
+        if ((int)lane >= d) incl += o;
+    }
+    const int ntask = (int)__builtin_amdgcn_readlane(incl, 63);
+    const int ny = __popc(yblk), nslot = ny + 2 * __popc(cblk);
+    if (nq + ntask > kSide || ns + nslot > kSide) {
+        if (nq) mx422_flush(L, nq, ns, g, T);
+        if (ntask > kSide || nslot > kSide) {
+            mx422_exact_inline(L, sp, qmask, bits, T);
+            return;
+        }
+    }
+    /* copy the pixel rows (lane < 48: row l / 6, dword l % 6) */
+    {
+        const unsigned y = lane / 6u, k = lane - 6u * y;
+        uint32_t bm = yblk;
+        int t = ns;
+        while (bm) {
+            const unsigned jb = (unsigned)__builtin_ctz(bm);
+            bm &= bm - 1u;
+            if (lane < 48)
+                *(__attribute__((address_space(3))) uint32_t *)(mx_lds(L.pix[t]) + 24u * y + 4u * k) =
+                    *(const __attribute__((address_space(3))) uint32_t *)(mx_lds((void *)sp) + 192u * y + 24u * jb + 4u * k);
+            if (lane == 0) L.sblk[t] = b0 + jb;
+            t++;
+        }
+        bm = cblk;
+        while (bm) {
+            const unsigned cb = (unsigned)__builtin_ctz(bm);
+            bm &= bm - 1u;
+            if (lane < 48) {
+                typedef __attribute__((address_space(3))) uint32_t l32;
+                const lds_u8 *left = mx_lds((void *)sp) + 192u * y + 48u * cb;
+                const lds_u8 *right = ((qmask >> cb) & 1u) ? mx_lds(L.qtrue[cb]) + 24u * y : left + 24u;
+                lds_u8 *d = mx_lds(L.pix[t]) + 48u * y + 4u * k;
+                *(l32 *)d = *(const l32 *)(left + 4u * k);
+                *(l32 *)(d + 24) = *(const l32 *)(right + 4u * k);
+            }
+            if (lane == 0) L.sblk[t] = b0 + 2u * cb;
+            t += 2;
+        }
+    }
+    {
+        unsigned pos = (unsigned)nq + incl - cnt;
+        const unsigned jj = lane & 15u, u = jj & 7u;
+        while (bits) {
+            const unsigned b = (unsigned)__builtin_ctz(bits);
+            bits &= bits - 1u;
+            const unsigned v = b & 7u;
+            unsigned slot, ch;
+            if (b < 8) {
+                const unsigned jb = mx422_yblock(lane);
+                slot = (unsigned)ns + (unsigned)__popc(yblk & ((1u << jb) - 1u));
+                ch = 0;
+            } else {
+                const unsigned cb = lane >> 4;
+                slot = (unsigned)(ns + ny) + 2u * (unsigned)__popc(cblk & ((1u << cb) - 1u));
+                ch = 1u + (jj >> 3);
+            }
+            L.dtask[pos++] = (uint16_t)(slot << 8 | ch << 6 | v << 3 | u);
+        }
+    }
+    mx_wave_sync();
+    nq += ntask;
+    ns += nslot;
+}
+
+/* the rare paths end with their loads complete (the exact pass's constant-table loads), so the
+ * compiler's wait for them does not land in the hot path of the next step */
+__device__ __forceinline__ void mx422_defer_step(Mx422Lds &L, const uint8_t *sp, uint32_t qmask, uint32_t bits,
+                                                 unsigned b0, int &nq, int &ns, const MxG &g, const jx_mxtab &T)
+{
+    mx422_defer(L, sp, qmask, bits, b0, nq, ns, g, T);
+    __builtin_amdgcn_s_waitcnt(0xF70);
+}
+
+/* a general step's row-last Y blocks (always odd: bpr is even): their true pixel rows 8r..8r+7
+ * into L.qtrue[cb]; returns the mask of chroma blocks cb that have one */
+__device__ __forceinline__ uint32_t mx422_true_rows(Mx422Lds &L, const MxG &g, unsigned b0)
+{
+    const unsigned l = mx_lane(), y = l & 7u, cb = (l >> 3) & 3u;
+    const unsigned b = b0 + 2u * cb + 1u;
+    bool last = false;
+    unsigned f = 0, r = 0, c = 0;
+    if (l < 32 && b < g.total) {
+        f = b / g.nb;
+        const unsigned bi = b - f * g.nb;
+        r = bi / g.bpr;
+        c = bi - r * g.bpr;
+        last = c == g.bpr - 1u;
+    }
+    const uint64_t bal = __ballot(last && y == 0);
+    uint32_t qm = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) qm |= (uint32_t)((bal >> (8 * k)) & 1u) << k;
+    if (qm) {
+        if (last) {
+            typedef const __attribute__((address_space(1))) mx_u2 gu2;
+            const gu2 *src = (const gu2 *)(g.rgb + (long long)f * g.fstride + (8ll * r + y) * g.pitch + 24ll * c);
+            const mx_u2 v0 = src[0], v1 = src[1], v2 = src[2];
+            uint8_t *d = L.qtrue[cb] + 24u * y;
+            *(mx_u2 *)d = v0;
+            *(mx_u2 *)(d + 8) = v1;
+            *(mx_u2 *)(d + 16) = v2;
+        }
+        __builtin_amdgcn_s_waitcnt(0xF70);             /* vmcnt(0) (rare; conservative) */
+        mx_wave_sync();
+    }
+    return qm;
+}
+
+__global__ __launch_bounds__(256, JX_MX_WPE) void k_mx422(const jx_xform_args a)
+{
+    __shared__ __attribute__((aligned(16))) Mx422Lds s_lds[4];
+    MxG g;
+    g.rgb = a.g.rgb;
+    g.out = a.g.out;
+    g.pitch = a.g.in_pitch;
+    g.fstride = a.g.in_fstride;
+    g.ofstride = a.g.out_fstride;
+    g.bpr = (unsigned)a.g.bpr;
+    g.nb = (unsigned)a.g.nb;
+    g.total = (unsigned)a.g.nb * (unsigned)a.g.nframes;
+    g.row0 = a.g.row0;
+    g.quality = a.quality;
+    g.force = a.force_exact;
+    g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
+#pragma unroll
+    for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+
+    const unsigned lane = threadIdx.x & 63u;
+    Mx422Lds &L = s_lds[threadIdx.x >> 6];
+    const unsigned nw = gridDim.x * 4u;
+    const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (32u * wv >= g.total) return;
+
+    /* Y A operands as k_mx's; chroma: row m = (chroma block m >> 2, pixel row m & 3 of the
+     * half), k-step 0 bytes 8q.. of the MCU's 48-byte row, k-step 1 bytes 32 + 8q (q < 2), the
+     * bias 1.0 (q = 2), zeros (q = 3) */
+    const unsigned m = lane & 15u, q = lane >> 4;
+    const uint32_t aoff = 192u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 0u);
+    const uint32_t s0 = q < 3 ? kSelLo : kSelOne;
+    const uint32_t s1 = q < 3 ? kSelHi : kSelZero;
+    const uint32_t s2 = q < 3 ? kSelLo : kSelZero;
+    const uint32_t coff0 = 192u * (m & 3u) + 48u * (m >> 2) + 8u * q;
+    const uint32_t coff1 = 192u * (m & 3u) + 48u * (m >> 2) + 32u + 8u * (q < 2 ? q : 0u);
+    const uint32_t t0 = q < 2 ? kSelLo : (q == 2 ? kSelOne : kSelZero);
+    const uint32_t t1 = q < 2 ? kSelHi : kSelZero;
+    const uint32_t t2 = q < 2 ? kSelLo : kSelZero;
+    const uint32_t off0 = (uint32_t)((lane / 12u) * (unsigned)g.pitch + 16u * (lane % 12u));
+    const uint32_t off1 = (uint32_t)(((64u + lane) / 12u) * (unsigned)g.pitch + 16u * ((64u + lane) % 12u));
+    /* stores: Y 8 blocks x 128 B (lane 16 B), chroma lanes 0..31 Cb / 32..63 Cr 4 blocks x 128 B */
+    const uint32_t soy = lane * 16u, soc = (lane & 31u) * 16u + (lane >> 5) * (g.nb / 2u) * 128u;
+    const uint32_t roy = mx_sb(2) + (lane >> 3) * kBS + (lane & 7u) * 16u;
+    const uint32_t roc = mx_sb(lane >> 5) + ((lane >> 3) & 3u) * kBS + (lane & 7u) * 16u;
+
+    const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
+    const jx_mxtab &T = g_mx422tab[g.force ? 1 : 0][g.quality];
+    const unsigned nyc = u, ncc = 8u + j;                  /* plan columns */
+    mx_f2 Wy[4], Ly[4], Wc[4], Lc[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const int v0 = jx_pk_k(p, 0), v1 = jx_pk_k(p, 1);
+        Wy[p] = mx_f2{T.w[nyc][v0], T.w[nyc][v1]};
+        Ly[p] = mx_f2{T.lsq[nyc][v0], T.lsq[nyc][v1]};
+        Wc[p] = mx_f2{T.w[ncc][v0], T.w[ncc][v1]};
+        Lc[p] = mx_f2{T.lsq[ncc][v0], T.lsq[ncc][v1]};
+    }
+    uint32_t zo[8];
+#pragma unroll
+    for (int v = 0; v < 8; v++) zo[v] = 2u * (unsigned)kMxScan[v][u];
+    uint8_t *const sty = L.stage + mx_sb(2) + kBS * (j < 8 ? gq : 4u + gq);
+    uint8_t *const stc = L.stage + mx_sb(j >> 3) + kBS * gq;
+    mx_u4 B[kParts][4];
+#pragma unroll
+    for (int p = 0; p < kParts; p++)
+#pragma unroll
+        for (int w = 0; w < 4; w++) B[p][w] = g_mx422B[4 * p + w][lane];
+    /* the operand and table loads complete here, once: otherwise the compiler's wait for them
+     * (it counts one operation for a DMA whose lane < 32 half might be skipped) lands inside
+     * the step loop as a vmcnt(0) that drains the prefetch every step */
+    __builtin_amdgcn_s_waitcnt(0xF70);
+
+    MxJump J;
+    J.jb = 32u * nw;
+    J.jr = J.jb / g.bpr;
+    J.jc = J.jb - J.jr * g.bpr;
+    J.rows = g.nb / g.bpr;
+    MxChunk cc;
+    mx_chunk_at(cc, g, 32u * wv);
+    MxChunk nx = cc;
+
+    const auto issue = [&](const MxChunk &C, unsigned k) {
+        uint8_t *const slot = L.ring[k];
+        const unsigned b = C.b0 + 8u * k;
+        if (b >= g.total) {
+            mx_pad(g, L, 2);
+        } else if (C.simple) {
+            const uint8_t *base = C.src + 192u * k;
+            __builtin_amdgcn_global_load_lds((mx_gp)(base + off0), (mx_lp)slot, 16, 0, 0);
+            if (lane < 32) __builtin_amdgcn_global_load_lds((mx_gp)(base + off1), (mx_lp)(slot + 1024u), 16, 0, 0);
+        } else {
+            MxCur P;
+            mx_seek(P, g, b);
+            mx_issue(g, P, b, mx_simple_load(P, g, b), off0, off1, slot);
+        }
+    };
+    for (unsigned d = 0; d < kDist; d++) {
+        issue(cc, d);
+        mx_pad(g, L, 2);
+    }
+    int nq = 0, ns = 0;
+    unsigned k = 0;
+    for (;;) {
+        const unsigned b0 = cc.b0 + 8u * k;
+        /* younger than this step's DMA: the two stores of steps s-2, s-1 and step s+1's DMA */
+        __builtin_amdgcn_s_waitcnt(kWaitImm422);
+        mx_wave_sync();
+        const uint8_t *const sp = L.ring[k];
+        if (k + kDist < kChunk) {
+            issue(cc, k + kDist);
+        } else {
+            if (k + kDist == kChunk) mx_chunk_next(nx, g, J);
+            issue(nx, k + kDist - kChunk);
+        }
+        const uint32_t qmask = cc.simple ? 0u : mx422_true_rows(L, g, b0);
+        const mx_u2 y00 = *(const mx_u2 *)(sp + aoff);
+        const mx_u2 y01 = *(const mx_u2 *)(sp + aoff + 768u);
+        const mx_u2 y10 = *(const mx_u2 *)(sp + aoff + 96u);
+        const mx_u2 y11 = *(const mx_u2 *)(sp + aoff + 864u);
+        mx_u2 c00, c01, c10, c11;
+        if (JX_DBG_NOQ || __builtin_expect(qmask == 0, 1)) {
+            c00 = *(const mx_u2 *)(sp + coff0);
+            c01 = *(const mx_u2 *)(sp + coff0 + 768u);
+            c10 = *(const mx_u2 *)(sp + coff1);
+            c11 = *(const mx_u2 *)(sp + coff1 + 768u);
+        } else {
+            /* chroma blocks with a row-last right block: its bytes (24..47 of the MCU row)
+             * from the true rows */
+            const unsigned l = mx_lane(), mm = l & 15u, qq = l >> 4, cb = mm >> 2;
+            const bool qb = (qmask >> cb) & 1u;
+            const uint8_t *qt = L.qtrue[cb] + 24u * (mm & 3u);
+            const uint8_t *p0 = qb && qq == 3 ? qt : sp + coff0;
+            const uint8_t *p1 = qb && qq < 2 ? qt + 8u + 8u * qq : sp + coff1;
+            const unsigned h0 = qb && qq == 3 ? 96u : 768u, h1 = qb && qq < 2 ? 96u : 768u;
+            c00 = *(const mx_u2 *)p0;
+            c01 = *(const mx_u2 *)(p0 + h0);
+            c10 = *(const mx_u2 *)p1;
+            c11 = *(const mx_u2 *)(p1 + h1);
+        }
+        const mx_h8 Y00 = mx_aop(y00, s0, s1, s2), Y01 = mx_aop(y01, s0, s1, s2);
+        const mx_h8 Y10 = mx_aop(y10, s0, s1, s2), Y11 = mx_aop(y11, s0, s1, s2);
+        const mx_h8 C00 = mx_aop(c00, kSelLo, kSelHi, kSelLo);
+        const mx_h8 C01 = mx_aop(c01, kSelLo, kSelHi, kSelLo);
+        const mx_h8 C10 = mx_aop(c10, t0, t1, t2), C11 = mx_aop(c11, t0, t1, t2);
+        const mx_f4 z = {};
+        uint32_t fl = 0;
+        mx_f2 R[4], F[4];
+        mx_f4 acc[2][4];                               /* [Y, chroma][hl, ll, hh, lh] */
+        const auto mma2 = [&](mx_f4(&o)[4], const mx_h8 &Al0, const mx_h8 &Ah0, const mx_h8 &Al1,
+                              const mx_h8 &Ah1, int w0) {
+            o[0] = mx_mma(Al0, B[0][w0], z);
+            o[2] = mx_mma(Ah0, B[0][w0], z);
+            o[1] = mx_mma(Al0, B[1][w0], z);
+            o[3] = mx_mma(Ah0, B[1][w0], z);
+            o[0] = mx_mma(Al1, B[0][w0 + 1], o[0]);
+            o[2] = mx_mma(Ah1, B[0][w0 + 1], o[2]);
+            o[1] = mx_mma(Al1, B[1][w0 + 1], o[1]);
+            o[3] = mx_mma(Ah1, B[1][w0 + 1], o[3]);
+            if (kParts == 3) {
+                o[1] = mx_mma(Al0, B[kParts - 1][w0], o[1]);
+                o[3] = mx_mma(Ah0, B[kParts - 1][w0], o[3]);
+                o[1] = mx_mma(Al1, B[kParts - 1][w0 + 1], o[1]);
+                o[3] = mx_mma(Ah1, B[kParts - 1][w0 + 1], o[3]);
+            }
+        };
+        const auto column = [&](int kc) {
+            mx_combine(acc[kc][0], acc[kc][1], acc[kc][2], acc[kc][3], R);
+            float e = -1.0f;
+            const mx_f2(&W)[4] = kc == 0 ? Wy : Wc;
+            const mx_f2(&Lq)[4] = kc == 0 ? Ly : Lc;
+            mx_column(R, W, Lq, kc == 0 ? sty : stc, zo, e, F);
+            if (__builtin_expect(__ballot(e >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * kc);
+        };
+        mma2(acc[0], Y00, Y01, Y10, Y11, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma2(acc[1], C00, C01, C10, C11, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        column(0);
+        __builtin_amdgcn_sched_barrier(0);
+        column(1);
+        mx_wave_sync();
+        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx422_defer_step(L, sp, qmask, fl, b0, nq, ns, g, T);
+        /* always two store instructions per step (the vmcnt accounting counts on it) */
+        if (cc.simple) {
+            const mx_u4 vy = *(const mx_u4 *)(L.stage + roy);
+            const mx_u4 vc = *(const mx_u4 *)(L.stage + roc);
+            __builtin_nontemporal_store(vy, (mx_u4 *)((const uint8_t *)(cc.dst + 512u * k) + soy));
+            __builtin_nontemporal_store(vc, (mx_u4 *)((const uint8_t *)(cc.cdst + 256u * k) + soc));
+        } else {
+            const unsigned l = mx_lane();
+            const unsigned by = b0 + (l >> 3), bc = b0 + 2u * ((l >> 3) & 3u);
+            const unsigned yb = by < g.total ? by : g.total - 1u, cbk = bc < g.total ? bc : g.total - 1u;
+            const unsigned fy = yb / g.nb, biy = yb - fy * g.nb;
+            const unsigned fc = cbk / g.nb, bic = cbk - fc * g.nb;
+            const mx_u4 vy = *(const mx_u4 *)(L.stage + mx_sb(2) + (l >> 3) * kBS + (l & 7u) * 16u);
+            const mx_u4 vc = *(const mx_u4 *)(L.stage + mx_sb(l >> 5) + ((l >> 3) & 3u) * kBS + (l & 7u) * 16u);
+            if (by < g.total)
+                __builtin_nontemporal_store(
+                    vy, (mx_u4 *)(g.out + (long long)fy * g.ofstride + (long long)biy * 64 + (l & 7u) * 8));
+            if (bc < g.total)
+                __builtin_nontemporal_store(
+                    vc, (mx_u4 *)(g.out + (long long)fc * g.ofstride +
+                                  ((long long)g.nb + (l >> 5) * (g.nb / 2u) + bic / 2u) * 64 + (l & 7u) * 8));
+        }
+        mx_wave_sync();
+        if (++k == kChunk) {
+            k = 0;
+            cc = nx;
+            if (cc.b0 >= g.total) break;
+        } else if (b0 + 8u >= g.total) {
+            break;
+        }
+    }
+    if (nq) mx422_flush(L, nq, ns, g, T);
+}
+
 int mx_rc(hipError_t e) { return e == hipSuccess ? JPGX_OK : JPGX_EHIP; }
 
 constexpr int kMaxDev = 64;
@@ -822,7 +1343,7 @@ int mx_tables_for_current_device(int *waves)
                 memcpy(t.q, qq, sizeof qq);
                 for (int n = 0; n < 24; n++)
                     for (int v = 0; v < 8; v++) {
-                        t.w[n][v] = w[n][v];
+                        t.w[n][v] = w[n][v] * kRScale;
                         t.lsq[n][v] = f ? -1.0f : mx_lsq(lim[n][v]);
                     }
             }
@@ -845,7 +1366,67 @@ int mx_tables_for_current_device(int *waves)
     return g_mx_rc[dev];
 }
 
+std::once_flag g_mx422_once[kMaxDev];
+int g_mx422_rc[kMaxDev];
+int g_mx422_waves[kMaxDev];
+
+int mx422_tables_for_current_device(int *waves)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return JPGX_ENODEV;
+    std::call_once(g_mx422_once[dev], [dev]() {
+        std::vector<jx_mxtab> tab(2 * (JX_MAXQ + 1));
+        memset(tab.data(), 0, tab.size() * sizeof(jx_mxtab));
+        int rc = JPGX_OK;
+        for (int q = 1; q <= JX_MAXQ && !rc; q++) {
+            float w[24][8], lim[24][8];
+            int16_t qq[2][64];
+            rc = jx_plan_tables_mx422(q, w, lim, qq);
+            for (int f = 0; f < 2; f++) {
+                jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
+                memcpy(t.q, qq, sizeof qq);
+                for (int n = 0; n < 24; n++)
+                    for (int v = 0; v < 8; v++) {
+                        t.w[n][v] = w[n][v] * kRScale;
+                        t.lsq[n][v] = f ? -1.0f : mx_lsq(lim[n][v]);
+                    }
+            }
+        }
+        static uint16_t ops[JX_MX_PARTS][4][64][8];
+        if (!rc) rc = jx_mx422_operands(ops);
+        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx422tab), tab.data(),
+                                              tab.size() * sizeof(jx_mxtab)));
+        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx422B), ops, sizeof ops));
+        int cus = 0, per_cu = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mx422, 256, 0) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 2;
+        g_mx422_waves[dev] = cus * per_cu * 4;
+        g_mx422_rc[dev] = rc;
+    });
+    if (waves) *waves = g_mx422_waves[dev];
+    return g_mx422_rc[dev];
+}
+
 }  // namespace
+
+
+/* k_mx422 over every frame of the stripe (true 4:2:2: Y [nb][64], Cb and Cr [nb / 2][64] per
+ * frame); no workspace. */
+extern "C" int jx_launch_mx422(const jx_xform_args *xa, void *stream)
+{
+    int waves = 0;
+    const int rc = mx422_tables_for_current_device(&waves);
+    if (rc) return rc;
+    const size_t total = (size_t)xa->g.nb * (size_t)xa->g.nframes;
+    const size_t nsteps = (total + 7) / 8;
+    const size_t w = std::min<size_t>(nsteps, (size_t)std::max(waves, 4));
+    const unsigned grid = (unsigned)((w + 3) / 4);
+    hipLaunchKernelGGL(k_mx422, dim3(grid), dim3(256), 0, (hipStream_t)stream, *xa);
+    return mx_rc(hipGetLastError());
+}
 
 
 /* k_mx over every frame of the stripe (4:4:4 / reference-parity output); no workspace. */

@@ -377,16 +377,21 @@ extern "C" {
 
 /* ---- k_mx: colour conversion + row DCT as one f16 MFMA product --------------------------
  *
- * k_mx multiplies each pixel row, 24 bytes b_k (k = 3x + p, plane p of pixel x) shifted to
- * s_k = b_k - 128 (exact in f16), by B[k][n] = a[c][p] cos((2x+1)u pi/16), n = 8c + u, with
- * a bias row (input 1.0) carrying 8 * (128 sum_p a[c][p] + shift_c) for u = 0 (the level
- * shift, preprocess.c:160-162,186-188; the true cosines of u > 0 sum to 0).  B is split into
- * JX_MX_PARTS f16 parts:
- *   Bh  B rounded to a multiple of 2^-11 (|B| < 1: 11 bits, an f16; bias: its f16),
- *   Bl  f16(2^12 (B - Bh)),  [Bm  f16(2^12 (B - Bh) - Bl)]   (scaled: normal f16 numbers).
- * acc_h = sum_k s_k Bh_k is EXACT whatever the order of the MFMA's additions: every product
+ * k_mx multiplies each pixel row, 24 bytes b_k (k = 3x + p, plane p of pixel x), by B[k][n] =
+ * a[c][p] cos((2x+1)u pi/16), n = 8c + u, with a bias row (input 1.0) carrying the level shift,
+ * -8 * 128 for Y at u = 0 (preprocess.c:160-162,186-188: Y - 128; the level-shifted chroma has
+ * no constant; the true cosines of u > 0 sum to 0).  B is split into JX_MX_PARTS f16 parts:
+ *   Bh  B rounded to a multiple of 2^-11 (|B| < 1: 11 bits; bias: its f16),
+ *   Bl  2^12 (B - Bh),  [Bm  2^12 (B - Bh) - Bl]   (each rounded to f16).
+ * Encoding (the kernel's A is one v_perm per two bytes): A holds the byte zero-extended to 16
+ * bits, i.e. the f16 subnormal b 2^-24 (exact), the bias lanes 1.0; B's byte rows are stored
+ * x 2^15 and the bias row x 2^-9, so every product is b B 2^-9 (exact in fp32) and the MFMA's
+ * results are R 2^-9.  Scaling by a power of two changes no rounding, so the kernel's fp32
+ * values are those of the true-scale arithmetic below times 2^-9 bit for bit; the column pass
+ * scales with them, and the quantiser's w x 2^9 (JX_MX_RSCALE) gives the very fp32 F w.
+ * acc_h = sum_k b_k Bh_k is EXACT whatever the order of the MFMA's additions: every product
  * and every partial sum is a multiple of 2^-11 below 2^13 in magnitude (24 bits).  acc_l =
- * sum_k s_k (Bl_k [+ Bm_k]) 2^-12 is below 1 in magnitude; each of its additions is charged
+ * sum_k b_k (Bl_k [+ Bm_k]) 2^-12 is below 1 in magnitude; each of its additions is charged
  * one ulp.  R = fl(acc_h + 2^-12 acc_l) (one fma) then enters the column pass (jx_fdct8,
  * FOps, two blocks per v_pk_* pair) as usual.
  *
@@ -433,11 +438,17 @@ static long double mx_exact(int k, int n)
         const int x = k / 3, p = k % 3;
         return (long double)kMxA[c][p] * cosl((2 * x + 1) * u * pi / 16);
     }
-    if (k == 24 && u == 0) {
-        const long double sa = (long double)kMxA[c][0] + kMxA[c][1] + kMxA[c][2];
-        return 8.0L * (128.0L * sa - (c == 0 ? 128.0L : 0.0L));
-    }
+    if (k == 24 && u == 0 && c == 0) return -1024.0L;
     return 0;
+}
+
+/* f16 encodings of the split parts (see above): a byte row's value x 2^15, the bias row's
+ * x 2^-9; returns the true-scale value the encoding represents */
+constexpr int kMxBExp = 15, kMxBiasExp = -9;
+static long double mx_enc(long double v, bool bias, uint16_t *bits)
+{
+    const int e = bias ? kMxBiasExp : kMxBExp;
+    return ldexpl(f16_round(ldexpl(v, e), bits), -e);
 }
 
 struct MxSplit {
@@ -451,28 +462,22 @@ static int mx_split(MxSplit &S)
     for (int k = 0; k < 25; k++)
         for (int n = 0; n < 24; n++) {
             const long double B = mx_exact(k, n);
-            long double hv;
-            if (k < 24) {
-                hv = rintl(ldexpl(B, 11)) / 2048.0L;
-                f16_round(hv, &S.bh[k][n]);
-            } else {
-                hv = f16_round(B, &S.bh[k][n]);
-            }
+            const bool bias = k == 24;
+            const long double hv = mx_enc(bias ? B : rintl(ldexpl(B, 11)) / 2048.0L, bias, &S.bh[k][n]);
             if (ldexpl(hv, 11) != rintl(ldexpl(hv, 11))) return JPGX_EARG;
             S.h[k][n] = hv;
-            /* the lo parts are stored scaled by 2^12 (normal f16 numbers, not subnormals that
-             * would flush the third part to 0); k_mx takes R = acc_h + 2^-12 acc_l, exact
+            /* the lo parts are stored scaled by 2^12; k_mx takes R = acc_h + 2^-12 acc_l, exact
              * scaling.  S.l / S.m hold the unscaled values. */
-            const long double ls = f16_round(ldexpl(B - hv, 12), &S.bl[k][n]);
+            const long double ls = mx_enc(ldexpl(B - hv, 12), bias, &S.bl[k][n]);
             S.l[k][n] = ldexpl(ls, -12);
             if (JX_MX_PARTS == 3) {
-                const long double ms = f16_round(ldexpl(B - hv, 12) - ls, &S.bm[k][n]);
+                const long double ms = mx_enc(ldexpl(B - hv, 12) - ls, bias, &S.bm[k][n]);
                 S.m[k][n] = ldexpl(ms, -12);
             }
         }
     for (int n = 0; n < 24; n++) {              /* acc_h exactness: partial sums < 2^13 */
         long double sh = fabsl(S.h[24][n]);
-        for (int k = 0; k < 24; k++) sh += 128.0L * fabsl(S.h[k][n]);
+        for (int k = 0; k < 24; k++) sh += 255.0L * fabsl(S.h[k][n]);
         if (sh >= 8192.0L) return JPGX_EARG;
     }
     return JPGX_OK;
@@ -510,14 +515,14 @@ static Bnd mx_row_bound(const MxSplit &S, int n)
     long double lol = S.l[24][n] + S.m[24][n], hil = lol;
     long double sl = fabsl(S.l[24][n]) + fabsl(S.m[24][n]);
     long double rep = fabsl(mx_exact(24, n) - S.h[24][n] - S.l[24][n] - S.m[24][n]);
-    for (int k = 0; k < 24; k++) {
+    for (int k = 0; k < 24; k++) {             /* bytes 0..255 */
         const long double bh = S.h[k][n], bo = S.l[k][n] + S.m[k][n];
-        loh += std::min(-128.0L * bh, 127.0L * bh);
-        hih += std::max(-128.0L * bh, 127.0L * bh);
-        lol += std::min(-128.0L * bo, 127.0L * bo);
-        hil += std::max(-128.0L * bo, 127.0L * bo);
-        sl += 128.0L * (fabsl(S.l[k][n]) + fabsl(S.m[k][n]));
-        rep += 128.0L * fabsl(mx_exact(k, n) - S.h[k][n] - S.l[k][n] - S.m[k][n]);
+        loh += std::min(0.0L, 255.0L * bh);
+        hih += std::max(0.0L, 255.0L * bh);
+        lol += std::min(0.0L, 255.0L * bo);
+        hil += std::max(0.0L, 255.0L * bo);
+        sl += 255.0L * (fabsl(S.l[k][n]) + fabsl(S.m[k][n]));
+        rep += 255.0L * fabsl(mx_exact(k, n) - S.h[k][n] - S.l[k][n] - S.m[k][n]);
     }
     /* acc_l: per lo part one MFMA of 32 products (K = 32: 25 weights, 7 zeros; the Cr tile's
      * second, K-concatenated MFMA adds exact zeros in every column) plus the accumulator input;
@@ -563,6 +568,231 @@ extern "C" int jx_plan_tables_mx(int quality, float w[24][8], float lim[24][8], 
     return JPGX_OK;
 }
 
+/* ---- k_mx422: true 4:2:2 on the matrix cores ------------------------------------------
+ *
+ * Y is k_mx's Y (plan columns n = u, the 4:4:4 split S), its B laid out K-concatenated: the
+ * product A_set0 B_Y0 + A_set1 B_Y1 puts set 0's blocks in C columns 0..7 and set 1's in
+ * 8..15 (B_Y0 zero in columns 8..15, B_Y1 zero in 0..7), exactly as k_mx's Cr tile.
+ * Chroma (the EXTENSION's definition, oracle/cpu_ref.c cpuref_chroma_sample): a chroma row of
+ * a chroma block is the 16 pixels (48 bytes) of its two Y blocks' row; the sample X is the
+ * average of pixels 2X, 2X+1 of the level-shifted chroma, so the row transform is
+ *   R(u) = sum_{x < 16, p} b_{3x+p} 0.5 a[c][p] cos((2 floor(x/2) + 1) u pi/16)
+ * (a = kMxA[c], c = Cb, Cr; b = the byte: the level-shifted chroma has no constant, so the bias
+ * row k = 48 is zero), i.e. B_C[k][n] over k = 3x + p < 48, n = 8 c' + u (c' = 0 Cb, 1 Cr).
+ * Two K = 32 MFMAs per chroma row tile (k = 0..31, 32..63).  Same encoding and split as k_mx: Bh a multiple
+ * of 2^-11 (acc_h exact in any order: every partial sum a multiple of 2^-11 below 2^13), the lo
+ * part(s) scaled by 2^12, each of acc_l's additions charged one ulp (65 per chroma row: two
+ * MFMAs of 32 products plus the accumulator).
+ */
+static long double mx422_exact(int k, int n)
+{
+    if (n >= 16) return 0;
+    const int c = 1 + n / 8, u = n % 8;
+    const long double pi = 3.141592653589793238462643383279502884L;
+    if (k < 48) {
+        const int x = k / 3, p = k % 3;
+        return 0.5L * (long double)kMxA[c][p] * cosl((2 * (x / 2) + 1) * u * pi / 16);
+    }
+    return 0;                                   /* k = 48: no level-shift constant in chroma */
+}
+
+struct Mx422Split {
+    long double h[49][16], l[49][16], m[49][16];
+    uint16_t bh[49][16], bl[49][16], bm[49][16];
+};
+
+static int mx422_split(Mx422Split &S)
+{
+    memset(&S, 0, sizeof S);
+    for (int k = 0; k < 49; k++)
+        for (int n = 0; n < 16; n++) {
+            const long double B = mx422_exact(k, n);
+            const bool bias = k == 48;
+            const long double hv = mx_enc(bias ? B : rintl(ldexpl(B, 11)) / 2048.0L, bias, &S.bh[k][n]);
+            if (ldexpl(hv, 11) != rintl(ldexpl(hv, 11))) return JPGX_EARG;
+            S.h[k][n] = hv;
+            const long double ls = mx_enc(ldexpl(B - hv, 12), bias, &S.bl[k][n]);
+            S.l[k][n] = ldexpl(ls, -12);
+            if (JX_MX_PARTS == 3) {
+                const long double ms = mx_enc(ldexpl(B - hv, 12) - ls, bias, &S.bm[k][n]);
+                S.m[k][n] = ldexpl(ms, -12);
+            }
+        }
+    for (int n = 0; n < 16; n++) {              /* acc_h exactness: partial sums < 2^13 */
+        long double sh = fabsl(S.h[48][n]);
+        for (int k = 0; k < 48; k++) sh += 255.0L * fabsl(S.h[k][n]);
+        if (sh >= 8192.0L) return JPGX_EARG;
+    }
+    return JPGX_OK;
+}
+
+/* operand [part][which][lane][e]: which 0 / 1 = Y of set 0 / set 1 (K = 32: 24 bytes + bias),
+ * 2 / 3 = chroma k = 0..31 / 32..63; lane l holds B[k = 8 (l >> 4) + e (+32)][column l & 15] */
+extern "C" int jx_mx422_operands(uint16_t ops[JX_MX_PARTS][4][64][8])
+{
+    static MxSplit S;
+    static Mx422Split C;
+    int rc = mx_split(S);
+    if (!rc) rc = mx422_split(C);
+    if (rc) return rc;
+    for (int part = 0; part < JX_MX_PARTS; part++)
+        for (int which = 0; which < 4; which++)
+            for (int l = 0; l < 64; l++)
+                for (int e = 0; e < 8; e++) {
+                    const int j = l & 15;
+                    uint16_t v = 0;
+                    if (which < 2) {
+                        const int k = 8 * (l >> 4) + e;
+                        const bool on = which == 0 ? j < 8 : j >= 8;
+                        if (on && k <= 24) {
+                            const int n = j & 7;
+                            v = part == 0 ? S.bh[k][n] : (part == 1 ? S.bl[k][n] : S.bm[k][n]);
+                        }
+                    } else {
+                        const int k = 32 * (which - 2) + 8 * (l >> 4) + e;
+                        if (k <= 48) v = part == 0 ? C.bh[k][j] : (part == 1 ? C.bl[k][j] : C.bm[k][j]);
+                    }
+                    ops[part][which][l][e] = v;
+                }
+    return JPGX_OK;
+}
+
+/* Interval + error bound of a chroma row transform R (column n = 8 c' + u) */
+static Bnd mx422_row_bound(const Mx422Split &S, int n)
+{
+    long double loh = S.h[48][n], hih = S.h[48][n];
+    long double lol = S.l[48][n] + S.m[48][n], hil = lol;
+    long double sl = fabsl(S.l[48][n]) + fabsl(S.m[48][n]);
+    long double rep = fabsl(mx422_exact(48, n) - S.h[48][n] - S.l[48][n] - S.m[48][n]);
+    for (int k = 0; k < 48; k++) {             /* bytes 0..255 */
+        const long double bh = S.h[k][n], bo = S.l[k][n] + S.m[k][n];
+        loh += std::min(0.0L, 255.0L * bh);
+        hih += std::max(0.0L, 255.0L * bh);
+        lol += std::min(0.0L, 255.0L * bo);
+        hil += std::max(0.0L, 255.0L * bo);
+        sl += 255.0L * (fabsl(S.l[k][n]) + fabsl(S.m[k][n]));
+        rep += 255.0L * fabsl(mx422_exact(k, n) - S.h[k][n] - S.l[k][n] - S.m[k][n]);
+    }
+    /* acc_l: per lo part two MFMAs of 32 products (49 weights, 15 zeros) plus the accumulator
+     * input, every addition charged one ulp of the magnitude bound, twice over (unknown
+     * summation tree and rounding mode) */
+    const double nadd = 2.0 * (65.0 * (JX_MX_PARTS - 1));
+    const double el = (double)(nadd * sl * 0x1p-23L + rep);
+    return BoundOps::add(Bnd{(double)loh, (double)hih, 0.0},
+                         Bnd{(double)lol - el, (double)hil + el, el});
+}
+
+/* plan columns n = 8 c + u as jx_mxtab: c = 0 Y (k_mx's bound), 1 Cb, 2 Cr (4:2:2 rows) */
+extern "C" int jx_plan_tables_mx422(int quality, float w[24][8], float lim[24][8], int16_t q[2][64])
+{
+    int qs[2][8][8];
+    int rc = jpgx_scale_table(0, quality, qs[0]);
+    if (rc) return rc;
+    jpgx_scale_table(1, quality, qs[1]);
+    for (int t = 0; t < 2; t++)
+        for (int u = 0; u < 8; u++)
+            for (int v = 0; v < 8; v++) q[t][u * 8 + v] = (int16_t)qs[t][u][v];
+    static MxSplit S;
+    static Mx422Split C;
+    rc = mx_split(S);
+    if (!rc) rc = mx422_split(C);
+    if (rc) return rc;
+    const long double a0 = 1.0L / sqrtl(2.0L);
+    for (int n = 0; n < 24; n++) {
+        const int c = n / 8, u = n % 8, t = c == 0 ? 0 : 1;
+        const Bnd R = c == 0 ? mx_row_bound(S, n) : mx422_row_bound(C, n - 8);
+        Bnd col[8], out[8];
+        for (int y = 0; y < 8; y++) col[y] = R;
+        jx_fdct8<BoundOps>(col, out);
+        for (int v = 0; v < 8; v++) {
+            const long double au = u == 0 ? a0 : 1.0L, av = v == 0 ? a0 : 1.0L;
+            const long double ws = 0.25L * au * av * dct_kfactor(v) / (long double)qs[t][u][v];
+            const float wf = (float)ws;
+            const Bnd &b = out[v];
+            const double mF = BoundOps::mag(b) + b.E;
+            double et = b.E * (double)wf + mF * (double)fabsl((long double)wf - ws) + 0x1p-25;
+            et = et * 1.01 + 1e-7;
+            w[n][v] = wf;
+            lim[n][v] = (float)(0.5 - et);
+        }
+    }
+    return JPGX_OK;
+}
+
+/* Host emulation of k_mx422's chroma fast path (acc_h exact, acc_l in fp32, R = fl(acc_h +
+ * 2^-12 acc_l), FOps column pass, quantiser) against the definition's exact quotient on random
+ * 16 x 8 pixel pairs: unflagged mismatches (must be 0), flagged count, worst error / band. */
+extern "C" long long jx_selftest_mx422(long long nblocks, unsigned long long seed, int quality,
+                                       long long *flagged, double *ratio)
+{
+    static Mx422Split C;
+    if (mx422_split(C)) return -1;
+    float w[24][8], lim[24][8];
+    int16_t q[2][64];
+    if (jx_plan_tables_mx422(quality, w, lim, q)) return -1;
+    const long double pi = 3.141592653589793238462643383279502884L;
+    const long double a0 = 1.0L / sqrtl(2.0L);
+    uint64_t s = seed;
+    long long bad = 0, nfl = 0;
+    double worst = 0;
+    for (long long bk = 0; bk < nblocks; bk++) {
+        int px[8][48];
+        for (int y = 0; y < 8; y++)
+            for (int k = 0; k < 48; k++) {
+                s = s * 6364136223846793005ULL + 1442695040888963407ULL;
+                px[y][k] = (int)(s >> 56);
+                if ((bk & 3) == 1) px[y][k] = px[0][k % 3];      /* flat blocks too */
+                if ((bk & 3) == 2) px[y][k] = (k % 3 == 0) ? 255 : 0;
+            }
+        for (int n = 0; n < 16; n++) {
+            const int c = 1 + n / 8, u = n % 8, pn = 8 + n;
+            float R[8];
+            for (int y = 0; y < 8; y++) {
+                long double ah = C.h[48][n];
+                float al = (float)(C.l[48][n] + C.m[48][n]);
+                for (int k = 0; k < 48; k++) {
+                    const int sv = px[y][k];
+                    ah += sv * C.h[k][n];
+                    al = al + (float)(sv * C.l[k][n]);
+                    if (JX_MX_PARTS == 3) al = al + (float)(sv * C.m[k][n]);
+                }
+                R[y] = (float)ah + al;
+            }
+            float F[8];
+            jx_fdct8<FOps>(R, F);
+            for (int v = 0; v < 8; v++) {
+                long double sum = 0;
+                for (int y = 0; y < 8; y++)
+                    for (int X = 0; X < 8; X++) {
+                        long double cs = 0;
+                        for (int h = 0; h < 2; h++) {
+                            const int x = 2 * X + h;
+                            cs += (long double)kMxA[c][0] * px[y][3 * x] + (long double)kMxA[c][1] * px[y][3 * x + 1] +
+                                  (long double)kMxA[c][2] * px[y][3 * x + 2];
+                        }
+                        sum += 0.5L * cs * cosl((2 * X + 1) * u * pi / 16) * cosl((2 * y + 1) * v * pi / 16);
+                    }
+                const long double au = u == 0 ? a0 : 1.0L, av = v == 0 ? a0 : 1.0L;
+                const long double qx = 0.25L * au * av * sum / q[1][u * 8 + v];
+                const float tm = fmaf(F[v], w[pn][v], 12582912.0f);
+                const float rr = tm - 12582912.0f;
+                const float d = fmaf(F[v], w[pn][v], -rr);
+                const double qf = (double)F[v] * (double)w[pn][v];
+                const double band = 0.5 - (double)lim[pn][v];
+                worst = std::max(worst, (double)fabsl((long double)qf - qx) / band);
+                if (fabsf(d) >= lim[pn][v]) {
+                    nfl++;
+                    continue;
+                }
+                if ((long double)rr != roundl(qx)) bad++;
+            }
+        }
+    }
+    if (flagged) *flagged = nfl;
+    if (ratio) *ratio = worst;
+    return bad;
+}
+
 /* Host emulation of k_mx's fast path on random blocks (acc_h exact, acc_l summed in fp32,
  * R = fl(acc_h + acc_l), then the kernel's FOps column pass and quantiser): counts the
  * coefficients whose unflagged fp32 result differs from round(exact quotient) (must be 0)
@@ -595,7 +825,7 @@ extern "C" long long jx_selftest_mx(long long nblocks, unsigned long long seed, 
                 long double ah = S.h[24][n];
                 float al = (float)(S.l[24][n] + S.m[24][n]);
                 for (int k = 0; k < 24; k++) {
-                    const int sv = px[y][k] - 128;
+                    const int sv = px[y][k];
                     ah += sv * S.h[k][n];
                     al = al + (float)(sv * S.l[k][n]);
                     if (JX_MX_PARTS == 3) al = al + (float)(sv * S.m[k][n]);

@@ -140,12 +140,14 @@ def test_mx_guard_band_holds_on_emulated_arithmetic(q):
 
 def test_mx_operands_make_the_hi_product_exact():
     """k_mx's B operands (jpgx_plan.cpp jx_mx_operands; v_mfma_f32_16x16x32_f16 layout: lane l
-    holds B[k = 8 (l >> 4) + e][column l & 15]; k < 24 the pixel-row bytes, k = 24 the bias,
-    k > 24 zero; operand 3 part + which, which 0 = Y | Cb columns, 1 = Cr in columns 0..7, 2 = Cr
-    in columns 8..15, the other half zero): the hi part is a multiple of 2^-11 whose products
-    with b - 128 sum below 2^13 in every column (so the MFMA's hi accumulation is exact in fp32
+    holds B[k = 8 (l >> 4) + e][column l & 15]; k < 24 the pixel-row bytes, stored x 2^15 (A is
+    the byte as the f16 subnormal b 2^-24), k = 24 the bias, stored x 2^-9 (A = 1.0), k > 24
+    zero; operand 3 part + which, which 0 = Y | Cb columns, 1 = Cr in columns 0..7, 2 = Cr in
+    columns 8..15, the other half zero): the hi part is a multiple of 2^-11 whose products with
+    bytes 0..255 sum below 2^13 in every column (so the MFMA's hi accumulation is exact in fp32
     whatever its internal order), and hi + lo [+ lo2] reconstruct the colour x cosine matrix and
-    the level-shift bias to the split's precision (the lo parts are stored scaled by 2^12)."""
+    the level-shift bias (-1024 for Y at u = 0, none for chroma) to the split's precision (the
+    lo parts are stored scaled by 2^12)."""
     import ctypes
     import math
     parts_n = jpgx.lib.jx_mx_parts()
@@ -159,6 +161,8 @@ def test_mx_operands_make_the_hi_product_exact():
     for lane in range(64):
         for e in range(8):
             B[:, :, 8 * (lane >> 4) + e, lane & 15] = vals.reshape(parts_n, 3, 64, 8)[:, :, lane, e]
+    B[:, :, :24] *= 2.0 ** -15                                  # the encodings' scales
+    B[:, :, 24] *= 2.0 ** 9
     assert not np.any(B[:, :, 25:, :])                          # K padding weighs 0
     assert not np.any(B[:, 1, :, 8:]) and not np.any(B[:, 2, :, :8])
     assert np.array_equal(B[:, 1, :, :8], B[:, 2, :, 8:])      # Cr of either set
@@ -167,7 +171,7 @@ def test_mx_operands_make_the_hi_product_exact():
     hi = M[0]
     lo = M[1:].sum(axis=0) * 2.0 ** -12                        # lo parts stored x 2^12
     assert np.all(hi * 2048 == np.round(hi * 2048))
-    assert np.all(128 * np.abs(hi[:24]).sum(axis=0) + np.abs(hi[24]) < 8192)
+    assert np.all(255 * np.abs(hi[:24]).sum(axis=0) + np.abs(hi[24]) < 8192)
     tol = 2 ** -30 if parts_n == 3 else 2 ** -23
     a = [(0.299, 0.587, 0.114), (-0.168736, 0.331264, -0.5), (0.5, -0.418688, -0.081312)]
     for c in range(3):
@@ -177,8 +181,65 @@ def test_mx_operands_make_the_hi_product_exact():
                 for p in range(3):
                     want = a[c][p] * math.cos((2 * x + 1) * u * math.pi / 16)
                     assert abs(hi[3 * x + p, n] + lo[3 * x + p, n] - want) < tol
-            bias = 8 * (128 * sum(a[c]) - (128 if c == 0 else 0)) if u == 0 else 0.0
+            bias = -1024.0 if (u == 0 and c == 0) else 0.0
             assert abs(hi[24, n] + lo[24, n] - bias) < tol * 512
+
+
+@pytest.mark.parametrize("q", [10, 50, 75, 90, 97])
+def test_mx422_guard_band_holds_on_emulated_arithmetic(q):
+    """k_mx422's chroma guard band (jpgx_plan.cpp jx_plan_tables_mx422: 48-byte rows of pixel
+    pairs, two K = 32 products per lo part) on the host emulation of its fast path against the
+    exact pair-averaged definition: no unflagged coefficient rounds differently."""
+    import ctypes
+    f = jpgx.lib.jx_selftest_mx422
+    f.restype = ctypes.c_longlong
+    f.argtypes = [ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_int,
+                  ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
+    flagged, ratio = ctypes.c_longlong(), ctypes.c_double()
+    assert f(600, 91 + q, q, ctypes.byref(flagged), ctypes.byref(ratio)) == 0
+    assert ratio.value < 0.6
+    assert flagged.value < 600 * 128 // 100
+
+
+def test_mx422_operands_reconstruct_the_pair_matrix():
+    """k_mx422's B operands (jx_mx422_operands, [part][which][lane][e]): which 0 / 1 = k_mx's Y
+    columns for set 0 (C columns 0..7) / set 1 (8..15), K = 25 used; which 2 / 3 = the chroma
+    matrix over k = 0..31 / 32..63: 0.5 a[c][p] cos((2 floor(x/2) + 1) u pi/16) at k = 3x + p <
+    48 (stored x 2^15, as k_mx's), zero from k = 48 on (chroma has no level-shift constant);
+    column j = Cb (j < 8) / Cr u.  The hi part is exact-accumulating (multiple of 2^-11, products
+    with bytes 0..255 below 2^13)."""
+    import ctypes
+    import math
+    parts_n = jpgx.lib.jx_mx_parts()
+    ops = np.zeros((parts_n, 4, 64, 8), np.uint16)
+    f = jpgx.lib.jx_mx422_operands
+    f.restype = ctypes.c_int
+    assert f(ops.ctypes.data_as(ctypes.c_void_p)) == 0
+    vals = ops.view(np.float16).astype(np.float64)
+    B = np.zeros((parts_n, 4, 32, 16))
+    for lane in range(64):
+        for e in range(8):
+            B[:, :, 8 * (lane >> 4) + e, lane & 15] = vals[:, :, lane, e]
+    B[:, :2, :24] *= 2.0 ** -15                                 # Y: byte rows and bias row
+    B[:, :2, 24] *= 2.0 ** 9
+    B[:, 2:] *= 2.0 ** -15                                      # chroma: byte rows (k < 48)
+    assert not np.any(B[:, 0, :, 8:]) and not np.any(B[:, 1, :, :8])
+    assert np.array_equal(B[:, 0, :, :8], B[:, 1, :, 8:])
+    assert not np.any(B[:, :2, 25:, :])
+    C = np.concatenate([B[:, 2], B[:, 3]], axis=1)              # [part][k 0..63][16]
+    assert not np.any(C[:, 48:, :])
+    hi, lo = C[0], C[1:].sum(axis=0) * 2.0 ** -12
+    assert np.all(hi * 2048 == np.round(hi * 2048))
+    assert np.all(255 * np.abs(hi[:48]).sum(axis=0) < 8192)
+    tol = 2 ** -30 if parts_n == 3 else 2 ** -23
+    a = [(-0.168736, 0.331264, -0.5), (0.5, -0.418688, -0.081312)]
+    for c in range(2):
+        for u in range(8):
+            n = 8 * c + u
+            for x in range(16):
+                for p in range(3):
+                    want = 0.5 * a[c][p] * math.cos((2 * (x // 2) + 1) * u * math.pi / 16)
+                    assert abs(hi[3 * x + p, n] + lo[3 * x + p, n] - want) < tol
 
 
 def test_packed_transform_matches_scalar_bit_for_bit():

@@ -1,14 +1,17 @@
 #!/bin/bash
-# PMC passes for one kernel ($1 = mx, or xform from the test-only libjpgx_alt.so), one counter group per rocprofv3 run.
+# PMC passes for one kernel ($1 = a name: xform = the test-only libjpgx_alt.so; the rest of the
+# arguments go to bench.py, e.g. --subsample --sample-ratio 1 --quality 75), one counter group per
+# rocprofv3 run.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
 if [ "$1" = xform ]; then export JPGX_LIB="$ROOT/jpeg-encoder-and-decoder_amd/lib/libjpgx_alt.so"; fi
-OUT="$ROOT/gpurun_out/pmc1_$1"; mkdir -p "$OUT"
+NAME=$1; shift
+OUT="$ROOT/gpurun_out/pmc1_$NAME"; mkdir -p "$OUT"
 cd /tmp
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT" "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_ACTIVE_INST_FLAT SQ_INSTS_FLAT"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- python "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/p$i.log" 2>&1; rc=$?
-  echo "$1 pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.log"; exit $rc; }
+  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- python "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline "$@" > "$OUT/p$i.log" 2>&1; rc=$?
+  echo "$NAME pmc pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.log"; exit $rc; }
 done
