@@ -71,6 +71,9 @@ constexpr unsigned kRing = 4;           /* LDS input slots: one chunk (step k in
 constexpr unsigned kVmWait = 5 * kDist - 2;
 constexpr int kWaitImm = (int)((kVmWait & 15u) | ((kVmWait >> 4) << 14) | 0xF70u);
 static_assert(kVmWait < 64, "vmcnt is 6 bits");
+#ifndef JX_MX_DYNLDS
+#define JX_MX_DYNLDS 0                  /* timing experiments only: extra LDS per workgroup (lower occupancy) */
+#endif
 #ifndef JX_MX_WPE
 #define JX_MX_WPE 3                     /* waves per SIMD the register allocation targets    */
 #endif
@@ -237,14 +240,17 @@ struct MxJump {
     unsigned jb, jr, jc, rows;          /* 32 nw blocks = jr block-rows + jc blocks; rows/frame */
 };
 
+/* CB = blocks per chunk (k_mx 32, k_mx422 24) */
+template <unsigned CB>
 __device__ __forceinline__ void mx_chunk_ptrs(MxChunk &C, const MxG &g)
 {
     C.src = g.rgb + (long long)C.f * g.fstride + 8ll * C.r * g.pitch + 24ll * C.c;
     C.dst = g.out + (long long)C.f * g.ofstride + 64ll * C.bi;
     C.cdst = g.out + (long long)C.f * g.ofstride + 64ll * (g.nb + C.bi / 2u);
-    C.simple = C.b0 + 32u <= g.total && C.c + 32u < g.bpr && g.lin_store;
+    C.simple = C.b0 + CB <= g.total && C.c + CB < g.bpr && g.lin_store;
 }
 
+template <unsigned CB>
 __device__ __forceinline__ void mx_chunk_at(MxChunk &C, const MxG &g, unsigned b0)
 {
     C.b0 = b0;
@@ -252,10 +258,11 @@ __device__ __forceinline__ void mx_chunk_at(MxChunk &C, const MxG &g, unsigned b
     C.bi = b0 - C.f * g.nb;
     C.r = C.bi / g.bpr;
     C.c = C.bi - C.r * g.bpr;
-    mx_chunk_ptrs(C, g);
+    mx_chunk_ptrs<CB>(C, g);
 }
 
-/* the wave's next chunk, 32 nw blocks on: no division */
+/* the wave's next chunk, CB nw blocks on: no division */
+template <unsigned CB>
 __device__ __forceinline__ void mx_chunk_next(MxChunk &C, const MxG &g, const MxJump &J)
 {
     C.b0 += J.jb;
@@ -272,7 +279,7 @@ __device__ __forceinline__ void mx_chunk_next(MxChunk &C, const MxG &g, const Mx
         C.r -= J.rows;
         C.f++;
     }
-    mx_chunk_ptrs(C, g);
+    mx_chunk_ptrs<CB>(C, g);
 }
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -649,7 +656,7 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     J.jc = J.jb - J.jr * g.bpr;
     J.rows = g.nb / g.bpr;
     MxChunk cc;
-    mx_chunk_at(cc, g, 32u * wv);
+    mx_chunk_at<32>(cc, g, 32u * wv);
     MxChunk nx = cc;
 
     /* DMA of step k of chunk C into ring slot k (the slot the step computes from) */
@@ -689,7 +696,7 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         if (k + kDist < kChunk) {
             issue(cc, k + kDist);
         } else {
-            if (k + kDist == kChunk) mx_chunk_next(nx, g, J);
+            if (k + kDist == kChunk) mx_chunk_next<32>(nx, g, J);
             issue(nx, k + kDist - kChunk);
         }
         /* A operands: set 0/1 x half lo/hi */
@@ -806,20 +813,26 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
 
 /* ==== k_mx422: true 4:2:2 (extension, JPGX_FLAG_SUBSAMPLE, sample_ratio 1) ==================
  *
- * The same persistent chunk loop, LDS-DMA ring and per-step bookkeeping as k_mx; a step is 8 Y
- * blocks = 4 MCUs (chroma block cb of the step = Y blocks 2 cb, 2 cb + 1: W is a multiple of 16
- * and steps start at multiples of 8, so an MCU never straddles a step or a block-row).
+ * k_mx's chunk loop, LDS-DMA ring and per-step bookkeeping; a step is 8 Y blocks = 4 MCUs
+ * (chroma block cb of the step = Y blocks 2 cb, 2 cb + 1: W is a multiple of 16 and steps start
+ * at multiples of 8, so an MCU never straddles a step or a block-row).
  *   Y       k_mx's Y row transform with the two sets concatenated along K (B_Y0 zero in columns
  *           8..15, B_Y1 in 0..7): column j of the C tile is set j / 8's Y at u = j % 8.
  *   Chroma  A row m = chroma block m >> 2, pixel row m & 3 of the half, K = the 48 bytes of the
- *           MCU's pixel row + the bias, over two K = 32 products; B (jpgx_plan.cpp
- *           jx_mx422_operands) holds 0.5 a[c][p] cos((2 floor(x/2) + 1) u pi/16), so column j is
- *           the row transform of the pair-averaged level-shifted chroma: Cb (j < 8) or Cr of
- *           chroma block gq at u = j % 8.  Same hi / lo split and rigorous band
- *           (jx_plan_tables_mx422: 65 fp32 additions per lo part instead of 33).
- *   Columns each lane holds two: Y and chroma -> 16 MFMAs and 2 x 8 column DCTs per step (k_mx:
- *           16 and 3 x 8), output 1 KiB Y + 512 B Cb + 512 B Cr in two stores (lanes 0..31 Cb,
- *           32..63 Cr).
+ *           MCU's pixel row over two K = 32 products; B (jpgx_plan.cpp jx_mx422_operands) holds
+ *           0.5 a[c][p] cos((2 floor(x/2) + 1) u pi/16), so column j is the row transform of the
+ *           pair-averaged level-shifted chroma: Cb (j < 8) or Cr of chroma block gq at u = j % 8.
+ *           Same encoding, split and rigorous band as k_mx (jx_plan_tables_mx422: 65 fp32
+ *           additions per lo part instead of 33).
+ *   Columns each lane holds two, Y block (j / 8) 4 + gq and chroma block (channel j / 8, gq):
+ *           16 MFMAs and 2 x 8 column DCTs per step (k_mx: 16 and 3 x 8); 1 KiB Y + 512 B Cb +
+ *           512 B Cr leave in two stores (lanes 0..31 Cb, 32..63 Cr).
+ *   Occupancy  four waves per SIMD (the kernel is latency-bound: at two waves it runs 1.5x
+ *           slower than at three): <= 128 VGPRs and 40 KiB of LDS per workgroup -- a ring of three
+ *           slots (chunks of three steps), the per-lane scales and band limits in a 2-KiB
+ *           workgroup table read per column, and one set of stage addresses for both columns
+ *           (stage layout: Y block jb at 144 jb, chroma (c, cb) at 1152 + 144 (4 c + cb), so the
+ *           chroma column's address is the Y column's plus a constant).
  *   Quirk   the x0 = -8 quirk shifts a row-last Y block's rows by one (Y only); a general step
  *           holding such a block loads the block's true rows into L.qtrue for its chroma block.
  *   Exact   deferred / inline as k_mx; a chroma task carries the MCU's 8 x 48 bytes (two side
@@ -827,16 +840,19 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
  *           dct_coef): X = (ls(2X) + ls(2X+1)) * 0.5, ls = the level-shifted chroma in
  *           preprocess.c's operation order.
  */
-#ifndef JX_DBG_NOQ
-#define JX_DBG_NOQ 0
-#endif
+constexpr unsigned kSteps422 = 3;             /* steps per chunk = ring slots */
+constexpr unsigned kCB422 = 8 * kSteps422;    /* blocks per chunk */
+static_assert(kDist == 2, "k_mx422: a ring of three slots holds the step and two ahead");
 constexpr unsigned kVmWait422 = 4 * kDist - 2;    /* 2 stores x kDist steps + 2 DMA x (kDist - 1) */
 constexpr int kWaitImm422 = (int)((kVmWait422 & 15u) | ((kVmWait422 >> 4) << 14) | 0xF70u);
+constexpr unsigned kSt422C = 8 * kBS;         /* chroma (c, cb) at kSt422C + kBS (4 c + cb) */
+#ifndef JX_MX422_WPE
+#define JX_MX422_WPE 4
+#endif
 
 struct Mx422Lds {
-    uint8_t ring[kRing][kSlot];
-    uint8_t stage[kStageBytes];         /* Cb block cb at mx_sb(0) + 144 cb, Cr at mx_sb(1) + ..,
-                                           Y block jb at mx_sb(2) + 144 jb                       */
+    uint8_t ring[kSteps422][kSlot];
+    uint8_t stage[16 * kBS];
     uint8_t qtrue[4][192];              /* general step: true rows [y][24] of row-last block 2cb+1 */
     uint8_t pix[kSide][192];            /* deferred blocks: Y [y][24] in one slot, an MCU [y][48]
                                            in two                                                */
@@ -845,12 +861,18 @@ struct Mx422Lds {
     uint16_t task[8];
     uint32_t dummy[64];
 };
-static_assert(sizeof(Mx422Lds) * 4 * 3 <= 160 * 1024, "3 workgroups of 4 waves per CU");
+/* per-lane scales / band limits, shared by the workgroup: table t (Wy, Ly, Wc, Lc), half h (pairs
+ * 2h, 2h + 1 in jx_pk_k order), profile j = lane & 15 -- a column's read of one (t, h) by the
+ * wave touches 16 consecutive 16-byte entries, every bank once */
+struct Mx422Tab {
+    mx_f4 wl[4][2][16];
+};
+static_assert(sizeof(Mx422Lds) * 4 + sizeof(Mx422Tab) <= 40 * 1024, "4 workgroups of 4 waves per CU");
 
 __device__ mx_u4 g_mx422B[JX_MX_PARTS * 4][64];  /* [part * 4 + which][lane] */
 __device__ jx_mxtab g_mx422tab[2][JX_MAXQ + 1];  /* n = 8 c + u: c = 0 Y, 1 Cb, 2 Cr */
 
-/* Y block of a lane's Y column (lane (gq, j): set j / 8) */
+/* Y block of a lane's columns (lane (gq, j): set j / 8); also the chroma column's stage slot */
 __device__ __forceinline__ unsigned mx422_yblock(unsigned sl)
 {
     return (sl & 15u) < 8 ? (sl >> 4) : 4u + (sl >> 4);
@@ -913,25 +935,22 @@ __device__ __forceinline__ void mx422_exact_inline(Mx422Lds &L, const uint8_t *s
         const unsigned code = L.task[live ? i : 0u];
         const unsigned sl = code >> 8, k = (code >> 3) & 1u, v = code & 7u;
         const unsigned jj = sl & 15u, u = jj & 7u;
-        unsigned ch, rs, d1, st;
+        const unsigned slot = mx422_yblock(sl);       /* Y block, or 4 c + cb for chroma */
+        unsigned ch, rs, d1;
         const lds_u8 *row0;
         if (k == 0) {
-            const unsigned jb = mx422_yblock(sl);
             ch = 0;
             rs = 192u;
             d1 = 0;
-            row0 = mx_lds((void *)sp) + 24u * jb + 3u * x;
-            st = mx_sb(2) + kBS * jb;
+            row0 = mx_lds((void *)sp) + 24u * slot + 3u * x;
         } else {
-            const unsigned cb = sl >> 4;
             ch = 1u + (jj >> 3);
             d1 = 3;
-            row0 = mx422_mcu_row0(L, sp, qmask, cb, x, rs);
-            st = mx_sb(jj >> 3) + kBS * cb;
+            row0 = mx422_mcu_row0(L, sp, qmask, sl >> 4, x, rs);
         }
         const int val = mx_exact_pair(row0, rs, d1, ch, u, v, x, T);
         if (live && x == 7)
-            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + st +
+            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + (k ? kSt422C : 0u) + kBS * slot +
                                                            2u * (unsigned)kMxScan[v][u]) = (int16_t)val;
         mx_wave_sync();
     }
@@ -1093,9 +1112,48 @@ __device__ __forceinline__ uint32_t mx422_true_rows(Mx422Lds &L, const MxG &g, u
     return qm;
 }
 
-__global__ __launch_bounds__(256, JX_MX_WPE) void k_mx422(const jx_xform_args a)
+/* a column's scales and band limits from the workgroup table (W pairs then L pairs) */
+struct Mx422WL {
+    mx_f4 w01, w23, l01, l23;
+};
+/* t0 = 0 (Y) or 2 (chroma) */
+__device__ __forceinline__ Mx422WL mx422_wl(const Mx422Tab &tb, unsigned t0, unsigned j)
+{
+    return Mx422WL{tb.wl[t0][0][j], tb.wl[t0][1][j], tb.wl[t0 + 1][0][j], tb.wl[t0 + 1][1][j]};
+}
+
+/* Column pass of one column (R pairs), quantiser, stage writes at za[v] + OFF, band flags (rare
+ * path) into fl */
+template <unsigned OFF>
+__device__ __forceinline__ void mx422_column(const mx_f4 (&acc)[4], const Mx422WL &t, const uint32_t (&za)[8],
+                                             uint32_t &fl, int kc)
+{
+    mx_f2 R[4], F[4];
+    mx_combine(acc[0], acc[1], acc[2], acc[3], R);
+    jx_fdct8_pk<MxPair>(R, F);
+    const mx_f4 w01 = t.w01, w23 = t.w23, l01 = t.l01, l23 = t.l23;
+    const mx_f2 W[4] = {mx_f2{w01.x, w01.y}, mx_f2{w01.z, w01.w}, mx_f2{w23.x, w23.y}, mx_f2{w23.z, w23.w}};
+    const mx_f2 Lq[4] = {mx_f2{l01.x, l01.y}, mx_f2{l01.z, l01.w}, mx_f2{l23.x, l23.y}, mx_f2{l23.z, l23.w}};
+    const mx_f2 M2 = {kMagic, kMagic};
+    typedef __attribute__((address_space(3))) uint16_t l16;
+    float em = -1.0f;
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
+        *(l16 *)(uintptr_t)(za[jx_pk_k(p, 0)] + OFF) = (uint16_t)__float_as_uint(tm.x);
+        *(l16 *)(uintptr_t)(za[jx_pk_k(p, 1)] + OFF) = (uint16_t)__float_as_uint(tm.y);
+        const mx_f2 rr = tm - M2;
+        const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
+        const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
+        em = __builtin_fmaxf(__builtin_fmaxf(em, e.x), e.y);
+    }
+    if (__builtin_expect(__ballot(em >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * kc);
+}
+
+__global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args a)
 {
     __shared__ __attribute__((aligned(16))) Mx422Lds s_lds[4];
+    __shared__ __attribute__((aligned(16))) Mx422Tab s_tab;
     MxG g;
     g.rgb = a.g.rgb;
     g.out = a.g.out;
@@ -1114,9 +1172,26 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx422(const jx_xform_args a)
 
     const unsigned lane = threadIdx.x & 63u;
     Mx422Lds &L = s_lds[threadIdx.x >> 6];
+    const jx_mxtab &T = g_mx422tab[g.force ? 1 : 0][g.quality];
+    /* the workgroup's scale / limit table: wave 0, lane (t = lane >> 4, profile j = lane & 15) */
+    if (threadIdx.x < 64) {
+        const unsigned t = lane >> 4, jp = lane & 15u;
+        const unsigned n = t < 2 ? (jp & 7u) : 8u + jp;
+        float x[8];
+#pragma unroll
+        for (int p = 0; p < 4; p++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int v = jx_pk_k(p, h);
+                x[2 * p + h] = (t & 1u) ? T.lsq[n][v] : T.w[n][v];
+            }
+        s_tab.wl[t][0][jp] = mx_f4{x[0], x[1], x[2], x[3]};
+        s_tab.wl[t][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
+    }
+    __syncthreads();
     const unsigned nw = gridDim.x * 4u;
     const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    if (32u * wv >= g.total) return;
+    if (kCB422 * wv >= g.total) return;
 
     /* Y A operands as k_mx's; chroma: row m = (chroma block m >> 2, pixel row m & 3 of the
      * half), k-step 0 bytes 8q.. of the MCU's 48-byte row, k-step 1 bytes 32 + 8q (q < 2), the
@@ -1133,28 +1208,19 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx422(const jx_xform_args a)
     const uint32_t t2 = q < 2 ? kSelLo : kSelZero;
     const uint32_t off0 = (uint32_t)((lane / 12u) * (unsigned)g.pitch + 16u * (lane % 12u));
     const uint32_t off1 = (uint32_t)(((64u + lane) / 12u) * (unsigned)g.pitch + 16u * ((64u + lane) % 12u));
-    /* stores: Y 8 blocks x 128 B (lane 16 B), chroma lanes 0..31 Cb / 32..63 Cr 4 blocks x 128 B */
+    /* stores: Y 8 blocks x 128 B (lane 16 B), chroma lanes 0..31 Cb / 32..63 Cr 4 blocks x 128 B;
+     * both read the stage at ro (+ kSt422C) */
     const uint32_t soy = lane * 16u, soc = (lane & 31u) * 16u + (lane >> 5) * (g.nb / 2u) * 128u;
-    const uint32_t roy = mx_sb(2) + (lane >> 3) * kBS + (lane & 7u) * 16u;
-    const uint32_t roc = mx_sb(lane >> 5) + ((lane >> 3) & 3u) * kBS + (lane & 7u) * 16u;
+    const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
 
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
-    const jx_mxtab &T = g_mx422tab[g.force ? 1 : 0][g.quality];
-    const unsigned nyc = u, ncc = 8u + j;                  /* plan columns */
-    mx_f2 Wy[4], Ly[4], Wc[4], Lc[4];
+    /* LDS addresses of the lane's 8 coefficients in the stage (Y column; chroma + kSt422C) */
+    uint32_t za[8];
+    {
+        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * ((j >> 3) * 4u + gq);
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
-        const int v0 = jx_pk_k(p, 0), v1 = jx_pk_k(p, 1);
-        Wy[p] = mx_f2{T.w[nyc][v0], T.w[nyc][v1]};
-        Ly[p] = mx_f2{T.lsq[nyc][v0], T.lsq[nyc][v1]};
-        Wc[p] = mx_f2{T.w[ncc][v0], T.w[ncc][v1]};
-        Lc[p] = mx_f2{T.lsq[ncc][v0], T.lsq[ncc][v1]};
+        for (int v = 0; v < 8; v++) za[v] = base + 2u * (unsigned)kMxScan[v][u];
     }
-    uint32_t zo[8];
-#pragma unroll
-    for (int v = 0; v < 8; v++) zo[v] = 2u * (unsigned)kMxScan[v][u];
-    uint8_t *const sty = L.stage + mx_sb(2) + kBS * (j < 8 ? gq : 4u + gq);
-    uint8_t *const stc = L.stage + mx_sb(j >> 3) + kBS * gq;
     mx_u4 B[kParts][4];
 #pragma unroll
     for (int p = 0; p < kParts; p++)
@@ -1166,12 +1232,12 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx422(const jx_xform_args a)
     __builtin_amdgcn_s_waitcnt(0xF70);
 
     MxJump J;
-    J.jb = 32u * nw;
+    J.jb = kCB422 * nw;
     J.jr = J.jb / g.bpr;
     J.jc = J.jb - J.jr * g.bpr;
     J.rows = g.nb / g.bpr;
     MxChunk cc;
-    mx_chunk_at(cc, g, 32u * wv);
+    mx_chunk_at<kCB422>(cc, g, kCB422 * wv);
     MxChunk nx = cc;
 
     const auto issue = [&](const MxChunk &C, unsigned k) {
@@ -1197,49 +1263,20 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx422(const jx_xform_args a)
     unsigned k = 0;
     for (;;) {
         const unsigned b0 = cc.b0 + 8u * k;
-        /* younger than this step's DMA: the two stores of steps s-2, s-1 and step s+1's DMA */
+        /* younger than this step's DMA: the two stores of each of the kDist steps before it and
+         * the DMA of the kDist - 1 steps after it */
         __builtin_amdgcn_s_waitcnt(kWaitImm422);
         mx_wave_sync();
         const uint8_t *const sp = L.ring[k];
-        if (k + kDist < kChunk) {
+        if (k + kDist < kSteps422) {
             issue(cc, k + kDist);
         } else {
-            if (k + kDist == kChunk) mx_chunk_next(nx, g, J);
-            issue(nx, k + kDist - kChunk);
+            if (k + kDist == kSteps422) mx_chunk_next<kCB422>(nx, g, J);
+            issue(nx, k + kDist - kSteps422);
         }
         const uint32_t qmask = cc.simple ? 0u : mx422_true_rows(L, g, b0);
-        const mx_u2 y00 = *(const mx_u2 *)(sp + aoff);
-        const mx_u2 y01 = *(const mx_u2 *)(sp + aoff + 768u);
-        const mx_u2 y10 = *(const mx_u2 *)(sp + aoff + 96u);
-        const mx_u2 y11 = *(const mx_u2 *)(sp + aoff + 864u);
-        mx_u2 c00, c01, c10, c11;
-        if (JX_DBG_NOQ || __builtin_expect(qmask == 0, 1)) {
-            c00 = *(const mx_u2 *)(sp + coff0);
-            c01 = *(const mx_u2 *)(sp + coff0 + 768u);
-            c10 = *(const mx_u2 *)(sp + coff1);
-            c11 = *(const mx_u2 *)(sp + coff1 + 768u);
-        } else {
-            /* chroma blocks with a row-last right block: its bytes (24..47 of the MCU row)
-             * from the true rows */
-            const unsigned l = mx_lane(), mm = l & 15u, qq = l >> 4, cb = mm >> 2;
-            const bool qb = (qmask >> cb) & 1u;
-            const uint8_t *qt = L.qtrue[cb] + 24u * (mm & 3u);
-            const uint8_t *p0 = qb && qq == 3 ? qt : sp + coff0;
-            const uint8_t *p1 = qb && qq < 2 ? qt + 8u + 8u * qq : sp + coff1;
-            const unsigned h0 = qb && qq == 3 ? 96u : 768u, h1 = qb && qq < 2 ? 96u : 768u;
-            c00 = *(const mx_u2 *)p0;
-            c01 = *(const mx_u2 *)(p0 + h0);
-            c10 = *(const mx_u2 *)p1;
-            c11 = *(const mx_u2 *)(p1 + h1);
-        }
-        const mx_h8 Y00 = mx_aop(y00, s0, s1, s2), Y01 = mx_aop(y01, s0, s1, s2);
-        const mx_h8 Y10 = mx_aop(y10, s0, s1, s2), Y11 = mx_aop(y11, s0, s1, s2);
-        const mx_h8 C00 = mx_aop(c00, kSelLo, kSelHi, kSelLo);
-        const mx_h8 C01 = mx_aop(c01, kSelLo, kSelHi, kSelLo);
-        const mx_h8 C10 = mx_aop(c10, t0, t1, t2), C11 = mx_aop(c11, t0, t1, t2);
         const mx_f4 z = {};
         uint32_t fl = 0;
-        mx_f2 R[4], F[4];
         mx_f4 acc[2][4];                               /* [Y, chroma][hl, ll, hh, lh] */
         const auto mma2 = [&](mx_f4(&o)[4], const mx_h8 &Al0, const mx_h8 &Ah0, const mx_h8 &Al1,
                               const mx_h8 &Ah1, int w0) {
@@ -1258,27 +1295,49 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx422(const jx_xform_args a)
                 o[3] = mx_mma(Ah1, B[kParts - 1][w0 + 1], o[3]);
             }
         };
-        const auto column = [&](int kc) {
-            mx_combine(acc[kc][0], acc[kc][1], acc[kc][2], acc[kc][3], R);
-            float e = -1.0f;
-            const mx_f2(&W)[4] = kc == 0 ? Wy : Wc;
-            const mx_f2(&Lq)[4] = kc == 0 ? Ly : Lc;
-            mx_column(R, W, Lq, kc == 0 ? sty : stc, zo, e, F);
-            if (__builtin_expect(__ballot(e >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * kc);
-        };
-        mma2(acc[0], Y00, Y01, Y10, Y11, 0);
+        /* every LDS read of the step is issued ahead of the work that waits for it: the A
+         * operands first, a column's scales / limits one phase before the column */
+        const mx_u2 y00 = *(const mx_u2 *)(sp + aoff);
+        const mx_u2 y01 = *(const mx_u2 *)(sp + aoff + 768u);
+        const mx_u2 y10 = *(const mx_u2 *)(sp + aoff + 96u);
+        const mx_u2 y11 = *(const mx_u2 *)(sp + aoff + 864u);
+        mx_u2 c00, c01, c10, c11;
+        {
+            if (__builtin_expect(qmask == 0, 1)) {
+                c00 = *(const mx_u2 *)(sp + coff0);
+                c01 = *(const mx_u2 *)(sp + coff0 + 768u);
+                c10 = *(const mx_u2 *)(sp + coff1);
+                c11 = *(const mx_u2 *)(sp + coff1 + 768u);
+            } else {
+                /* chroma blocks with a row-last right block: its bytes (24..47 of the MCU row)
+                 * from the true rows */
+                const unsigned l = mx_lane(), mm = l & 15u, qq = l >> 4, cb = mm >> 2;
+                const bool qb = (qmask >> cb) & 1u;
+                const uint8_t *qt = L.qtrue[cb] + 24u * (mm & 3u);
+                const uint8_t *p0 = qb && qq == 3 ? qt : sp + coff0;
+                const uint8_t *p1 = qb && qq < 2 ? qt + 8u + 8u * qq : sp + coff1;
+                const unsigned h0 = qb && qq == 3 ? 96u : 768u, h1 = qb && qq < 2 ? 96u : 768u;
+                c00 = *(const mx_u2 *)p0;
+                c01 = *(const mx_u2 *)(p0 + h0);
+                c10 = *(const mx_u2 *)p1;
+                c11 = *(const mx_u2 *)(p1 + h1);
+            }
+        }
+        mma2(acc[0], mx_aop(y00, s0, s1, s2), mx_aop(y01, s0, s1, s2), mx_aop(y10, s0, s1, s2),
+             mx_aop(y11, s0, s1, s2), 0);
         __builtin_amdgcn_sched_barrier(0);
-        mma2(acc[1], C00, C01, C10, C11, 2);
+        mma2(acc[1], mx_aop(c00, kSelLo, kSelHi, kSelLo), mx_aop(c01, kSelLo, kSelHi, kSelLo),
+             mx_aop(c10, t0, t1, t2), mx_aop(c11, t0, t1, t2), 2);
         __builtin_amdgcn_sched_barrier(0);
-        column(0);
+        mx422_column<0>(acc[0], mx422_wl(s_tab, 0, j), za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
-        column(1);
+        mx422_column<kSt422C>(acc[1], mx422_wl(s_tab, 2, j), za, fl, 1);
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx422_defer_step(L, sp, qmask, fl, b0, nq, ns, g, T);
         /* always two store instructions per step (the vmcnt accounting counts on it) */
         if (cc.simple) {
-            const mx_u4 vy = *(const mx_u4 *)(L.stage + roy);
-            const mx_u4 vc = *(const mx_u4 *)(L.stage + roc);
+            const mx_u4 vy = *(const mx_u4 *)(L.stage + ro);
+            const mx_u4 vc = *(const mx_u4 *)(L.stage + kSt422C + ro);
             __builtin_nontemporal_store(vy, (mx_u4 *)((const uint8_t *)(cc.dst + 512u * k) + soy));
             __builtin_nontemporal_store(vc, (mx_u4 *)((const uint8_t *)(cc.cdst + 256u * k) + soc));
         } else {
@@ -1287,8 +1346,9 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx422(const jx_xform_args a)
             const unsigned yb = by < g.total ? by : g.total - 1u, cbk = bc < g.total ? bc : g.total - 1u;
             const unsigned fy = yb / g.nb, biy = yb - fy * g.nb;
             const unsigned fc = cbk / g.nb, bic = cbk - fc * g.nb;
-            const mx_u4 vy = *(const mx_u4 *)(L.stage + mx_sb(2) + (l >> 3) * kBS + (l & 7u) * 16u);
-            const mx_u4 vc = *(const mx_u4 *)(L.stage + mx_sb(l >> 5) + ((l >> 3) & 3u) * kBS + (l & 7u) * 16u);
+            const uint32_t rl = (l >> 3) * kBS + (l & 7u) * 16u;
+            const mx_u4 vy = *(const mx_u4 *)(L.stage + rl);
+            const mx_u4 vc = *(const mx_u4 *)(L.stage + kSt422C + rl);
             if (by < g.total)
                 __builtin_nontemporal_store(
                     vy, (mx_u4 *)(g.out + (long long)fy * g.ofstride + (long long)biy * 64 + (l & 7u) * 8));
@@ -1298,7 +1358,7 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx422(const jx_xform_args a)
                                   ((long long)g.nb + (l >> 5) * (g.nb / 2u) + bic / 2u) * 64 + (l & 7u) * 8));
         }
         mx_wave_sync();
-        if (++k == kChunk) {
+        if (++k == kSteps422) {
             k = 0;
             cc = nx;
             if (cc.b0 >= g.total) break;
@@ -1356,7 +1416,7 @@ int mx_tables_for_current_device(int *waves)
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mx, 256, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mx, 256, JX_MX_DYNLDS) != hipSuccess ||
             per_cu < 1)
             per_cu = 2;
         g_mx_waves[dev] = cus * per_cu * 4;
@@ -1400,7 +1460,7 @@ int mx422_tables_for_current_device(int *waves)
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mx422, 256, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mx422, 256, JX_MX_DYNLDS) != hipSuccess ||
             per_cu < 1)
             per_cu = 2;
         g_mx422_waves[dev] = cus * per_cu * 4;
@@ -1424,7 +1484,7 @@ extern "C" int jx_launch_mx422(const jx_xform_args *xa, void *stream)
     const size_t nsteps = (total + 7) / 8;
     const size_t w = std::min<size_t>(nsteps, (size_t)std::max(waves, 4));
     const unsigned grid = (unsigned)((w + 3) / 4);
-    hipLaunchKernelGGL(k_mx422, dim3(grid), dim3(256), 0, (hipStream_t)stream, *xa);
+    hipLaunchKernelGGL(k_mx422, dim3(grid), dim3(256), JX_MX_DYNLDS, (hipStream_t)stream, *xa);
     return mx_rc(hipGetLastError());
 }
 
@@ -1443,6 +1503,6 @@ extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)
     const size_t w = JX_MX_NP ? (nsteps + JX_MX_NP - 1) / JX_MX_NP
                               : std::min<size_t>(nsteps, (size_t)std::max(waves, 4));
     const unsigned grid = (unsigned)((w + 3) / 4);
-    hipLaunchKernelGGL(k_mx, dim3(grid), dim3(256), 0, (hipStream_t)stream, *xa);
+    hipLaunchKernelGGL(k_mx, dim3(grid), dim3(256), JX_MX_DYNLDS, (hipStream_t)stream, *xa);
     return mx_rc(hipGetLastError());
 }
