@@ -65,7 +65,7 @@ constexpr unsigned kSlot = 1536;        /* one step's pixels: [y][8 blocks x 24 
 #define JX_MX_DIST 2                    /* DMA issued this many steps ahead                  */
 #endif
 constexpr unsigned kDist = JX_MX_DIST;
-constexpr unsigned kRing = 4;           /* LDS input slots: one chunk (step k in slot k)      */
+constexpr unsigned kSteps = 3;          /* steps per chunk = LDS input slots (step k in slot k) */
 /* s_waitcnt immediate for vmcnt(5 kDist - 2): the VMEM operations younger than a step's DMA
  * (kDist steps' 3 stores each, kDist - 1 steps' 2 DMA pieces each) */
 constexpr unsigned kVmWait = 5 * kDist - 2;
@@ -75,27 +75,41 @@ static_assert(kVmWait < 64, "vmcnt is 6 bits");
 #define JX_MX_DYNLDS 0                  /* timing experiments only: extra LDS per workgroup (lower occupancy) */
 #endif
 #ifndef JX_MX_WPE
-#define JX_MX_WPE 3                     /* waves per SIMD the register allocation targets    */
+#define JX_MX_WPE 4                     /* waves per SIMD the register allocation targets    */
 #endif
 
-/* LDS stage: channel c's 8 blocks at mx_sb(c) + 144 jb, 128 B each in zig-zag order.  The
- * 16-B block padding and the channel offsets keep the column writes at most 3-way (mean 2.3)
- * on a bank and the 16-B store reads conflict-free (searched offline). */
-__host__ __device__ constexpr unsigned mx_sb(unsigned c) { return c == 0 ? 0u : (c == 1 ? 1216u : 2368u); }
+/* LDS stage: 128 B per block in zig-zag order, 16 B of padding between blocks (kBS).  k_mx's
+ * block (c, jb) sits at slot mx_pos(c, jb): Y 0..7, Cr 0..3 at 8..11, Cb at 12..19, Cr 4..7 at
+ * 20..23 -- so that a lane's three columns, (c = j / 8, gq), (c = j / 8, 4 + gq) and (Cr,
+ * 4 (j / 8) + gq), lie at one lane address plus 0, 4 and 8 slots (one set of address registers
+ * with immediate offsets). */
 constexpr unsigned kBS = 144;
-constexpr unsigned kStageBytes = 2368 + 8 * kBS;
+__host__ __device__ constexpr unsigned mx_pos(unsigned c, unsigned jb)
+{
+    return c == 0 ? jb : (c == 1 ? 12u + jb : (jb < 4 ? 8u + jb : 16u + jb));
+}
+constexpr unsigned kStageBytes = 24 * kBS;
 
-constexpr int kSide = 8;                /* deferred exact tasks (and their blocks) per wave  */
-struct MxLds {
-    uint8_t ring[kRing][kSlot];
+constexpr int kSide = 8;                /* deferred exact tasks per flush (8-lane groups)    */
+constexpr int kSidePix = 6;             /* k_mx: deferred blocks' pixel slots per wave       */
+struct alignas(16) MxLds {          /* 16-byte aligned: every wave's DMA slots and stage */
+    uint8_t ring[kSteps][kSlot];
     uint8_t stage[kStageBytes];
-    uint8_t pix[kSide][192];            /* deferred blocks' pixel rows, [y][24]              */
-    uint32_t sblk[kSide];               /* and their launch-global block indices             */
+    uint8_t pix[kSidePix][192];         /* deferred blocks' pixel rows, [y][24]              */
+    uint32_t sblk[kSidePix];            /* and their launch-global block indices             */
     uint16_t dtask[kSide];              /* deferred tasks: slot << 8 | c << 6 | v << 3 | u   */
     uint16_t task[8];                   /* inline batch: source lane << 8 | column << 3 | v  */
     uint32_t dummy[64];                 /* landing area of padding DMA operations            */
 };
-static_assert(kSlot % 16 == 0 && kStageBytes % 16 == 0, "16-byte aligned LDS regions");
+static_assert(kSlot % 16 == 0 && kStageBytes % 16 == 0 && sizeof(MxLds) % 16 == 0, "16-byte aligned LDS regions");
+/* per-lane scales / band limits, shared by the workgroup: table t, half h (pairs 2h, 2h + 1 in
+ * jx_pk_k order), profile j = lane & 15 -- a column's read of one (t, h) by the wave touches 16
+ * consecutive 16-byte entries, every bank once.  k_mx: t = Wy|b, Ly|b (plan column j), Wr, Lr
+ * (16 + j % 8); k_mx422: Wy, Ly (j % 8), Wc, Lc (8 + j). */
+struct MxTab {
+    mx_f4 wl[4][2][16];
+};
+static_assert(sizeof(MxLds) * 4 + sizeof(MxTab) <= 40 * 1024, "4 workgroups of 4 waves per CU");
 
 __device__ mx_u4 g_mxB[3 * JX_MX_PARTS][64];     /* B operands: (part, which) x lane        */
 __device__ jx_mxtab g_mxtab[2][JX_MAXQ + 1];     /* [force][quality]                        */
@@ -222,12 +236,8 @@ __device__ __forceinline__ bool mx_simple_load(const MxCur &p, const MxG &g, uns
  * The rare other chunks (a row's last 32 blocks, frame / stripe / launch ends) take the general
  * per-step path.
  */
-#ifndef JX_MX_CHUNK
-#define JX_MX_CHUNK 4
-#endif
-constexpr unsigned kChunk = JX_MX_CHUNK;
-static_assert(kChunk == 4 && (kDist == 2 || kDist == 3),
-              "the ring holds one chunk: step k of a chunk in slot k, at most 3 steps ahead");
+static_assert(kSteps == 3 && kDist == 2, "the ring holds one chunk: step k of a chunk in slot k");
+constexpr unsigned kCB = 8 * kSteps;    /* blocks per chunk */
 struct MxChunk {
     unsigned b0;                        /* first block (launch-global); >= total: none        */
     unsigned f, bi, r, c;               /* frame, block in frame, block-row, column of b0      */
@@ -432,7 +442,7 @@ __device__ __forceinline__ void mx_exact_inline(MxLds &L, const uint8_t *slot, u
         const unsigned jb = mx_col_block(k, sl);
         const int val = mx_exact_coef(mx_lds((void *)slot) + 24u * jb, 192u, ch, u, v, x, T);
         if (live && x == 7)
-            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + mx_sb(ch) + kBS * jb +
+            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + kBS * mx_pos(ch, jb) +
                                                            2u * (unsigned)kMxScan[v][u]) = (int16_t)val;
         mx_wave_sync();
     }
@@ -494,9 +504,9 @@ __device__ __forceinline__ void mx_defer(MxLds &L, const uint8_t *sp, uint32_t b
     }
     const int ntask = (int)__builtin_amdgcn_readlane(incl, 63);
     const int nblk = __popc(blk);
-    if (nq + ntask > kSide || ns + nblk > kSide) {
+    if (nq + ntask > kSide || ns + nblk > kSidePix) {
         if (nq) mx_flush(L, nq, ns, g, T);
-        if (ntask > kSide) {
+        if (ntask > kSide || nblk > kSidePix) {
             mx_exact_inline(L, sp, bits, T);
             return;
         }
@@ -535,28 +545,7 @@ __device__ __forceinline__ void mx_defer(MxLds &L, const uint8_t *sp, uint32_t b
     ns += nblk;
 }
 
-/* Column pass of one column (8 rows as 4 register pairs), quantiser, stage writes, band max */
-__device__ __forceinline__ void mx_column(const mx_f2 (&R)[4], const mx_f2 (&W)[4], const mx_f2 (&Lq)[4],
-                                          uint8_t *st, const uint32_t (&zo)[8], float &emax,
-                                          mx_f2 (&F)[4])
-{
-    jx_fdct8_pk<MxPair>(R, F);
-    const mx_f2 M2 = {kMagic, kMagic};
-#pragma unroll
-    for (int p = 0; p < 4; p++) {
-        const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
-        *(uint16_t *)(st + zo[jx_pk_k(p, 0)]) = (uint16_t)__float_as_uint(tm.x);
-        *(uint16_t *)(st + zo[jx_pk_k(p, 1)]) = (uint16_t)__float_as_uint(tm.y);
-#ifndef JX_MX_DBG_NOBAND               /* timing experiments only: no band test (NOT exact) */
-        const mx_f2 rr = tm - M2;
-        const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
-        const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
-        emax = __builtin_fmaxf(__builtin_fmaxf(emax, e.x), e.y);          /* v_max3_f32 */
-#endif
-    }
-}
-
-/* rare: the flagged v's of one column (the same arithmetic as mx_column) */
+/* rare: the flagged v's of one column (the same arithmetic as mx_column_t) */
 __device__ __forceinline__ uint32_t mx_flags(const mx_f2 (&F)[4], const mx_f2 (&W)[4], const mx_f2 (&Lq)[4])
 {
     const mx_f2 M2 = {kMagic, kMagic};
@@ -583,9 +572,48 @@ __device__ __forceinline__ void mx_combine(mx_f4 hl, mx_f4 ll, mx_f4 hh, mx_f4 l
     R[3] = __builtin_elementwise_fma(mx_f2{lh.z, lh.w}, s, mx_f2{hh.z, hh.w});
 }
 
+/* a column's scales and band limits from the workgroup table (W pairs then L pairs) */
+struct MxWL {
+    mx_f4 w01, w23, l01, l23;
+};
+/* t0 = 0 (k_mx: Y|Cb, k_mx422: Y) or 2 (k_mx: Cr, k_mx422: chroma) */
+__device__ __forceinline__ MxWL mx_wl(const MxTab &tb, unsigned t0, unsigned j)
+{
+    return MxWL{tb.wl[t0][0][j], tb.wl[t0][1][j], tb.wl[t0 + 1][0][j], tb.wl[t0 + 1][1][j]};
+}
+
+/* Column pass of one column (R pairs), quantiser, stage writes at za[v] + OFF, band flags (rare
+ * path) into fl */
+template <unsigned OFF>
+__device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxWL &t, const uint32_t (&za)[8],
+                                             uint32_t &fl, int kc)
+{
+    mx_f2 R[4], F[4];
+    mx_combine(acc[0], acc[1], acc[2], acc[3], R);
+    jx_fdct8_pk<MxPair>(R, F);
+    const mx_f4 w01 = t.w01, w23 = t.w23, l01 = t.l01, l23 = t.l23;
+    const mx_f2 W[4] = {mx_f2{w01.x, w01.y}, mx_f2{w01.z, w01.w}, mx_f2{w23.x, w23.y}, mx_f2{w23.z, w23.w}};
+    const mx_f2 Lq[4] = {mx_f2{l01.x, l01.y}, mx_f2{l01.z, l01.w}, mx_f2{l23.x, l23.y}, mx_f2{l23.z, l23.w}};
+    const mx_f2 M2 = {kMagic, kMagic};
+    typedef __attribute__((address_space(3))) uint16_t l16;
+    float em = -1.0f;
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
+        *(l16 *)(uintptr_t)(za[jx_pk_k(p, 0)] + OFF) = (uint16_t)__float_as_uint(tm.x);
+        *(l16 *)(uintptr_t)(za[jx_pk_k(p, 1)] + OFF) = (uint16_t)__float_as_uint(tm.y);
+        const mx_f2 rr = tm - M2;
+        const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
+        const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
+        em = __builtin_fmaxf(__builtin_fmaxf(em, e.x), e.y);
+    }
+    if (__builtin_expect(__ballot(em >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * kc);
+}
+
 __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
 {
     __shared__ __attribute__((aligned(16))) MxLds s_lds[4];
+    __shared__ __attribute__((aligned(16))) MxTab s_tab;
     MxG g;
     g.rgb = a.g.rgb;
     g.out = a.g.out;
@@ -605,9 +633,27 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
 
     const unsigned lane = threadIdx.x & 63u;
     MxLds &L = s_lds[threadIdx.x >> 6];
+    const jx_mxtab &T = g_mxtab[g.force ? 1 : 0][g.quality];
+    /* the workgroup's scale / limit table: wave 0, lane (t = lane >> 4, profile j = lane & 15);
+     * plan columns n = 8c + u: Y|Cb j, Cr 16 + j % 8 */
+    if (threadIdx.x < 64) {
+        const unsigned t = lane >> 4, jp = lane & 15u;
+        const unsigned n = t < 2 ? jp : 16u + (jp & 7u);
+        float x[8];
+#pragma unroll
+        for (int p = 0; p < 4; p++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int v = jx_pk_k(p, h);
+                x[2 * p + h] = (t & 1u) ? T.lsq[n][v] : T.w[n][v];
+            }
+        s_tab.wl[t][0][jp] = mx_f4{x[0], x[1], x[2], x[3]};
+        s_tab.wl[t][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
+    }
+    __syncthreads();
     const unsigned nw = gridDim.x * 4u;
     const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    if (32u * wv >= g.total) return;
+    if (kCB * wv >= g.total) return;
 
     /* A operand of this lane: row m = lane & 15 (block m >> 2 of the set, pixel row m & 3 of the
      * half), k-group q = lane >> 4 (bytes 8q..8q+7; q = 3: the bias) */
@@ -619,28 +665,21 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     /* DMA pieces p = lane, 64 + lane: pixel row p / 12, bytes 16 (p % 12) of the step's row */
     const uint32_t off0 = (uint32_t)((lane / 12u) * (unsigned)g.pitch + 16u * (lane % 12u));
     const uint32_t off1 = (uint32_t)(((64u + lane) / 12u) * (unsigned)g.pitch + 16u * ((64u + lane) % 12u));
-    /* stores: lane's 16 bytes of channel c's 8 blocks, as byte offsets from the step's block 0 */
+    /* stores: lane's 16 bytes of channel c's 8 blocks, as byte offsets from the step's block 0;
+     * the stage reads at ro (Y), ro + 12 slots (Cb), rr (Cr: slots 8..11, 20..23) */
     const uint32_t so0 = lane * 16u, so1 = so0 + g.nb * 128u, so2 = so1 + g.nb * 128u;
     const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
+    const uint32_t rr = ro + ((lane >> 3) < 4 ? 8u : 16u) * kBS;
 
-    /* C layout: lane (gq = lane >> 4, j = lane & 15) holds column j of rows 4 gq..4 gq + 3 */
+    /* C layout: lane (gq = lane >> 4, j = lane & 15) holds column j of rows 4 gq..4 gq + 3;
+     * its three columns' coefficients go to za[v] + 0, 4 and 8 slots */
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
-    const jx_mxtab &T = g_mxtab[g.force ? 1 : 0][g.quality];
-    const unsigned ny = j, nc = 16u + u;                /* plan columns n = 8c + u */
-    mx_f2 Wy[4], Ly[4], Wc[4], Lc[4];
+    uint32_t za[8];
+    {
+        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * mx_pos(j >> 3, gq);
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
-        const int v0 = jx_pk_k(p, 0), v1 = jx_pk_k(p, 1);
-        Wy[p] = mx_f2{T.w[ny][v0], T.w[ny][v1]};
-        Ly[p] = mx_f2{T.lsq[ny][v0], T.lsq[ny][v1]};
-        Wc[p] = mx_f2{T.w[nc][v0], T.w[nc][v1]};
-        Lc[p] = mx_f2{T.lsq[nc][v0], T.lsq[nc][v1]};
+        for (int v = 0; v < 8; v++) za[v] = base + 2u * (unsigned)kMxScan[v][u];
     }
-    uint32_t zo[8];
-#pragma unroll
-    for (int v = 0; v < 8; v++) zo[v] = 2u * (unsigned)kMxScan[v][u];
-    uint8_t *const st1 = L.stage + mx_sb(j >> 3) + kBS * gq;           /* set 0: block gq       */
-    uint8_t *const st3 = L.stage + mx_sb(2) + kBS * (j < 8 ? gq : 4u + gq);
     mx_u4 B[kParts][3];
 #pragma unroll
     for (int p = 0; p < kParts; p++)
@@ -648,15 +687,14 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         for (int w = 0; w < 3; w++) B[p][w] = g_mxB[3 * p + w][lane];
     __builtin_amdgcn_s_waitcnt(0xF70);              /* see k_mx422 */
 
-    /* chunks: cc (computed now), nc2 (the next one; its first two steps are issued during cc's
-     * last two) */
+    /* chunks: cc (computed now), nx (the next one; its first steps are issued during cc's last) */
     MxJump J;
-    J.jb = 32u * nw;
+    J.jb = kCB * nw;
     J.jr = J.jb / g.bpr;
     J.jc = J.jb - J.jr * g.bpr;
     J.rows = g.nb / g.bpr;
     MxChunk cc;
-    mx_chunk_at<32>(cc, g, 32u * wv);
+    mx_chunk_at<kCB>(cc, g, kCB * wv);
     MxChunk nx = cc;
 
     /* DMA of step k of chunk C into ring slot k (the slot the step computes from) */
@@ -675,8 +713,8 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             mx_issue(g, P, b, mx_simple_load(P, g, b), off0, off1, slot);
         }
     };
-    /* prologue: steps 0 and 1, each followed by three padding operations in place of the stores
-     * of the (absent) steps before the first */
+    /* prologue: the first kDist steps, each followed by three padding operations in place of the
+     * stores of the (absent) steps before the first */
     for (unsigned d = 0; d < kDist; d++) {
         issue(cc, d);
         mx_pad(g, L, 3);
@@ -686,18 +724,18 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     for (;;) {
         const unsigned b0 = cc.b0 + 8u * k;
         /* VMEM operations younger than this step's DMA, in issue order: the three stores of each
-         * of steps s-2, s-1 and the two DMA pieces of step s+1 (padding operations stand in for
-         * the ones that do not exist; a general step's loads and the exact flush wait for
-         * themselves, which only makes this count conservative) */
+         * of the kDist steps before it and the two DMA pieces of each of the kDist - 1 after it
+         * (padding operations stand in for the ones that do not exist; a general step's loads
+         * and the exact flush wait for themselves, which only makes this count conservative) */
         __builtin_amdgcn_s_waitcnt(kWaitImm);
         mx_wave_sync();
         const uint8_t *const sp = L.ring[k];
         /* the step kDist ahead: step k + kDist of this chunk, or of the next */
-        if (k + kDist < kChunk) {
+        if (k + kDist < kSteps) {
             issue(cc, k + kDist);
         } else {
-            if (k + kDist == kChunk) mx_chunk_next<32>(nx, g, J);
-            issue(nx, k + kDist - kChunk);
+            if (k + kDist == kSteps) mx_chunk_next<kCB>(nx, g, J);
+            issue(nx, k + kDist - kSteps);
         }
         /* A operands: set 0/1 x half lo/hi */
         const mx_u2 d00 = *(const mx_u2 *)(sp + aoff);
@@ -708,8 +746,6 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         const mx_h8 A10 = mx_aop(d10, s0, s1, s2), A11 = mx_aop(d11, s0, s1, s2);
         const mx_f4 z = {};
         uint32_t fl = 0;                               /* bit 8 col + v: flagged (rare) */
-        float em = -1.0f;
-        mx_f2 R[4], F[4];
         /* MFMAs one column ahead of the VALU work: MFMA(c0), MFMA(c1), VALU(c0), MFMA(c2),
          * VALU(c1), VALU(c2) -- an accumulator is read only after another column's products or
          * VALU work (no exposed MFMA latency, and far more than the MFMA -> VALU wait states the
@@ -730,20 +766,11 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
                 o[3] = mx_mma(Ahi, B[kParts - 1][0], o[3]);
             }
         };
-        const auto column = [&](int kc) {
-            mx_combine(acc[kc][0], acc[kc][1], acc[kc][2], acc[kc][3], R);
-            float e = -1.0f;
-            const mx_f2(&W)[4] = kc < 2 ? Wy : Wc;
-            const mx_f2(&Lq)[4] = kc < 2 ? Ly : Lc;
-            mx_column(R, W, Lq, kc == 0 ? st1 : (kc == 1 ? st1 + 4u * kBS : st3), zo, e, F);
-            if (__builtin_expect(__ballot(e >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * kc);
-            em = __builtin_fmaxf(em, e);
-        };
         mma_set(acc[0], A00, A01);
         __builtin_amdgcn_sched_barrier(0);
         mma_set(acc[1], A10, A11);
         __builtin_amdgcn_sched_barrier(0);
-        column(0);
+        mx_column_t<0>(acc[0], mx_wl(s_tab, 0, j), za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
         acc[2][0] = mx_mma(A00, B[0][1], z);
         acc[2][2] = mx_mma(A01, B[0][1], z);
@@ -767,21 +794,24 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             acc[2][3] = mx_mma(A11, B[kParts - 1][2], acc[2][3]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        column(1);
+        mx_column_t<4 * kBS>(acc[1], mx_wl(s_tab, 0, j), za, fl, 1);
         __builtin_amdgcn_sched_barrier(0);
-        column(2);
-        (void)em;
+        mx_column_t<8 * kBS>(acc[2], mx_wl(s_tab, 2, j), za, fl, 2);
         mx_wave_sync();
-        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx_defer(L, sp, fl, b0, nq, ns, g, T);
+        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
+            mx_defer(L, sp, fl, b0, nq, ns, g, T);
+            __builtin_amdgcn_s_waitcnt(0xF70);         /* see mx422_defer_step */
+        }
         /* stores: channel c's 8 blocks x 128 B; always three store instructions (the vmcnt
          * accounting above counts on it) */
         if (cc.simple) {
             const uint8_t *const ob = (const uint8_t *)(cc.dst + 512u * k);
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                const mx_u4 val = *(const mx_u4 *)(L.stage + mx_sb((unsigned)c) + ro);
-                __builtin_nontemporal_store(val, (mx_u4 *)(ob + (c == 0 ? so0 : (c == 1 ? so1 : so2))));
-            }
+            const mx_u4 v0 = *(const mx_u4 *)(L.stage + ro);
+            const mx_u4 v1 = *(const mx_u4 *)(L.stage + 12u * kBS + ro);
+            const mx_u4 v2 = *(const mx_u4 *)(L.stage + rr);
+            __builtin_nontemporal_store(v0, (mx_u4 *)(ob + so0));
+            __builtin_nontemporal_store(v1, (mx_u4 *)(ob + so1));
+            __builtin_nontemporal_store(v2, (mx_u4 *)(ob + so2));
         } else {
             /* lanes past the launch's end (the clamped copies of the last block) store nothing;
              * block b0 is always in range, so each store instruction still issues (the vmcnt
@@ -789,10 +819,9 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             const unsigned l = mx_lane();
             const unsigned bl = b0 + (l >> 3), b = bl < g.total ? bl : g.total - 1u;
             const unsigned f = b / g.nb, bi = b - f * g.nb;
-            const uint32_t rl = (l >> 3) * kBS + (l & 7u) * 16u;
 #pragma unroll
             for (int c = 0; c < 3; c++) {
-                const mx_u4 val = *(const mx_u4 *)(L.stage + mx_sb((unsigned)c) + rl);
+                const mx_u4 val = *(const mx_u4 *)(L.stage + kBS * mx_pos((unsigned)c, l >> 3) + (l & 7u) * 16u);
                 if (bl < g.total)
                     __builtin_nontemporal_store(
                         val, (mx_u4 *)(g.out + (long long)f * g.ofstride +
@@ -800,7 +829,7 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             }
         }
         mx_wave_sync();
-        if (++k == kChunk) {
+        if (++k == kSteps) {
             k = 0;
             cc = nx;
             if (cc.b0 >= g.total) break;
@@ -850,7 +879,7 @@ constexpr unsigned kSt422C = 8 * kBS;         /* chroma (c, cb) at kSt422C + kBS
 #define JX_MX422_WPE 4
 #endif
 
-struct Mx422Lds {
+struct alignas(16) Mx422Lds {
     uint8_t ring[kSteps422][kSlot];
     uint8_t stage[16 * kBS];
     uint8_t qtrue[4][192];              /* general step: true rows [y][24] of row-last block 2cb+1 */
@@ -861,13 +890,7 @@ struct Mx422Lds {
     uint16_t task[8];
     uint32_t dummy[64];
 };
-/* per-lane scales / band limits, shared by the workgroup: table t (Wy, Ly, Wc, Lc), half h (pairs
- * 2h, 2h + 1 in jx_pk_k order), profile j = lane & 15 -- a column's read of one (t, h) by the
- * wave touches 16 consecutive 16-byte entries, every bank once */
-struct Mx422Tab {
-    mx_f4 wl[4][2][16];
-};
-static_assert(sizeof(Mx422Lds) * 4 + sizeof(Mx422Tab) <= 40 * 1024, "4 workgroups of 4 waves per CU");
+static_assert(sizeof(Mx422Lds) * 4 + sizeof(MxTab) <= 40 * 1024, "4 workgroups of 4 waves per CU");
 
 __device__ mx_u4 g_mx422B[JX_MX_PARTS * 4][64];  /* [part * 4 + which][lane] */
 __device__ jx_mxtab g_mx422tab[2][JX_MAXQ + 1];  /* n = 8 c + u: c = 0 Y, 1 Cb, 2 Cr */
@@ -1112,48 +1135,10 @@ __device__ __forceinline__ uint32_t mx422_true_rows(Mx422Lds &L, const MxG &g, u
     return qm;
 }
 
-/* a column's scales and band limits from the workgroup table (W pairs then L pairs) */
-struct Mx422WL {
-    mx_f4 w01, w23, l01, l23;
-};
-/* t0 = 0 (Y) or 2 (chroma) */
-__device__ __forceinline__ Mx422WL mx422_wl(const Mx422Tab &tb, unsigned t0, unsigned j)
-{
-    return Mx422WL{tb.wl[t0][0][j], tb.wl[t0][1][j], tb.wl[t0 + 1][0][j], tb.wl[t0 + 1][1][j]};
-}
-
-/* Column pass of one column (R pairs), quantiser, stage writes at za[v] + OFF, band flags (rare
- * path) into fl */
-template <unsigned OFF>
-__device__ __forceinline__ void mx422_column(const mx_f4 (&acc)[4], const Mx422WL &t, const uint32_t (&za)[8],
-                                             uint32_t &fl, int kc)
-{
-    mx_f2 R[4], F[4];
-    mx_combine(acc[0], acc[1], acc[2], acc[3], R);
-    jx_fdct8_pk<MxPair>(R, F);
-    const mx_f4 w01 = t.w01, w23 = t.w23, l01 = t.l01, l23 = t.l23;
-    const mx_f2 W[4] = {mx_f2{w01.x, w01.y}, mx_f2{w01.z, w01.w}, mx_f2{w23.x, w23.y}, mx_f2{w23.z, w23.w}};
-    const mx_f2 Lq[4] = {mx_f2{l01.x, l01.y}, mx_f2{l01.z, l01.w}, mx_f2{l23.x, l23.y}, mx_f2{l23.z, l23.w}};
-    const mx_f2 M2 = {kMagic, kMagic};
-    typedef __attribute__((address_space(3))) uint16_t l16;
-    float em = -1.0f;
-#pragma unroll
-    for (int p = 0; p < 4; p++) {
-        const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
-        *(l16 *)(uintptr_t)(za[jx_pk_k(p, 0)] + OFF) = (uint16_t)__float_as_uint(tm.x);
-        *(l16 *)(uintptr_t)(za[jx_pk_k(p, 1)] + OFF) = (uint16_t)__float_as_uint(tm.y);
-        const mx_f2 rr = tm - M2;
-        const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
-        const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
-        em = __builtin_fmaxf(__builtin_fmaxf(em, e.x), e.y);
-    }
-    if (__builtin_expect(__ballot(em >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * kc);
-}
-
 __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args a)
 {
     __shared__ __attribute__((aligned(16))) Mx422Lds s_lds[4];
-    __shared__ __attribute__((aligned(16))) Mx422Tab s_tab;
+    __shared__ __attribute__((aligned(16))) MxTab s_tab;
     MxG g;
     g.rgb = a.g.rgb;
     g.out = a.g.out;
@@ -1329,9 +1314,9 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
         mma2(acc[1], mx_aop(c00, kSelLo, kSelHi, kSelLo), mx_aop(c01, kSelLo, kSelHi, kSelLo),
              mx_aop(c10, t0, t1, t2), mx_aop(c11, t0, t1, t2), 2);
         __builtin_amdgcn_sched_barrier(0);
-        mx422_column<0>(acc[0], mx422_wl(s_tab, 0, j), za, fl, 0);
+        mx_column_t<0>(acc[0], mx_wl(s_tab, 0, j), za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
-        mx422_column<kSt422C>(acc[1], mx422_wl(s_tab, 2, j), za, fl, 1);
+        mx_column_t<kSt422C>(acc[1], mx_wl(s_tab, 2, j), za, fl, 1);
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx422_defer_step(L, sp, qmask, fl, b0, nq, ns, g, T);
         /* always two store instructions per step (the vmcnt accounting counts on it) */
