@@ -18,10 +18,10 @@
  *   colour conversion in its operand order, -128, the 64-term sum x-outer / y-inner with
  *   (X*c_u[x])*c_v[y] and the glibc cosine doubles, ((0.25*a_u)*a_v)*s, true double division
  *   by the transposed table entry, round() half away from zero.
- * k_sub422: true 4:2:2 (extension, JPGX_FLAG_SUBSAMPLE) in one pass: k_xform's Y, then the
+ * k_sub420: true 4:2:0 (extension, JPGX_FLAG_SUBSAMPLE) in one pass: k_xform's Y, then the
  *   chroma of the same pixels from the registers (lanes pair up over DPP).
- * k_chroma: true 4:2:0 chroma (and 4:2:2 with JPGX_SUB422=two-pass); k_xform does Y.
- * k_mx (csrc/jpgx_mx.hip): the matrix-core 4:4:4 kernel.
+ * k_chroma<1|2>: true 4:2:2 / 4:2:0 chroma of the test-only cross-check library; k_xform does Y.
+ * k_mx / k_mx422 (csrc/jpgx_mx.hip): the matrix-core 4:4:4 and true 4:2:2 kernels.
  *
  * Compiled with FP contraction off; the fast path uses explicit fmaf.  Variants of k_xform
  * measured slower are kept out of this file: tools/probes/k_xform_variants.patch.
@@ -692,219 +692,10 @@ __global__ __launch_bounds__(JX_WG, 3) void k_chroma(const jx_xform_args a)
     }
 }
 
-/* ---- k_sub422: true 4:2:2 in one pass over the pixels (extension) ------------------------
- * Tile t = Y blocks 64t..64t+63 = MCUs 32t..32t+31: W is a multiple of 16, so the two Y
- * blocks of an MCU are raster neighbours 2m, 2m+1 (never split by a block row) and the chroma
- * block of MCU m is block m of the (W/2) x H plane.  The Y pass is k_xform's channel 0.  The
- * chroma pass reuses the pixel rows still in the lanes' registers: lane 2m (left half of MCU m)
- * forms the Cb and Cr pair averages of its 8 pixels in every row, keeps Cb and hands Cr to lane
- * 2m+1, which keeps Cr and hands Cb back (one DPP swap per sample); lane 2m then transforms Cb
- * block m and lane 2m+1 Cr block m with exactly k_chroma<1>'s fp32 operations, so the same guard
- * band (g_limsub[0]) and exact recomputation (fix_chroma) apply.  RGB is read from HBM once;
- * the output is 7 B/px (3 in, 2 Y + 2 chroma out). */
-
 /* swap with the neighbouring lane (quad_perm [1,0,3,2]) */
 __device__ __forceinline__ float swap_pair(float v)
 {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
-}
-
-/* The chroma rows of this lane's block (Cb for even lanes, Cr for odd) from raw, the pixel rows
- * of the lane's Y block: for the last block of a block row raw holds the x0 = -8 quirk's rows
- * (one pixel row higher), which the caller has already replaced by the true rows. */
-__device__ __forceinline__ void sub422_rows(uint32_t (&raw)[8][6], bool odd, const float (&kk)[3],
-                                            const float (&ks)[3], float (&T)[8][8])
-{
-#pragma unroll
-    for (int y = 0; y < 8; y++)
-#pragma unroll
-        for (int k = 0; k < 6; k++) asm volatile("" : "+v"(raw[y][k]));
-#pragma unroll
-    for (int y = 0; y < 8; y++) {
-        float keep[4], got[4];
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-            const int i0 = 6 * x, i1 = 6 * x + 3;            /* bytes of pixels 2x, 2x+1 */
-            /* byte sums of the pair (exact), converted once: k_chroma<1>'s sequence */
-            const float R = (float)byte_of(raw[y], i0) + (float)byte_of(raw[y], i1);
-            const float G = (float)byte_of(raw[y], i0 + 1) + (float)byte_of(raw[y], i1 + 1);
-            const float B = (float)byte_of(raw[y], i0 + 2) + (float)byte_of(raw[y], i1 + 2);
-            keep[x] = __builtin_fmaf(R, kk[0], __builtin_fmaf(G, kk[1], __builtin_fmaf(B, kk[2], -0.0f))) * 0.5f;
-            got[x] = swap_pair(
-                __builtin_fmaf(R, ks[0], __builtin_fmaf(G, ks[1], __builtin_fmaf(B, ks[2], -0.0f))) * 0.5f);
-        }
-        float smp[8];
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-            smp[x] = odd ? got[x] : keep[x];
-            smp[4 + x] = odd ? keep[x] : got[x];
-        }
-        jx_fdct8<FOps>(smp, T[y]);
-    }
-}
-
-/* Column pass of the tile's 64 chroma blocks: as xform_cols, with the channel per lane (the
- * scale is the chroma table for both; the guard band the one both channels satisfy, wave-
- * uniform: 5-6% faster than selecting Cb's or Cr's per lane), staged at slot
- * (lane & 1) * 32 + lane / 2 so that Cb blocks 32t.. and Cr blocks 32t.. leave as two 4 KiB
- * runs; flagged blocks are queued per channel for fix_chroma. */
-__device__ __forceinline__ void sub422_cols(float (&T)[8][8], const jx_xform_args &ac, const jx_geom &g, WaveLds &W,
-                                            Queue &Q, bool active, unsigned bc, unsigned t,
-                                            unsigned lane, unsigned total_c)
-{
-    const jx_qtab &tab = g_qtab[ac.quality];
-    const jx_limtab &band = g_limsub[0][ac.force_exact ? 1 : 0][ac.quality];
-    const unsigned slot = (lane & 1u) * 32u + (lane >> 1);
-    uint64_t seen = 0;
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-        float wc[8], lc[8];
-#pragma unroll
-        for (int v = 0; v < 8; v++) {
-            wc[v] = tab.w[1][u][v];
-            lc[v] = band.lim[0][u][v];       /* the band both chroma channels satisfy */
-        }
-        float col[8], F[8];
-#pragma unroll
-        for (int y = 0; y < 8; y++) col[y] = T[y][u];
-        jx_fdct8<FOps>(col, F);
-#pragma unroll
-        for (int v = 0; v < 8; v++) {
-            float tm, d;
-            quant_coef(F[v], wc[v], tm, d);
-            ((uint16_t *)W.stage)[slot * 66 + zz_of(v, u)] = (uint16_t)__float_as_uint(tm);
-            uint64_t m;
-            asm("v_cmp_ge_f32_e64 %[m], |%[d]|, %[l]\n\t"
-                "s_or_b64 %[seen], %[seen], %[m]"
-                : [m] "=&s"(m), [seen] "+s"(seen)
-                : [d] "v"(d), [l] "s"(lc[v])
-                : "scc");
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    const unsigned nbc = (unsigned)g.nb, c0 = t * 32u;
-    const unsigned f0 = c0 / nbc, fl = std::min(c0 + 31u, total_c - 1u) / nbc;
-    if (f0 == fl && c0 + 31u < total_c) {
-        int16_t *base = g.out + (long long)f0 * g.out_fstride + (long long)(c0 - f0 * nbc) * 64;
-        u32x4 *cb = (u32x4 *)(base + (long long)nbc * 64), *cr = (u32x4 *)(base + 2ll * nbc * 64);
-        unsigned o0 = (lane >> 3) * 33 + (lane & 7) * 4;
-        asm volatile("" : "+v"(o0));
-        u32x4 unit[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const unsigned o = o0 + 264u * (unsigned)j;
-            unit[j] = u32x4{W.stage[o], W.stage[o + 1], W.stage[o + 2], W.stage[o + 3]};
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 4; j++) jx_store(cb + (unsigned)j * 64u + lane, unit[j]);
-#pragma unroll
-        for (int j = 4; j < 8; j++) jx_store(cr + (unsigned)(j - 4) * 64u + lane, unit[j]);
-    } else {                                   /* tile crosses a frame end or the last tile */
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const unsigned e = (unsigned)j * 64u + lane, sl = e >> 3, bb = c0 + (sl & 31u);
-            if (bb < total_c)                  /* slots past the end hold no block */
-                jx_store((u32x4 *)coef_ptr(g, bb, 1 + (int)(sl >> 5), (int)(e & 7) * 8),
-                         stage_unit(W, e));
-        }
-    }
-    if (seen != 0) {
-        const uint64_t M = seen & __ballot(active);
-        const uint64_t Mb = M & 0x5555555555555555ull, Mr = M & 0xAAAAAAAAAAAAAAAAull;
-        if ((Mb >> lane) & 1u) W.item[1][Q.n[1] + lane_rank(Mb)] = bc;
-        if ((Mr >> lane) & 1u) W.item[2][Q.n[2] + lane_rank(Mr)] = bc;
-        Q.n[1] += __popcll(Mb);
-        Q.n[2] += __popcll(Mr);
-    }
-}
-
-#ifndef JX_SUB_WPE
-#define JX_SUB_WPE 3
-#endif
-
-__global__ __launch_bounds__(JX_WG, JX_SUB_WPE) void k_sub422(const jx_xform_args a, const jx_geom gc)
-{
-    __shared__ WaveLds s_wave[JX_WG / 64];
-    const jx_geom &g = a.g;
-    const unsigned nb = (unsigned)g.nb, bpr = (unsigned)g.bpr;
-    const unsigned total = nb * (unsigned)g.nframes, total_c = total / 2u;
-    const unsigned ntiles = (total + 63u) / 64u;
-    const unsigned lane = threadIdx.x & 63u;
-    const unsigned nwaves = gridDim.x * (JX_WG / 64);
-    unsigned t = __builtin_amdgcn_readfirstlane(blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6));
-    if (t >= ntiles) return;
-    WaveLds &W = s_wave[threadIdx.x >> 6];
-    Queue Q{{0, 0, 0}, {0u, 0u, 0u}};
-    uint32_t raw[8][6];
-    for (; t < ntiles; t += nwaves) {
-        /* every per-lane value is derived from an opaque lane id inside the loop: hoisted out of
-         * it, they would be loop invariants that the exact-pass code's registers push to scratch */
-        unsigned ln = lane;
-        asm volatile("" : "+v"(ln));
-        /* colour constants per lane: the channel it keeps (Cb even, Cr odd), the one it sends */
-        const bool odd = ln & 1u;
-        const float kk[3] = {odd ? JX_K(0.5).f : JX_K(-0.168736).f,
-                             odd ? JX_K(-0.418688).f : JX_K(0.331264).f,
-                             odd ? JX_K(-0.081312).f : JX_K(-0.5).f};
-        const float ks[3] = {odd ? JX_K(-0.168736).f : JX_K(0.5).f,
-                             odd ? JX_K(0.331264).f : JX_K(-0.418688).f,
-                             odd ? JX_K(-0.5).f : JX_K(-0.081312).f};
-        const unsigned b0 = t * 64u + ln;
-        const bool active = b0 < total;
-        const unsigned b = active ? b0 : total - 1;
-        const unsigned f = b / nb, bi = b - f * nb, r = bi / bpr, c = bi - r * bpr;
-        load_block(g, f, bi, raw);
-        float T[8][8];
-        xform_rows(0, raw, T);
-        xform_cols(0, T, a, W, Q, active, b, t, ln);
-        __builtin_amdgcn_sched_barrier(0);
-        /* last block of a block row: raw holds rows 8r-1..8r+6 (x0 = -8 quirk, Y only); the
-         * chroma needs rows 8r..8r+7 */
-        const bool last = c == bpr - 1u;
-        if (__ballot(last)) {
-            if (last) {
-                const uint8_t *p = g.rgb + (long long)f * g.in_fstride + 8ll * r * g.in_pitch +
-                                   24ll * c;
-#pragma unroll
-                for (int y = 0; y < 8; y++) {
-                    const uint8_t *q = (const uint8_t *)__builtin_assume_aligned(
-                        p + (long long)y * g.in_pitch, 8);
-                    u32x4 q4;
-                    u32x2 q2;
-                    __builtin_memcpy(&q4, q, 16);
-                    __builtin_memcpy(&q2, q + 16, 8);
-                    raw[y][0] = q4.x; raw[y][1] = q4.y; raw[y][2] = q4.z; raw[y][3] = q4.w;
-                    raw[y][4] = q2.x; raw[y][5] = q2.y;
-                }
-            }
-        }
-        sub422_rows(raw, ln & 1u, kk, ks, T);
-        sub422_cols(T, a, gc, W, Q, active, b >> 1, t, ln, total_c);
-        __builtin_amdgcn_sched_barrier(0);
-        while (Q.n[0] > kItems - 64) {
-            int n[3] = {Q.n[0], 0, 0};
-            fix_queued(W, n, a, lane);
-            Q.n[0] = n[0];
-        }
-        if (Q.n[1] > kItems - 32 || Q.n[2] > kItems - 32) {
-            jx_xform_args ac = a;
-            ac.g = gc;
-            ac.sub = 1;
-            fix_chroma(W, Q, 1, ac, lane);
-            fix_chroma(W, Q, 2, ac, lane);
-        }
-    }
-    while (Q.n[0] > 0) {
-        int n[3] = {Q.n[0], 0, 0};
-        fix_queued(W, n, a, lane);
-        Q.n[0] = n[0];
-    }
-    jx_xform_args ac = a;
-    ac.g = gc;
-    ac.sub = 1;
-    fix_chroma(W, Q, 1, ac, lane);
-    fix_chroma(W, Q, 2, ac, lane);
 }
 
 /* ---- k_sub420: true 4:2:0 in one pass over the pixels (extension) ------------------------
@@ -1247,7 +1038,7 @@ int tables_for_current_device()
                     for (int u = 0; u < 8; u++)
                         for (int v = 0; v < 8; v++) {
                             /* slot 0 (luma is never averaged): the band both chroma channels
-                             * satisfy, for k_sub422's mixed Cb / Cr lanes; for 4:2:0 also both
+                             * satisfy, for a kernel's mixed Cb / Cr lanes; for 4:2:0 also both
                              * column halves u, u ^ 4 (k_sub420's top / bottom lanes) */
                             const int k = v * 8 + u, k2 = v * 8 + (u ^ 4);
                             const float j = std::min(lim[1][k], lim[2][k]);
@@ -1290,7 +1081,7 @@ int resident_waves()
 }
 
 /* Dispatch.  The product library (libjpgx.so) runs one kernel per mode: k_mx for 4:4:4,
- * k_sub422 / k_sub420 for true 4:2:2 / 4:2:0.  The test-only cross-check library
+ * k_mx422 / k_sub420 for true 4:2:2 / 4:2:0.  The test-only cross-check library
  * (libjpgx_alt.so, built from the same sources with -DJPGX_ALT_DISPATCH) runs the second
  * implementations instead: k_xform for 4:4:4 and k_xform (Y) + k_chroma<1|2> for true 4:2:x. */
 #ifndef JPGX_ALT_DISPATCH

@@ -23,6 +23,6 @@ while [ $# -ge 2 ]; do
       $flags --cuda-device-only -S "$PKG/csrc/jpgx_mx.hip" -o "$PKG/build/variants/$name.s"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -I"$ROOT/include" \
       $flags --cuda-device-only -S "$PKG/csrc/jpgx_kernels.hip" -o "$PKG/build/variants/${name}_k.s"
-  echo "$name (k_sub422): $(grep -A40 'name:.*k_sub422' "$PKG/build/variants/${name}_k.s" | grep -E '^\s+\.(vgpr_count|vgpr_spill_count|sgpr_spill_count):' | head -3 | tr -s ' ' | tr '\n' ' ')"
+
   echo "$name (k_mx): $(grep -E '^\s+\.(vgpr_count|vgpr_spill_count|sgpr_spill_count):' "$PKG/build/variants/$name.s" | head -3 | tr -s ' ' | tr '\n' ' ')"
 done
