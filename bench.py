@@ -233,7 +233,7 @@ def sub_kernel_name(sr):
     """The kernels a true-subsampling launch runs (jpgx_blocks_gpu's dispatch)."""
     if alt_selected():
         return f"k_xform(Y)+k_chroma<{sr}>"
-    return "k_mx422" if sr == 1 else "k_sub420"
+    return "k_mx422" if sr == 1 else "k_mx420"
 
 
 def launch_ranks(n):

@@ -18,10 +18,9 @@
  *   colour conversion in its operand order, -128, the 64-term sum x-outer / y-inner with
  *   (X*c_u[x])*c_v[y] and the glibc cosine doubles, ((0.25*a_u)*a_v)*s, true double division
  *   by the transposed table entry, round() half away from zero.
- * k_sub420: true 4:2:0 (extension, JPGX_FLAG_SUBSAMPLE) in one pass: k_xform's Y, then the
- *   chroma of the same pixels from the registers (lanes pair up over DPP).
  * k_chroma<1|2>: true 4:2:2 / 4:2:0 chroma of the test-only cross-check library; k_xform does Y.
- * k_mx / k_mx422 (csrc/jpgx_mx.hip): the matrix-core 4:4:4 and true 4:2:2 kernels.
+ * k_mx / k_mx422 / k_mx420 (csrc/jpgx_mx.hip): the product kernels (4:4:4, true 4:2:2 / 4:2:0)
+ *   with the colour conversion and row DCT on the matrix cores.
  *
  * Compiled with FP contraction off; the fast path uses explicit fmaf.  Variants of k_xform
  * measured slower are kept out of this file: tools/probes/k_xform_variants.patch.
@@ -692,269 +691,6 @@ __global__ __launch_bounds__(JX_WG, 3) void k_chroma(const jx_xform_args a)
     }
 }
 
-/* swap with the neighbouring lane (quad_perm [1,0,3,2]) */
-__device__ __forceinline__ float swap_pair(float v)
-{
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
-}
-
-/* ---- k_sub420: true 4:2:0 in one pass over the pixels (extension) ------------------------
- * Tile = 16 MCUs of one MCU row (MCU = 2 x 2 Y blocks): lane l holds Y block (2 my + h,
- * 2 mx0 + k), h = l >> 5 (top / bottom block row), k = l & 31; MCU m = k >> 1, side k & 1.
- * Y: k_xform's channel 0 on the lane's block, stored as two runs of 32 blocks.  Chroma, from the
- * same pixel rows in registers: each lane forms the quad sums of its 4 x 4 samples (pixel-row
- * pairs x pixel pairs) for Cb and Cr, keeps one channel (Cb on even lanes, Cr on odd) and trades
- * the other with its side neighbour (DPP), so it holds 4 sample rows x 8 of its channel's block;
- * after the 4 row DCTs the top and bottom lanes of the block trade half-rows (lane ^ 32), so the
- * top lane runs columns 0..3 and the bottom lane columns 4..7 of the column pass.  The fp32
- * operations are k_chroma<2>'s (quad byte sums converted once, x 0.25, the same jx_fdct8), so the
- * 4:2:0 guard band and fix_chroma's exact pass apply.  RGB is read from HBM once: 6 B/px. */
-
-/* Column pass of the lane's block, columns u0 + 0..NU-1 (u0 = 0 or 4 per lane: `hi`), into the
- * stage at block slot `slot`; returns the lane mask of coefficients inside the guard band.
- * The scales, band limits and zig-zag positions of the two column halves are both formed from
- * wave-uniform values and selected per lane. */
-template <int NU>
-__device__ __forceinline__ uint64_t cols_to_stage(int wch, float (&T)[8][NU], const jx_limtab &band,
-                                                  int lch, const jx_xform_args &a, WaveLds &W,
-                                                  unsigned slot, bool hi)
-{
-    const jx_qtab &tab = g_qtab[a.quality];
-    uint64_t seen = 0;
-#pragma unroll
-    for (int uu = 0; uu < NU; uu++) {
-        constexpr int kHi = NU == 8 ? 0 : 4;
-        float wc[8], lc[8];
-#pragma unroll
-        for (int v = 0; v < 8; v++) {
-            wc[v] = hi ? tab.w[wch][uu + kHi][v] : tab.w[wch][uu][v];
-            lc[v] = band.lim[lch][uu][v];    /* wave-uniform: for NU = 4 the joint band */
-        }
-        float col[8], F[8];
-#pragma unroll
-        for (int y = 0; y < 8; y++) col[y] = T[y][uu];
-        jx_fdct8<FOps>(col, F);
-#pragma unroll
-        for (int v = 0; v < 8; v++) {
-            float tm, d;
-            quant_coef(F[v], wc[v], tm, d);
-            const unsigned zz = hi ? (unsigned)zz_of(v, uu + kHi) : (unsigned)zz_of(v, uu);
-            ((uint16_t *)W.stage)[slot * 66 + zz] = (uint16_t)__float_as_uint(tm);
-            uint64_t mk;
-            asm("v_cmp_ge_f32_e64 %[m], |%[d]|, %[l]\n\t"
-                "s_or_b64 %[seen], %[seen], %[m]"
-                : [m] "=&s"(mk), [seen] "+s"(seen)
-                : [d] "v"(d), [l] "s"(lc[v])
-                : "scc");
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    return seen;
-}
-
-#ifndef JX_SUB420_WPE
-#define JX_SUB420_WPE 3
-#endif
-__global__ __launch_bounds__(JX_WG, JX_SUB420_WPE) void k_sub420(const jx_xform_args a, const jx_geom gc)
-{
-    __shared__ WaveLds s_wave[JX_WG / 64];
-    const jx_geom &g = a.g;
-    const unsigned nb = (unsigned)g.nb, bpr = (unsigned)g.bpr;
-    const unsigned mpr = bpr / 2u;                         /* MCUs per row                  */
-    const unsigned mrows = nb / bpr / 2u;                  /* MCU rows per frame stripe     */
-    const unsigned tpr = (mpr + 15u) / 16u;                /* tiles per MCU row             */
-    const unsigned tpf = tpr * mrows, ntiles = tpf * (unsigned)g.nframes;
-    const unsigned nbc = (unsigned)gc.nb;
-    const unsigned lane = threadIdx.x & 63u;
-    const unsigned nwaves = gridDim.x * (JX_WG / 64);
-    unsigned t = __builtin_amdgcn_readfirstlane(blockIdx.x * (JX_WG / 64) + (threadIdx.x >> 6));
-    if (t >= ntiles) return;
-    WaveLds &W = s_wave[threadIdx.x >> 6];
-    Queue Q{{0, 0, 0}, {0u, 0u, 0u}};
-    jx_xform_args ac = a;
-    ac.g = gc;
-    ac.sub = 2;
-    const jx_limtab &cband = g_limsub[1][a.force_exact ? 1 : 0][a.quality];
-    uint32_t raw[8][6];
-    /* the tile loop runs while the queues have room for a tile's items; the (rare) exact passes
-     * run outside it, one copy of their code for mid-run drains and the end */
-    for (;;) {
-    for (; t < ntiles;) {
-        /* every per-lane value is derived from an opaque lane id inside the loop: hoisted out of
-         * it, they would be loop invariants that the exact-pass code's registers push to scratch */
-        unsigned ln = lane;
-        asm volatile("" : "+v"(ln));
-        const unsigned h = ln >> 5, k = ln & 31u, m = k >> 1;
-        const bool odd = ln & 1u;
-        const float kk[3] = {odd ? JX_K(0.5).f : JX_K(-0.168736).f,
-                             odd ? JX_K(-0.418688).f : JX_K(0.331264).f,
-                             odd ? JX_K(-0.081312).f : JX_K(-0.5).f};
-        const float ks[3] = {odd ? JX_K(-0.168736).f : JX_K(0.5).f,
-                             odd ? JX_K(0.331264).f : JX_K(-0.418688).f,
-                             odd ? JX_K(-0.5).f : JX_K(-0.081312).f};
-        const unsigned f = t / tpf, tr = t - f * tpf, my = tr / tpr, mx0 = (tr - my * tpr) * 16u;
-        const bool full = mx0 + 16u <= mpr;                 /* wave-uniform                  */
-        const bool active = mx0 + m < mpr;
-        const unsigned c = active ? 2u * mx0 + k : bpr - 1u, r = 2u * my + h;
-        const unsigned bi = r * bpr + c, b = f * nb + bi;   /* launch-global Y block          */
-        load_block(g, f, bi, raw);
-        /* ---- Y ---- */
-        {
-            float T[8][8];
-            xform_rows(0, raw, T);
-            unsigned ysl = ln;                            /* opaque: no hoisted addresses  */
-            asm volatile("" : "+v"(ysl));
-            const uint64_t seen = cols_to_stage<8>(0, T, g_lim[a.force_exact ? 1 : 0][a.quality],
-                                                   0, a, W, ysl, false);
-            int16_t *yrow = g.out + (long long)f * g.out_fstride + (long long)(2u * my * bpr + 2u * mx0) * 64;
-            if (full) {
-                unsigned o0 = (ln >> 3) * 33 + (ln & 7) * 4;
-                asm volatile("" : "+v"(o0));
-                u32x4 unit[8];
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const unsigned o = o0 + 264u * (unsigned)j;
-                    unit[j] = u32x4{W.stage[o], W.stage[o + 1], W.stage[o + 2], W.stage[o + 3]};
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    jx_store((u32x4 *)(yrow + (j < 4 ? 0ll : (long long)bpr * 64)) + (unsigned)(j & 3) * 64u + ln,
-                             unit[j]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const unsigned e = (unsigned)j * 64u + ln, sl = e >> 3;
-                    if (mx0 + ((sl & 31u) >> 1) < mpr)
-                        jx_store((u32x4 *)(yrow + (long long)(sl >> 5) * bpr * 64 +
-                                           (long long)(sl & 31u) * 64 + (e & 7) * 8),
-                                 stage_unit(W, e));
-                }
-            }
-            if (seen != 0) {
-                const uint64_t M = seen & __ballot(active);
-                if ((M >> ln) & 1u) W.item[0][Q.n[0] + lane_rank(M)] = b;
-                Q.n[0] += __popcll(M);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        /* ---- chroma ---- the last block of a block row read the x0 = -8 quirk's rows for Y */
-        const bool last = c == bpr - 1u;
-        if (__ballot(last && active)) {
-            if (last) {
-                const uint8_t *p = g.rgb + (long long)f * g.in_fstride + 8ll * r * g.in_pitch + 24ll * c;
-#pragma unroll
-                for (int y = 0; y < 8; y++) {
-                    const uint8_t *q = (const uint8_t *)__builtin_assume_aligned(p + (long long)y * g.in_pitch, 8);
-                    u32x4 q4;
-                    u32x2 q2;
-                    __builtin_memcpy(&q4, q, 16);
-                    __builtin_memcpy(&q2, q + 16, 8);
-                    raw[y][0] = q4.x; raw[y][1] = q4.y; raw[y][2] = q4.z; raw[y][3] = q4.w;
-                    raw[y][4] = q2.x; raw[y][5] = q2.y;
-                }
-            }
-        }
-#pragma unroll
-        for (int y = 0; y < 8; y++)
-#pragma unroll
-            for (int q = 0; q < 6; q++) asm volatile("" : "+v"(raw[y][q]));
-        float Th[4][8];                                    /* this ln's 4 sample rows      */
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            float keep[4], got[4];
-#pragma unroll
-            for (int x = 0; x < 4; x++) {
-                const int i0 = 6 * x, i1 = 6 * x + 3;
-                const float R = ((float)byte_of(raw[2 * i], i0) + (float)byte_of(raw[2 * i], i1)) +
-                                ((float)byte_of(raw[2 * i + 1], i0) + (float)byte_of(raw[2 * i + 1], i1));
-                const float G = ((float)byte_of(raw[2 * i], i0 + 1) + (float)byte_of(raw[2 * i], i1 + 1)) +
-                                ((float)byte_of(raw[2 * i + 1], i0 + 1) + (float)byte_of(raw[2 * i + 1], i1 + 1));
-                const float B = ((float)byte_of(raw[2 * i], i0 + 2) + (float)byte_of(raw[2 * i], i1 + 2)) +
-                                ((float)byte_of(raw[2 * i + 1], i0 + 2) + (float)byte_of(raw[2 * i + 1], i1 + 2));
-                keep[x] = __builtin_fmaf(R, kk[0], __builtin_fmaf(G, kk[1], __builtin_fmaf(B, kk[2], -0.0f))) * 0.25f;
-                got[x] = swap_pair(
-                    __builtin_fmaf(R, ks[0], __builtin_fmaf(G, ks[1], __builtin_fmaf(B, ks[2], -0.0f))) * 0.25f);
-            }
-            float smp[8];
-#pragma unroll
-            for (int x = 0; x < 4; x++) {
-                smp[x] = odd ? got[x] : keep[x];
-                smp[4 + x] = odd ? keep[x] : got[x];
-            }
-            jx_fdct8<FOps>(smp, Th[i]);
-        }
-        /* top ln: columns 0..3 of all 8 rows; bottom ln: columns 4..7 */
-        float Tc[8][4];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int cc = 0; cc < 4; cc++) {
-                const float mine = h ? Th[i][4 + cc] : Th[i][cc];
-                const float give = h ? Th[i][cc] : Th[i][4 + cc];
-                const float other = __shfl_xor(give, 32, 64);
-                Tc[i][cc] = h ? other : mine;              /* rows 0..3: the top ln's     */
-                Tc[4 + i][cc] = h ? mine : other;
-            }
-        unsigned cslot = (ln & 1u) * 16u + m;             /* Cb blocks 0..15, Cr 16..31    */
-        asm volatile("" : "+v"(cslot));
-        /* opaque per tile: the per-ln selects of scales, limits and zig-zag positions would
-         * otherwise be hoisted out of the tile loop as 96 loop-invariant registers and spilled */
-        unsigned hsel = h;
-        asm volatile("" : "+v"(hsel));
-        const uint64_t cseen = cols_to_stage<4>(1, Tc, cband, 0, ac, W, cslot, hsel != 0);
-        const unsigned cb0 = f * nbc + my * mpr + mx0;      /* launch-global chroma block 0  */
-        int16_t *crow = gc.out + (long long)f * gc.out_fstride + (long long)(my * mpr + mx0) * 64;
-        if (full) {
-            unsigned o0 = (ln >> 3) * 33 + (ln & 7) * 4;
-            asm volatile("" : "+v"(o0));
-            u32x4 unit[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const unsigned o = o0 + 264u * (unsigned)j;
-                unit[j] = u32x4{W.stage[o], W.stage[o + 1], W.stage[o + 2], W.stage[o + 3]};
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                jx_store((u32x4 *)(crow + (long long)(1 + (j >> 1)) * nbc * 64) + (unsigned)(j & 1) * 64u + ln,
-                         unit[j]);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const unsigned e = (unsigned)j * 64u + ln, sl = e >> 3;
-                if (mx0 + (sl & 15u) < mpr)
-                    jx_store((u32x4 *)(crow + (long long)(1 + (sl >> 4)) * nbc * 64 +
-                                       (long long)(sl & 15u) * 64 + (e & 7) * 8),
-                             stage_unit(W, e));
-            }
-        }
-        if (cseen != 0) {
-            /* a block's two lanes (top and bottom) flag together: lanes 0..31 speak for it */
-            const uint64_t Mf = cseen & __ballot(active);
-            const uint64_t M = (Mf | (Mf >> 32)) & 0xFFFFFFFFull;
-            const uint64_t Mb = M & 0x55555555ull, Mr = M & 0xAAAAAAAAull;
-            const unsigned bc = cb0 + m;
-            if ((Mb >> ln) & 1u) W.item[1][Q.n[1] + lane_rank(Mb)] = bc;
-            if ((Mr >> ln) & 1u) W.item[2][Q.n[2] + lane_rank(Mr)] = bc;
-            Q.n[1] += __popcll(Mb);
-            Q.n[2] += __popcll(Mr);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        t += nwaves;
-        if (Q.n[0] > kItems - 64 || Q.n[1] > kItems - 16 || Q.n[2] > kItems - 16) break;
-    }
-    while (Q.n[0] > 0) {
-        int n[3] = {Q.n[0], 0, 0};
-        fix_queued(W, n, a, lane);
-        Q.n[0] = n[0];
-    }
-    fix_chroma(W, Q, 1, ac, lane);
-    fix_chroma(W, Q, 2, ac, lane);
-    if (t >= ntiles) break;
-    }
-}
-
 __device__ __forceinline__ uint8_t splitmix_byte(uint64_t seed, uint64_t k)
 {
     uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
@@ -1037,14 +773,10 @@ int tables_for_current_device()
                 for (int ch = 0; ch < 3; ch++)
                     for (int u = 0; u < 8; u++)
                         for (int v = 0; v < 8; v++) {
-                            /* slot 0 (luma is never averaged): the band both chroma channels
-                             * satisfy, for a kernel's mixed Cb / Cr lanes; for 4:2:0 also both
-                             * column halves u, u ^ 4 (k_sub420's top / bottom lanes) */
-                            const int k = v * 8 + u, k2 = v * 8 + (u ^ 4);
-                            const float j = std::min(lim[1][k], lim[2][k]);
-                            bn.lim[ch][u][v] = ch ? lim[ch][k]
-                                                  : (sm == 2 ? std::min(j, std::min(lim[1][k2], lim[2][k2]))
-                                                             : j);
+                            /* k_chroma reads the chroma slots; slot 0 (luma is never
+                             * averaged) holds the joint Cb / Cr band */
+                            const int k = v * 8 + u;
+                            bn.lim[ch][u][v] = ch ? lim[ch][k] : std::min(lim[1][k], lim[2][k]);
                             bf.lim[ch][u][v] = -1.0f;
                         }
             }
@@ -1081,7 +813,7 @@ int resident_waves()
 }
 
 /* Dispatch.  The product library (libjpgx.so) runs one kernel per mode: k_mx for 4:4:4,
- * k_mx422 / k_sub420 for true 4:2:2 / 4:2:0.  The test-only cross-check library
+ * k_mx422 / k_mx420 for true 4:2:2 / 4:2:0.  The test-only cross-check library
  * (libjpgx_alt.so, built from the same sources with -DJPGX_ALT_DISPATCH) runs the second
  * implementations instead: k_xform for 4:4:4 and k_xform (Y) + k_chroma<1|2> for true 4:2:x. */
 #ifndef JPGX_ALT_DISPATCH
@@ -1161,17 +893,8 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     const size_t waves = std::min<size_t>(ntiles, (size_t)std::max(resident_waves(), 4));
     const unsigned grid = (unsigned)((waves + JX_WG / 64 - 1) / (JX_WG / 64));
     if (sub && p->sample_ratio == 2 && !kAltDispatch) {
-        /* true 4:2:0 in one pass (k_sub420): tiles of 16 MCUs */
-        jx_geom gc = xa.g;
-        gc.bpr = fr->width / 16;
-        gc.nb = (int)nbc;
-        gc.out = d_out + (long long)nb * 64 - (long long)nbc * 64;
-        const size_t tiles = (size_t)((fr->width / 16 + 15) / 16) * (size_t)((fr->row_end - fr->row_begin) / 2) *
-                             (size_t)fr->nframes;
-        const size_t w = std::min<size_t>(tiles, (size_t)std::max(resident_waves(), 4));
-        const unsigned g2 = (unsigned)((w + JX_WG / 64 - 1) / (JX_WG / 64));
-        hipLaunchKernelGGL(k_sub420, dim3(g2), dim3(JX_WG), 0, s, xa, gc);
-        rc = hip_rc(hipGetLastError());
+        /* true 4:2:0 in one pass on the matrix cores (k_mx420, csrc/jpgx_mx.hip) */
+        rc = jx_launch_mx420(&xa, stream);
         if (!rc && event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
         return rc;
     }

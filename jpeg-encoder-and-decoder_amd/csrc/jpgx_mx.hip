@@ -585,11 +585,10 @@ __device__ __forceinline__ MxWL mx_wl(const MxTab &tb, unsigned t0, unsigned j)
 /* Column pass of one column (R pairs), quantiser, stage writes at za[v] + OFF, band flags (rare
  * path) into fl */
 template <unsigned OFF>
-__device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxWL &t, const uint32_t (&za)[8],
+__device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxWL &t, const uint32_t (&za)[8],
                                              uint32_t &fl, int kc)
 {
-    mx_f2 R[4], F[4];
-    mx_combine(acc[0], acc[1], acc[2], acc[3], R);
+    mx_f2 F[4];
     jx_fdct8_pk<MxPair>(R, F);
     const mx_f4 w01 = t.w01, w23 = t.w23, l01 = t.l01, l23 = t.l23;
     const mx_f2 W[4] = {mx_f2{w01.x, w01.y}, mx_f2{w01.z, w01.w}, mx_f2{w23.x, w23.y}, mx_f2{w23.z, w23.w}};
@@ -608,6 +607,16 @@ __device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxWL &t
         em = __builtin_fmaxf(__builtin_fmaxf(em, e.x), e.y);
     }
     if (__builtin_expect(__ballot(em >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * kc);
+}
+
+/* the same from the hi / lo accumulator tiles of rows 0..3 and 4..7 */
+template <unsigned OFF>
+__device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxWL &t, const uint32_t (&za)[8],
+                                             uint32_t &fl, int kc)
+{
+    mx_f2 R[4];
+    mx_combine(acc[0], acc[1], acc[2], acc[3], R);
+    mx_column_r<OFF>(R, t, za, fl, kc);
 }
 
 __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
@@ -1354,6 +1363,625 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
     if (nq) mx422_flush(L, nq, ns, g, T);
 }
 
+/* ==== k_mx420: true 4:2:0 (extension, JPGX_FLAG_SUBSAMPLE, sample_ratio 2) ==================
+ *
+ * A step is two consecutive MCUs (MCU-linear launch-global index, frames concatenated): their
+ * 16 pixel rows x 96 bytes (8 Y blocks: the top block row of the two MCUs is set 0, the bottom
+ * one set 1) land in a 1.5-KiB ring slot by the same LDS-DMA as k_mx; chunks of 6 steps (12
+ * MCUs) grid-stride, the ring's three slots holding step k in slot k % 3.
+ *   Y       k_mx422's Y: the two sets K-concatenated, column j = set j / 8 at u = j % 8.
+ *   Chroma  A row m = (MCU cb = m >> 3, chroma row Y' = m & 7), K = the 96 bytes of the MCU's
+ *           pixel rows 2Y', 2Y'+1 over three K = 32 products; B (jpgx_plan.cpp
+ *           jx_mx420_operands) holds 0.25 a[c][p] cos((2 floor(x/2) + 1) u pi/16): column j of
+ *           the one C tile is the row transform of the quad-averaged chroma, Cb (j < 8) or Cr, at
+ *           rows 4gq..4gq+3 of the tile.  Two consecutive steps form a pair: after the second,
+ *           one v_permlane16_swap per row value gives every lane a whole column of one of the
+ *           pair's four MCUs (lane gq: MCU (gq & 1) 2 + (gq >> 1) of the pair), so the chroma
+ *           column DCTs run once per pair on all 64 lanes: 1.5 column passes per step.
+ *   Output  per step 8 Y blocks in one store (lanes 0..31 the top row, 32..63 the bottom row,
+ *           bpr blocks further); per pair 4 Cb + 4 Cr blocks in one store (the first step of a
+ *           pair issues a padding operation instead, so every step counts two).
+ *   Quirk   a general step whose MCU's right block column is a row's last loads that column's
+ *           true pixel rows into L.qtrue for the chroma A operands.
+ *   Exact   Y tasks as k_mx422's (pixels copied from the slot); chroma tasks carry the MCU index
+ *           and read its pixels from global memory at flush time (the pair's first slot is gone
+ *           by then), in the oracle's order: ((ls(p00) + ls(p01)) + (ls(p10) + ls(p11))) * 0.25.
+ */
+constexpr unsigned kSteps420 = 6;             /* steps per chunk (3 pairs); ring slot = k % 3 */
+constexpr unsigned kCM420 = 2 * kSteps420;    /* MCUs per chunk */
+constexpr unsigned kVmWait420 = 4 * kDist - 2;
+constexpr int kWaitImm420 = (int)((kVmWait420 & 15u) | ((kVmWait420 >> 4) << 14) | 0xF70u);
+constexpr unsigned kSt420C = 8 * kBS;         /* chroma (c, lane group gq) at kSt420C + kBS (4 c + gq) */
+#ifndef JX_MX420_WPE
+#define JX_MX420_WPE 4
+#endif
+
+struct alignas(16) Mx420Lds {
+    uint8_t ring[3][kSlot];             /* [y 0..15][4 blocks x 24 B] */
+    uint8_t stage[16 * kBS];
+    uint8_t qtrue[2][384];              /* general step: MCU's right column, true rows [16][24] */
+    uint8_t pix[kSide][192];            /* deferred Y blocks' pixel rows [y][24] */
+    uint32_t sblk[kSide];               /* their launch-global Y block (frame-concatenated) */
+    uint32_t tmcu[kSide];               /* chroma task: launch-global MCU */
+    uint16_t dtask[kSide];              /* Y: slot << 8 | v << 3 | u; chroma: 0x8000 | c << 6 | v << 3 | u */
+    uint16_t task[8];
+    uint32_t dummy[64];
+};
+static_assert(sizeof(Mx420Lds) % 16 == 0 && sizeof(Mx420Lds) * 4 + sizeof(MxTab) <= 40 * 1024,
+              "4 workgroups of 4 waves per CU, 16-byte aligned regions");
+
+__device__ mx_u4 g_mx420B[JX_MX_PARTS * 5][64];  /* [part * 5 + which][lane] */
+__device__ jx_mxtab g_mx420tab[2][JX_MAXQ + 1];
+
+/* MCU geometry of the launch */
+struct Mx420G {
+    unsigned mpr, nmcu, tm, rows;       /* MCUs per row, per frame, in the launch; MCU rows per frame */
+};
+
+struct Mx420Chunk {
+    unsigned m0, f, mi, my, mx;         /* first MCU (launch-global), frame, MCU in frame, row, col */
+    const uint8_t *src;                 /* pixel (16 mx, 16 my) of frame f */
+    int16_t *ydst, *cdst;               /* Y block (2my, 2mx), chroma block mi (Cb) of frame f */
+    bool simple;
+};
+
+__device__ __forceinline__ void mx420_ptrs(Mx420Chunk &C, const MxG &g, const Mx420G &h)
+{
+    C.src = g.rgb + (long long)C.f * g.fstride + 16ll * C.my * g.pitch + 48ll * C.mx;
+    C.ydst = g.out + (long long)C.f * g.ofstride + 64ll * (2ull * C.my * g.bpr + 2u * C.mx);
+    C.cdst = g.out + (long long)C.f * g.ofstride + 64ll * (g.nb + C.mi);
+    C.simple = C.m0 + kCM420 <= h.tm && C.mx + kCM420 < h.mpr && g.lin_store;
+}
+
+__device__ __forceinline__ void mx420_at(Mx420Chunk &C, const MxG &g, const Mx420G &h, unsigned m0)
+{
+    C.m0 = m0;
+    C.f = m0 / h.nmcu;
+    C.mi = m0 - C.f * h.nmcu;
+    C.my = C.mi / h.mpr;
+    C.mx = C.mi - C.my * h.mpr;
+    mx420_ptrs(C, g, h);
+}
+
+__device__ __forceinline__ void mx420_next(Mx420Chunk &C, const MxG &g, const Mx420G &h, const MxJump &J)
+{
+    C.m0 += J.jb;
+    if (C.m0 >= h.tm) return;
+    C.mi += J.jb;
+    C.mx += J.jc;
+    C.my += J.jr;
+    if (C.mx >= h.mpr) {
+        C.mx -= h.mpr;
+        C.my++;
+    }
+    while (C.mi >= h.nmcu) {
+        C.mi -= h.nmcu;
+        C.my -= h.rows;
+        C.f++;
+    }
+    mx420_ptrs(C, g, h);
+}
+
+/* Position of the launch-global MCU m: frame, MCU in frame, row, column */
+__device__ __forceinline__ void mx420_mcu(const Mx420G &h, unsigned m, unsigned &f, unsigned &mi,
+                                          unsigned &my, unsigned &mx)
+{
+    f = m / h.nmcu;
+    mi = m - f * h.nmcu;
+    my = mi / h.mpr;
+    mx = mi - my * h.mpr;
+}
+
+/* A general step's pixels (row / frame crossings, a row's last MCU, the launch's end): lane l
+ * loads pixel row y = l & 15 of block column jb = l >> 4 (MCU m0 + jb / 2, its column jb % 2)
+ * with the reference's addressing (the x0 = -8 quirk for the row's last block, the underflow
+ * bytes at frame block-row 0) into the slot; MCUs past the launch's end are clamped copies. */
+__device__ __forceinline__ void mx420_issue_general(const MxG &g, const Mx420G &h, unsigned m0, uint8_t *slot)
+{
+    const unsigned lane = mx_lane(), y = lane & 15u, jb = lane >> 4;
+    unsigned m = m0 + (jb >> 1);
+    m = m < h.tm ? m : h.tm - 1u;
+    unsigned f, mi, my, mx;
+    mx420_mcu(h, m, f, mi, my, mx);
+    const unsigned br = 2u * my + (y >> 3), bc = 2u * mx + (jb & 1u), yy = y & 7u;
+    const bool last = bc == g.bpr - 1u;
+    const bool under = last && yy == 0 && g.row0 + (int)br == 0;
+    const long long prow = under ? 8ll * br : 8ll * br + yy - (last ? 1 : 0);
+    typedef const __attribute__((address_space(1))) mx_u2 gu2;
+    const gu2 *src = (const gu2 *)(g.rgb + (long long)f * g.fstride + prow * g.pitch + 24ll * bc);
+    mx_u2 v0 = src[0], v1 = src[1], v2 = src[2];
+    if (under) {
+        v0 = mx_u2{g.u[0], g.u[1]};
+        v1 = mx_u2{g.u[2], g.u[3]};
+        v2 = mx_u2{g.u[4], g.u[5]};
+    }
+    uint8_t *d = slot + 96u * y + 24u * jb;
+    *(mx_u2 *)d = v0;
+    *(mx_u2 *)(d + 8) = v1;
+    *(mx_u2 *)(d + 16) = v2;
+    __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0) (rare; conservative) */
+}
+
+/* a general step's MCUs whose right block column is a row's last: its true pixel rows (16 x 24 B)
+ * into L.qtrue[MCU of the step]; returns the mask of those MCUs */
+__device__ __forceinline__ uint32_t mx420_true_rows(Mx420Lds &L, const MxG &g, const Mx420G &h, unsigned m0)
+{
+    const unsigned l = mx_lane(), y = l & 15u, ms = (l >> 4) & 1u;
+    const unsigned m = m0 + ms;
+    bool last = false;
+    unsigned f = 0, mi = 0, my = 0, mx = 0;
+    if (l < 32 && m < h.tm) {
+        mx420_mcu(h, m, f, mi, my, mx);
+        last = 2u * mx + 1u == g.bpr - 1u;
+    }
+    const uint64_t bal = __ballot(last && y == 0);
+    const uint32_t qm = (uint32_t)(bal & 1u) | (uint32_t)((bal >> 16) & 1u) << 1;
+    if (qm) {
+        if (last) {
+            typedef const __attribute__((address_space(1))) mx_u2 gu2;
+            const gu2 *src = (const gu2 *)(g.rgb + (long long)f * g.fstride + (16ll * my + y) * g.pitch +
+                                           24ll * (2u * mx + 1u));
+            const mx_u2 v0 = src[0], v1 = src[1], v2 = src[2];
+            uint8_t *d = L.qtrue[ms] + 24u * y;
+            *(mx_u2 *)d = v0;
+            *(mx_u2 *)(d + 8) = v1;
+            *(mx_u2 *)(d + 16) = v2;
+        }
+        __builtin_amdgcn_s_waitcnt(0xF70);
+        mx_wave_sync();
+    }
+    return qm;
+}
+
+/* One exact chroma coefficient per 8-lane group from the MCU's pixels in global memory: lane x
+ * averages the quad ((ls(p00) + ls(p01)) + (ls(p10) + ls(p11))) * 0.25 of chroma row y
+ * (oracle/cpu_ref.c cpuref_chroma_sample), then as mx_exact_coef.  row0 = the MCU's pixel (0, 0).
+ * Valid in lane x == 7. */
+__device__ __forceinline__ int mx_exact_quad(const uint8_t *row0, long long pitch, unsigned ch, unsigned u,
+                                             unsigned v, unsigned x, const jx_mxtab &T)
+{
+    const double cu = kMxCos[u][x];
+    const double k0c = kMxColour[ch][0], k1c = kMxColour[ch][1], k2c = kMxColour[ch][2];
+    const double Ac = kMxColour[ch][3], Sc = kMxColour[ch][4];
+    double prod[8];
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+        const uint8_t *p = row0 + (2ll * y) * pitch + 6u * x, *q = p + pitch;
+        const double l00 = (Ac + Sc * ((k0c * (double)p[0] + k1c * (double)p[1]) + k2c * (double)p[2])) - 128.0;
+        const double l01 = (Ac + Sc * ((k0c * (double)p[3] + k1c * (double)p[4]) + k2c * (double)p[5])) - 128.0;
+        const double l10 = (Ac + Sc * ((k0c * (double)q[0] + k1c * (double)q[1]) + k2c * (double)q[2])) - 128.0;
+        const double l11 = (Ac + Sc * ((k0c * (double)q[3] + k1c * (double)q[4]) + k2c * (double)q[5])) - 128.0;
+        const double X = ((l00 + l01) + (l10 + l11)) * 0.25;
+        prod[y] = X * cu * kMxCos[v][y];
+    }
+    return mx_exact_sum(prod, ch, u, v, x, T);
+}
+
+/* the MCU's pixel (0, 0) */
+__device__ __forceinline__ const uint8_t *mx420_mcu_src(const MxG &g, const Mx420G &h, unsigned m)
+{
+    unsigned f, mi, my, mx;
+    mx420_mcu(h, m, f, mi, my, mx);
+    return g.rgb + (long long)f * g.fstride + 16ll * my * g.pitch + 48ll * mx;
+}
+
+/* pair-MCU of a chroma-column lane group (the permlane16 swap's order) */
+__device__ __forceinline__ unsigned mx420_pm(unsigned gq) { return (gq & 1u) * 2u + (gq >> 1); }
+
+/* Inline exact pass: Y bits (col 0) of this step and chroma bits (col 1, pair base mp) */
+__device__ __forceinline__ void mx420_exact_inline(Mx420Lds &L, const uint8_t *sp, uint32_t bits, unsigned mp,
+                                                   const MxG &g, const Mx420G &h, const jx_mxtab &T)
+{
+    const unsigned lane = mx_lane();
+    mx_wave_sync();
+    for (;;) {
+        const uint64_t act = __ballot(bits != 0);
+        if (!act) break;
+        const int rk = mx_rank(act);
+        if (bits != 0 && rk < 8) {
+            const unsigned b = (unsigned)__builtin_ctz(bits);
+            bits &= bits - 1u;
+            L.task[rk] = (uint16_t)(lane << 8 | b);
+        }
+        mx_wave_sync();
+        const int nt = std::min((int)__popcll(act), 8);
+        const unsigned i = lane >> 3, x = lane & 7u;
+        const bool live = (int)i < nt;
+        const unsigned code = L.task[live ? i : 0u];
+        const unsigned sl = code >> 8, k = (code >> 3) & 1u, v = code & 7u;
+        const unsigned jj = sl & 15u, u = jj & 7u, gq = sl >> 4;
+        const unsigned slot = 4u * (jj >> 3) + gq;     /* Y: set (j / 8), block gq; chroma: (c, gq) */
+        int val;
+        if (k == 0) {
+            val = mx_exact_pair(mx_lds((void *)sp) + 96u * 8u * (jj >> 3) + 24u * gq + 3u * x, 96u, 0u, 0u, u, v,
+                                x, T);
+        } else {
+            unsigned m = mp + mx420_pm(gq);
+            m = m < h.tm ? m : h.tm - 1u;
+            val = mx_exact_quad(mx420_mcu_src(g, h, m), g.pitch, 1u + (jj >> 3), u, v, x, T);
+        }
+        if (live && x == 7)
+            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + (k ? kSt420C : 0u) + kBS * slot +
+                                                           2u * (unsigned)kMxScan[v][u]) = (int16_t)val;
+        mx_wave_sync();
+    }
+}
+
+__device__ __forceinline__ void mx420_flush(Mx420Lds &L, int &nq, int &ns, const MxG &g, const Mx420G &h,
+                                            const jx_mxtab &T)
+{
+    __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0): the tasks' blocks are stored */
+    mx_wave_sync();
+    const unsigned lane = mx_lane(), i = lane >> 3, x = lane & 7u;
+    const bool live = (int)i < nq;
+    const unsigned code = L.dtask[live ? i : 0u];
+    const unsigned v = (code >> 3) & 7u, u = code & 7u;
+    int val;
+    long long dst;
+    if (code & 0x8000u) {
+        const unsigned ch = (code >> 6) & 3u, m = L.tmcu[live ? i : 0u];
+        unsigned f, mi, my, mx;
+        mx420_mcu(h, m, f, mi, my, mx);
+        val = mx_exact_quad(g.rgb + (long long)f * g.fstride + 16ll * my * g.pitch + 48ll * mx, g.pitch, ch, u,
+                            v, x, T);
+        dst = (long long)f * g.ofstride + ((long long)g.nb + (ch - 1u) * h.nmcu + mi) * 64;
+    } else {
+        const unsigned slot = code >> 8;
+        val = mx_exact_pair(mx_lds(L.pix[slot]) + 3u * x, 24u, 0u, 0u, u, v, x, T);
+        const unsigned b = L.sblk[slot], f = b / g.nb, bi = b - f * g.nb;
+        dst = (long long)f * g.ofstride + (long long)bi * 64;
+    }
+    if (live && x == 7) g.out[dst + kMxScan[v][u]] = (int16_t)val;
+    mx_wave_sync();
+    nq = 0;
+    ns = 0;
+}
+
+/* Y block (launch-global, frame-concatenated) of step m0's block (set, jb) */
+__device__ __forceinline__ unsigned mx420_yblock(const MxG &g, const Mx420G &h, unsigned m0, unsigned set,
+                                                 unsigned jb)
+{
+    unsigned f, mi, my, mx;
+    mx420_mcu(h, m0 + (jb >> 1), f, mi, my, mx);
+    return f * g.nb + (2u * my + set) * g.bpr + 2u * mx + (jb & 1u);
+}
+
+/* Queue a step's flagged coefficients: bits 0..7 Y (this step's blocks), 8..15 chroma (pair base
+ * mp, only on a pair's second step) */
+__device__ __forceinline__ void mx420_defer(Mx420Lds &L, const uint8_t *sp, uint32_t bits, unsigned m0, unsigned mp,
+                                            int &nq, int &ns, const MxG &g, const Mx420G &h, const jx_mxtab &T)
+{
+    const unsigned lane = mx_lane();
+    {   /* clamped MCUs past the launch's end: no tasks (Y block (set, gq) is MCU m0 + gq / 2) */
+        const unsigned gq = lane >> 4;
+        if (m0 + (gq >> 1) >= h.tm) bits &= ~0xffu;
+        if (mp + mx420_pm(gq) >= h.tm) bits &= ~0xff00u;
+    }
+    const uint64_t m0b = __ballot((bits & 0xffu) != 0);
+    uint32_t yblk = 0;
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) {
+        yblk |= (((m0b >> (16 * gq)) & 0xffu) ? 1u : 0u) << gq;              /* set 0, block gq */
+        yblk |= (((m0b >> (16 * gq + 8)) & 0xffu) ? 1u : 0u) << (4 + gq);    /* set 1 */
+    }
+    const unsigned cnt = (unsigned)__popc(bits);
+    unsigned incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned o = __shfl_up(incl, d, 64);
+        if ((int)lane >= d) incl += o;
+    }
+    const int ntask = (int)__builtin_amdgcn_readlane(incl, 63);
+    const int ny = __popc(yblk);
+    if (nq + ntask > kSide || ns + ny > kSide) {
+        if (nq) mx420_flush(L, nq, ns, g, h, T);
+        if (ntask > kSide) {
+            mx420_exact_inline(L, sp, bits, mp, g, h, T);
+            return;
+        }
+    }
+    {   /* Y blocks' pixel rows to side slots (lane < 48: row l / 6, dword l % 6) */
+        const unsigned y = lane / 6u, k = lane - 6u * y;
+        uint32_t bm = yblk;
+        int t = ns;
+        while (bm) {
+            const unsigned yb = (unsigned)__builtin_ctz(bm), set = yb >> 2, jb = yb & 3u;
+            bm &= bm - 1u;
+            if (lane < 48)
+                *(__attribute__((address_space(3))) uint32_t *)(mx_lds(L.pix[t]) + 24u * y + 4u * k) =
+                    *(const __attribute__((address_space(3))) uint32_t *)(mx_lds((void *)sp) + 96u * (8u * set + y) +
+                                                                          24u * jb + 4u * k);
+            if (lane == 0) L.sblk[t] = mx420_yblock(g, h, m0, set, jb);
+            t++;
+        }
+    }
+    {
+        unsigned pos = (unsigned)nq + incl - cnt;
+        const unsigned jj = lane & 15u, u = jj & 7u, gq = lane >> 4;
+        while (bits) {
+            const unsigned b = (unsigned)__builtin_ctz(bits);
+            bits &= bits - 1u;
+            const unsigned v = b & 7u;
+            if (b < 8) {
+                const unsigned yb = 4u * (jj >> 3) + gq;
+                const unsigned slot = (unsigned)ns + (unsigned)__popc(yblk & ((1u << yb) - 1u));
+                L.dtask[pos] = (uint16_t)(slot << 8 | v << 3 | u);
+            } else {
+                L.dtask[pos] = (uint16_t)(0x8000u | (1u + (jj >> 3)) << 6 | v << 3 | u);
+                L.tmcu[pos] = mp + mx420_pm(gq);
+            }
+            pos++;
+        }
+    }
+    mx_wave_sync();
+    nq += ntask;
+    ns += ny;
+}
+
+__global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args a)
+{
+    __shared__ __attribute__((aligned(16))) Mx420Lds s_lds[4];
+    __shared__ __attribute__((aligned(16))) MxTab s_tab;
+    MxG g;
+    g.rgb = a.g.rgb;
+    g.out = a.g.out;
+    g.pitch = a.g.in_pitch;
+    g.fstride = a.g.in_fstride;
+    g.ofstride = a.g.out_fstride;
+    g.bpr = (unsigned)a.g.bpr;
+    g.nb = (unsigned)a.g.nb;
+    g.total = (unsigned)a.g.nb * (unsigned)a.g.nframes;
+    g.row0 = a.g.row0;
+    g.quality = a.quality;
+    g.force = a.force_exact;
+    g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
+#pragma unroll
+    for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+    Mx420G h;
+    h.mpr = g.bpr / 2u;
+    h.rows = g.nb / g.bpr / 2u;
+    h.nmcu = h.rows * h.mpr;
+    h.tm = h.nmcu * (unsigned)a.g.nframes;
+
+    const unsigned lane = threadIdx.x & 63u;
+    Mx420Lds &L = s_lds[threadIdx.x >> 6];
+    const jx_mxtab &T = g_mx420tab[g.force ? 1 : 0][g.quality];
+    if (threadIdx.x < 64) {
+        const unsigned t = lane >> 4, jp = lane & 15u;
+        const unsigned n = t < 2 ? (jp & 7u) : 8u + jp;
+        float x[8];
+#pragma unroll
+        for (int p = 0; p < 4; p++)
+#pragma unroll
+            for (int hh = 0; hh < 2; hh++) {
+                const int v = jx_pk_k(p, hh);
+                x[2 * p + hh] = (t & 1u) ? T.lsq[n][v] : T.w[n][v];
+            }
+        s_tab.wl[t][0][jp] = mx_f4{x[0], x[1], x[2], x[3]};
+        s_tab.wl[t][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
+    }
+    __syncthreads();
+    const unsigned nw = gridDim.x * 4u;
+    const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (kCM420 * wv >= h.tm) return;
+
+    /* Y A operand: row m = 4 jb + y' (block jb of the set, pixel row y' of the half), k-group q
+     * (bytes 8q.. of the block row; q = 3 the bias); set s / half hh at +768 s + 384 hh.
+     * Chroma A operand: row m = (MCU cb = m >> 3, chroma row Y' = m & 7); k-step 0: bytes 8q.. of
+     * pixel row 2Y' (48 cb + ..), k-step 1: bytes 32 + 8q (q < 2) of row 2Y', bytes 8 (q - 2) of
+     * row 2Y' + 1 (q >= 2), k-step 2: bytes 16 + 8q of row 2Y' + 1 */
+    const unsigned m = lane & 15u, q = lane >> 4;
+    const uint32_t aoff = 96u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 0u);
+    const uint32_t s0 = q < 3 ? kSelLo : kSelOne;
+    const uint32_t s1 = q < 3 ? kSelHi : kSelZero;
+    const uint32_t s2 = q < 3 ? kSelLo : kSelZero;
+    const uint32_t cof0 = 192u * (m & 7u) + 48u * (m >> 3) + 8u * q;
+    const uint32_t cof1 = cof0 + (q < 2 ? 32u : 80u);
+    const uint32_t off0 = (uint32_t)((lane / 6u) * (unsigned)g.pitch + 16u * (lane % 6u));
+    const uint32_t off1 = (uint32_t)(((64u + lane) / 6u) * (unsigned)g.pitch + 16u * ((64u + lane) % 6u));
+    /* stores: Y lanes 0..31 the top block row's 4 blocks, 32..63 the bottom row's; chroma lanes
+     * 0..31 Cb of the pair's 4 MCUs, 32..63 Cr; stage reads at ro (Y) and rc (chroma: lane group
+     * gq of the column pass holds pair-MCU mx420_pm(gq), an involution) */
+    const uint32_t soy = (lane & 31u) * 16u + (lane >> 5) * g.bpr * 128u;
+    const uint32_t soc = (lane & 31u) * 16u + (lane >> 5) * h.nmcu * 128u;
+    const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
+    const uint32_t rc = kSt420C + kBS * (4u * (lane >> 5) + mx420_pm((lane >> 3) & 3u)) + (lane & 7u) * 16u;
+
+    const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
+    uint32_t za[8];
+    {
+        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * (4u * (j >> 3) + gq);
+#pragma unroll
+        for (int v = 0; v < 8; v++) za[v] = base + 2u * (unsigned)kMxScan[v][u];
+    }
+    mx_u4 B[kParts][5];
+#pragma unroll
+    for (int p = 0; p < kParts; p++)
+#pragma unroll
+        for (int w = 0; w < 5; w++) B[p][w] = g_mx420B[5 * p + w][lane];
+    __builtin_amdgcn_s_waitcnt(0xF70);              /* see k_mx422 */
+
+    MxJump J;
+    J.jb = kCM420 * nw;
+    J.jr = J.jb / h.mpr;
+    J.jc = J.jb - J.jr * h.mpr;
+    J.rows = h.rows;
+    Mx420Chunk cc;
+    mx420_at(cc, g, h, kCM420 * wv);
+    Mx420Chunk nx = cc;
+
+    const auto issue = [&](const Mx420Chunk &C, unsigned k) {
+        uint8_t *const slot = L.ring[k % 3u];
+        const unsigned m0 = C.m0 + 2u * k;
+        if (m0 >= h.tm) {
+            mx_pad(g, L, 2);
+        } else if (C.simple) {
+            const uint8_t *base = C.src + 96u * k;
+            __builtin_amdgcn_global_load_lds((mx_gp)(base + off0), (mx_lp)slot, 16, 0, 0);
+            if (lane < 32) __builtin_amdgcn_global_load_lds((mx_gp)(base + off1), (mx_lp)(slot + 1024u), 16, 0, 0);
+        } else {
+            mx420_issue_general(g, h, m0, slot);
+        }
+    };
+    for (unsigned d = 0; d < kDist; d++) {
+        issue(cc, d);
+        mx_pad(g, L, 2);
+    }
+    int nq = 0, ns = 0;
+    unsigned k = 0;
+    mx_f4 rA = {};                                 /* chroma R of the pair's first step */
+    for (;;) {
+        const unsigned m0 = cc.m0 + 2u * k;
+        __builtin_amdgcn_s_waitcnt(kWaitImm420);
+        mx_wave_sync();
+        const uint8_t *const sp = L.ring[k % 3u];
+        if (k + kDist < kSteps420) {
+            issue(cc, k + kDist);
+        } else {
+            if (k + kDist == kSteps420) mx420_next(nx, g, h, J);
+            issue(nx, k + kDist - kSteps420);
+        }
+        const uint32_t qmask = cc.simple ? 0u : mx420_true_rows(L, g, h, m0);
+        const mx_f4 z = {};
+        uint32_t fl = 0;
+        mx_f4 accY[4], accC[2];
+        const mx_u2 y00 = *(const mx_u2 *)(sp + aoff);
+        const mx_u2 y01 = *(const mx_u2 *)(sp + aoff + 384u);
+        const mx_u2 y10 = *(const mx_u2 *)(sp + aoff + 768u);
+        const mx_u2 y11 = *(const mx_u2 *)(sp + aoff + 1152u);
+        mx_u2 c0, c1, c2;
+        if (__builtin_expect(qmask == 0, 1)) {
+            c0 = *(const mx_u2 *)(sp + cof0);
+            c1 = *(const mx_u2 *)(sp + cof1);
+            c2 = *(const mx_u2 *)(sp + cof0 + 112u);
+        } else {
+            /* MCUs whose right block column is a row's last: bytes 24..47 of a 48-byte MCU row
+             * from the true rows (k-step 0: q = 3; k-step 1: q < 2; k-step 2: q >= 1) */
+            const unsigned l = mx_lane(), mm = l & 15u, qq = l >> 4, cb = mm >> 3, yr = 2u * (mm & 7u);
+            const bool qb = (qmask >> cb) & 1u;
+            const uint8_t *qt = L.qtrue[cb];
+            const uint8_t *p0 = qb && qq == 3 ? qt + 24u * yr : sp + cof0;
+            const uint8_t *p1 = qb && qq < 2 ? qt + 24u * yr + 8u + 8u * qq : sp + cof1;
+            const uint8_t *p2 = qb && qq >= 1 ? qt + 24u * (yr + 1u) + 8u * (qq - 1u) : sp + cof0 + 112u;
+            c0 = *(const mx_u2 *)p0;
+            c1 = *(const mx_u2 *)p1;
+            c2 = *(const mx_u2 *)p2;
+        }
+        {
+            const mx_h8 Al0 = mx_aop(y00, s0, s1, s2), Ah0 = mx_aop(y01, s0, s1, s2);
+            const mx_h8 Al1 = mx_aop(y10, s0, s1, s2), Ah1 = mx_aop(y11, s0, s1, s2);
+            accY[0] = mx_mma(Al0, B[0][0], z);
+            accY[2] = mx_mma(Ah0, B[0][0], z);
+            accY[1] = mx_mma(Al0, B[1][0], z);
+            accY[3] = mx_mma(Ah0, B[1][0], z);
+            accY[0] = mx_mma(Al1, B[0][1], accY[0]);
+            accY[2] = mx_mma(Ah1, B[0][1], accY[2]);
+            accY[1] = mx_mma(Al1, B[1][1], accY[1]);
+            accY[3] = mx_mma(Ah1, B[1][1], accY[3]);
+            if (kParts == 3) {
+                accY[1] = mx_mma(Al0, B[kParts - 1][0], accY[1]);
+                accY[3] = mx_mma(Ah0, B[kParts - 1][0], accY[3]);
+                accY[1] = mx_mma(Al1, B[kParts - 1][1], accY[1]);
+                accY[3] = mx_mma(Ah1, B[kParts - 1][1], accY[3]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        {
+            const mx_h8 C0 = mx_aop(c0, kSelLo, kSelHi, kSelLo), C1 = mx_aop(c1, kSelLo, kSelHi, kSelLo);
+            const mx_h8 C2 = mx_aop(c2, kSelLo, kSelHi, kSelLo);
+            accC[0] = mx_mma(C0, B[0][2], z);
+            accC[1] = mx_mma(C0, B[1][2], z);
+            accC[0] = mx_mma(C1, B[0][3], accC[0]);
+            accC[1] = mx_mma(C1, B[1][3], accC[1]);
+            accC[0] = mx_mma(C2, B[0][4], accC[0]);
+            accC[1] = mx_mma(C2, B[1][4], accC[1]);
+            if (kParts == 3) {
+                accC[1] = mx_mma(C0, B[kParts - 1][2], accC[1]);
+                accC[1] = mx_mma(C1, B[kParts - 1][3], accC[1]);
+                accC[1] = mx_mma(C2, B[kParts - 1][4], accC[1]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mx_column_t<0>(accY, mx_wl(s_tab, 0, j), za, fl, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        const mx_f4 s12 = {0x1p-12f, 0x1p-12f, 0x1p-12f, 0x1p-12f};
+        const mx_f4 rc4 = __builtin_elementwise_fma(accC[1], s12, accC[0]);
+        const bool second = (k & 1u) != 0;
+        if (second) {
+            /* rows Y' 0..3 / 4..7 of the lane's pair-MCU column: lanes in even 16-lane rows take
+             * the first step's tile, odd rows the second's */
+            mx_f2 R[4];
+            float lo4[4], hi4[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(rA[i]), __float_as_uint(rc4[i]),
+                                                                false, false);
+                lo4[i] = __uint_as_float(r[0]);
+                hi4[i] = __uint_as_float(r[1]);
+            }
+            R[0] = mx_f2{lo4[0], lo4[1]};
+            R[1] = mx_f2{lo4[2], lo4[3]};
+            R[2] = mx_f2{hi4[0], hi4[1]};
+            R[3] = mx_f2{hi4[2], hi4[3]};
+            mx_column_r<kSt420C>(R, mx_wl(s_tab, 2, j), za, fl, 1);
+        } else {
+            rA = rc4;
+        }
+        mx_wave_sync();
+        const unsigned mp = m0 - 2u;                   /* the pair's first MCU (second step) */
+        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
+            mx420_defer(L, sp, fl, m0, second ? mp : 0u, nq, ns, g, h, T);
+            __builtin_amdgcn_s_waitcnt(0xF70);         /* see mx422_defer_step */
+        }
+        /* always two VMEM operations per step: the Y store, and the chroma store or a pad */
+        if (cc.simple) {
+            const mx_u4 vy = *(const mx_u4 *)(L.stage + ro);
+            __builtin_nontemporal_store(vy, (mx_u4 *)((const uint8_t *)(cc.ydst + 256u * k) + soy));
+            if (second) {
+                const mx_u4 vc = *(const mx_u4 *)(L.stage + rc);
+                __builtin_nontemporal_store(vc, (mx_u4 *)((const uint8_t *)(cc.cdst + 256u * (k >> 1)) + soc));
+            } else {
+                mx_pad(g, L, 1);
+            }
+        } else {
+            const unsigned l = mx_lane();
+            {   /* Y: lane's block (set l >> 5, block column (l >> 3) & 3 of the step) */
+                const unsigned jb = (l >> 3) & 3u, mm = m0 + (jb >> 1);
+                const unsigned mc = mm < h.tm ? mm : h.tm - 1u;
+                const unsigned yb = mx420_yblock(g, h, mc - (jb >> 1), l >> 5, jb);
+                const unsigned f = yb / g.nb, bi = yb - f * g.nb;
+                const mx_u4 vy = *(const mx_u4 *)(L.stage + (l >> 3) * kBS + (l & 7u) * 16u);
+                if (mm < h.tm)
+                    __builtin_nontemporal_store(
+                        vy, (mx_u4 *)(g.out + (long long)f * g.ofstride + (long long)bi * 64 + (l & 7u) * 8));
+            }
+            if (second) {
+                const unsigned pm = (l >> 3) & 3u, mm = mp + pm;
+                const unsigned mc = mm < h.tm ? mm : h.tm - 1u;
+                unsigned f, mi, my, mx;
+                mx420_mcu(h, mc, f, mi, my, mx);
+                const mx_u4 vc = *(const mx_u4 *)(L.stage + kSt420C + kBS * (4u * (l >> 5) + mx420_pm(pm)) +
+                                                   (l & 7u) * 16u);
+                if (mm < h.tm)
+                    __builtin_nontemporal_store(
+                        vc, (mx_u4 *)(g.out + (long long)f * g.ofstride +
+                                      ((long long)g.nb + (l >> 5) * h.nmcu + mi) * 64 + (l & 7u) * 8));
+            } else {
+                mx_pad(g, L, 1);
+            }
+        }
+        mx_wave_sync();
+        if (++k == kSteps420) {
+            k = 0;
+            cc = nx;
+            if (cc.m0 >= h.tm) break;
+        } else if (m0 + 2u >= h.tm && second) {
+            break;
+        }
+    }
+    if (nq) mx420_flush(L, nq, ns, g, h, T);
+}
+
 int mx_rc(hipError_t e) { return e == hipSuccess ? JPGX_OK : JPGX_EHIP; }
 
 constexpr int kMaxDev = 64;
@@ -1455,7 +2083,67 @@ int mx422_tables_for_current_device(int *waves)
     return g_mx422_rc[dev];
 }
 
+std::once_flag g_mx420_once[kMaxDev];
+int g_mx420_rc[kMaxDev];
+int g_mx420_waves[kMaxDev];
+
+int mx420_tables_for_current_device(int *waves)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return JPGX_ENODEV;
+    std::call_once(g_mx420_once[dev], [dev]() {
+        std::vector<jx_mxtab> tab(2 * (JX_MAXQ + 1));
+        memset(tab.data(), 0, tab.size() * sizeof(jx_mxtab));
+        int rc = JPGX_OK;
+        for (int q = 1; q <= JX_MAXQ && !rc; q++) {
+            float w[24][8], lim[24][8];
+            int16_t qq[2][64];
+            rc = jx_plan_tables_mx420(q, w, lim, qq);
+            for (int f = 0; f < 2; f++) {
+                jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
+                memcpy(t.q, qq, sizeof qq);
+                for (int n = 0; n < 24; n++)
+                    for (int v = 0; v < 8; v++) {
+                        t.w[n][v] = w[n][v] * kRScale;
+                        t.lsq[n][v] = f ? -1.0f : mx_lsq(lim[n][v]);
+                    }
+            }
+        }
+        static uint16_t ops[JX_MX_PARTS][5][64][8];
+        if (!rc) rc = jx_mx420_operands(ops);
+        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx420tab), tab.data(),
+                                              tab.size() * sizeof(jx_mxtab)));
+        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx420B), ops, sizeof ops));
+        int cus = 0, per_cu = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mx420, 256, JX_MX_DYNLDS) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 2;
+        g_mx420_waves[dev] = cus * per_cu * 4;
+        g_mx420_rc[dev] = rc;
+    });
+    if (waves) *waves = g_mx420_waves[dev];
+    return g_mx420_rc[dev];
+}
+
 }  // namespace
+
+
+/* k_mx420 over every frame of the stripe (true 4:2:0: Y [nb][64], Cb and Cr [nb / 4][64] per
+ * frame, the stripe an even number of block rows); no workspace. */
+extern "C" int jx_launch_mx420(const jx_xform_args *xa, void *stream)
+{
+    int waves = 0;
+    const int rc = mx420_tables_for_current_device(&waves);
+    if (rc) return rc;
+    const size_t mcus = (size_t)xa->g.nb / 4 * (size_t)xa->g.nframes;
+    const size_t chunks = (mcus + kCM420 - 1) / kCM420;
+    const size_t w = std::min<size_t>(chunks, (size_t)std::max(waves, 4));
+    const unsigned grid = (unsigned)((w + 3) / 4);
+    hipLaunchKernelGGL(k_mx420, dim3(grid), dim3(256), JX_MX_DYNLDS, (hipStream_t)stream, *xa);
+    return mx_rc(hipGetLastError());
+}
 
 
 /* k_mx422 over every frame of the stripe (true 4:2:2: Y [nb][64], Cb and Cr [nb / 2][64] per

@@ -568,75 +568,76 @@ extern "C" int jx_plan_tables_mx(int quality, float w[24][8], float lim[24][8], 
     return JPGX_OK;
 }
 
-/* ---- k_mx422: true 4:2:2 on the matrix cores ------------------------------------------
+/* ---- k_mx422 / k_mx420: true 4:2:2 / 4:2:0 on the matrix cores --------------------------
  *
  * Y is k_mx's Y (plan columns n = u, the 4:4:4 split S), its B laid out K-concatenated: the
  * product A_set0 B_Y0 + A_set1 B_Y1 puts set 0's blocks in C columns 0..7 and set 1's in
  * 8..15 (B_Y0 zero in columns 8..15, B_Y1 zero in 0..7), exactly as k_mx's Cr tile.
- * Chroma (the EXTENSION's definition, oracle/cpu_ref.c cpuref_chroma_sample): a chroma row of
- * a chroma block is the 16 pixels (48 bytes) of its two Y blocks' row; the sample X is the
- * average of pixels 2X, 2X+1 of the level-shifted chroma, so the row transform is
- *   R(u) = sum_{x < 16, p} b_{3x+p} 0.5 a[c][p] cos((2 floor(x/2) + 1) u pi/16)
- * (a = kMxA[c], c = Cb, Cr; b = the byte: the level-shifted chroma has no constant, so the bias
- * row k = 48 is zero), i.e. B_C[k][n] over k = 3x + p < 48, n = 8 c' + u (c' = 0 Cb, 1 Cr).
- * Two K = 32 MFMAs per chroma row tile (k = 0..31, 32..63).  Same encoding and split as k_mx: Bh a multiple
- * of 2^-11 (acc_h exact in any order: every partial sum a multiple of 2^-11 below 2^13), the lo
- * part(s) scaled by 2^12, each of acc_l's additions charged one ulp (65 per chroma row: two
- * MFMAs of 32 products plus the accumulator).
+ * Chroma (the EXTENSION's definition, oracle/cpu_ref.c cpuref_chroma_sample): a chroma row of a
+ * chroma block is, for 4:2:2 (sub 1), the 16 pixels (48 bytes) of one pixel row of its MCU, the
+ * sample X the average of pixels 2X, 2X+1 of the level-shifted chroma; for 4:2:0 (sub 2) the 16
+ * pixels of two pixel rows (96 bytes, k = 48 r + 3x + p), the sample the average of the 2 x 2
+ * quad.  The row transform is linear in the bytes:
+ *   R(u) = sum_{r, x < 16, p} b_{48r+3x+p} w a[c][p] cos((2 floor(x/2) + 1) u pi/16),
+ * w = 1/2 (4:2:2) or 1/4 (4:2:0), a = kMxA[c], c = Cb, Cr, b = the byte (the level-shifted
+ * chroma has no constant: no bias row), n = 8 c' + u (c' = 0 Cb, 1 Cr).  K = 32 MFMAs over
+ * k = 0..31, 32..63 [, 64..95].  Same encoding and split as k_mx: Bh a multiple of 2^-11 (acc_h
+ * exact in any order: every partial sum a multiple of 2^-11 below 2^13), the lo part(s) scaled
+ * by 2^12, each of acc_l's additions charged one ulp (65 per 4:2:2 chroma row, 97 per 4:2:0 one:
+ * 32 products per MFMA plus the accumulator).
  */
-static long double mx422_exact(int k, int n)
+static int mxc_nk(int sub) { return 48 * sub; }
+static int mxc_ksteps(int sub) { return sub == 1 ? 2 : 3; }
+
+static long double mxc_exact(int sub, int k, int n)
 {
-    if (n >= 16) return 0;
-    const int c = 1 + n / 8, u = n % 8;
+    if (n >= 16 || k >= mxc_nk(sub)) return 0;
+    const int c = 1 + n / 8, u = n % 8, kk = k % 48, x = kk / 3, p = kk % 3;
     const long double pi = 3.141592653589793238462643383279502884L;
-    if (k < 48) {
-        const int x = k / 3, p = k % 3;
-        return 0.5L * (long double)kMxA[c][p] * cosl((2 * (x / 2) + 1) * u * pi / 16);
-    }
-    return 0;                                   /* k = 48: no level-shift constant in chroma */
+    return (sub == 1 ? 0.5L : 0.25L) * (long double)kMxA[c][p] * cosl((2 * (x / 2) + 1) * u * pi / 16);
 }
 
-struct Mx422Split {
-    long double h[49][16], l[49][16], m[49][16];
-    uint16_t bh[49][16], bl[49][16], bm[49][16];
+struct MxcSplit {
+    long double h[96][16], l[96][16], m[96][16];
+    uint16_t bh[96][16], bl[96][16], bm[96][16];
 };
 
-static int mx422_split(Mx422Split &S)
+static int mxc_split(int sub, MxcSplit &S)
 {
     memset(&S, 0, sizeof S);
-    for (int k = 0; k < 49; k++)
+    const int nk = mxc_nk(sub);
+    for (int k = 0; k < nk; k++)
         for (int n = 0; n < 16; n++) {
-            const long double B = mx422_exact(k, n);
-            const bool bias = k == 48;
-            const long double hv = mx_enc(bias ? B : rintl(ldexpl(B, 11)) / 2048.0L, bias, &S.bh[k][n]);
+            const long double B = mxc_exact(sub, k, n);
+            const long double hv = mx_enc(rintl(ldexpl(B, 11)) / 2048.0L, false, &S.bh[k][n]);
             if (ldexpl(hv, 11) != rintl(ldexpl(hv, 11))) return JPGX_EARG;
             S.h[k][n] = hv;
-            const long double ls = mx_enc(ldexpl(B - hv, 12), bias, &S.bl[k][n]);
+            const long double ls = mx_enc(ldexpl(B - hv, 12), false, &S.bl[k][n]);
             S.l[k][n] = ldexpl(ls, -12);
             if (JX_MX_PARTS == 3) {
-                const long double ms = mx_enc(ldexpl(B - hv, 12) - ls, bias, &S.bm[k][n]);
+                const long double ms = mx_enc(ldexpl(B - hv, 12) - ls, false, &S.bm[k][n]);
                 S.m[k][n] = ldexpl(ms, -12);
             }
         }
     for (int n = 0; n < 16; n++) {              /* acc_h exactness: partial sums < 2^13 */
-        long double sh = fabsl(S.h[48][n]);
-        for (int k = 0; k < 48; k++) sh += 255.0L * fabsl(S.h[k][n]);
+        long double sh = 0;
+        for (int k = 0; k < nk; k++) sh += 255.0L * fabsl(S.h[k][n]);
         if (sh >= 8192.0L) return JPGX_EARG;
     }
     return JPGX_OK;
 }
 
 /* operand [part][which][lane][e]: which 0 / 1 = Y of set 0 / set 1 (K = 32: 24 bytes + bias),
- * 2 / 3 = chroma k = 0..31 / 32..63; lane l holds B[k = 8 (l >> 4) + e (+32)][column l & 15] */
-extern "C" int jx_mx422_operands(uint16_t ops[JX_MX_PARTS][4][64][8])
+ * 2.. = chroma k-steps (k = 32 (which - 2) + 8 (l >> 4) + e); lane l holds B[k][column l & 15] */
+static int mxc_operands(int sub, uint16_t (*ops)[5][64][8])
 {
     static MxSplit S;
-    static Mx422Split C;
+    static MxcSplit C;
     int rc = mx_split(S);
-    if (!rc) rc = mx422_split(C);
+    if (!rc) rc = mxc_split(sub, C);
     if (rc) return rc;
     for (int part = 0; part < JX_MX_PARTS; part++)
-        for (int which = 0; which < 4; which++)
+        for (int which = 0; which < 5; which++)
             for (int l = 0; l < 64; l++)
                 for (int e = 0; e < 8; e++) {
                     const int j = l & 15;
@@ -650,40 +651,51 @@ extern "C" int jx_mx422_operands(uint16_t ops[JX_MX_PARTS][4][64][8])
                         }
                     } else {
                         const int k = 32 * (which - 2) + 8 * (l >> 4) + e;
-                        if (k <= 48) v = part == 0 ? C.bh[k][j] : (part == 1 ? C.bl[k][j] : C.bm[k][j]);
+                        if (k < mxc_nk(sub)) v = part == 0 ? C.bh[k][j] : (part == 1 ? C.bl[k][j] : C.bm[k][j]);
                     }
                     ops[part][which][l][e] = v;
                 }
     return JPGX_OK;
 }
 
-/* Interval + error bound of a chroma row transform R (column n = 8 c' + u) */
-static Bnd mx422_row_bound(const Mx422Split &S, int n)
+extern "C" int jx_mx422_operands(uint16_t ops[JX_MX_PARTS][4][64][8])
 {
-    long double loh = S.h[48][n], hih = S.h[48][n];
-    long double lol = S.l[48][n] + S.m[48][n], hil = lol;
-    long double sl = fabsl(S.l[48][n]) + fabsl(S.m[48][n]);
-    long double rep = fabsl(mx422_exact(48, n) - S.h[48][n] - S.l[48][n] - S.m[48][n]);
-    for (int k = 0; k < 48; k++) {             /* bytes 0..255 */
+    static uint16_t o5[JX_MX_PARTS][5][64][8];
+    const int rc = mxc_operands(1, o5);
+    if (rc) return rc;
+    for (int part = 0; part < JX_MX_PARTS; part++) memcpy(ops[part], o5[part], sizeof ops[part]);
+    return JPGX_OK;
+}
+
+extern "C" int jx_mx420_operands(uint16_t ops[JX_MX_PARTS][5][64][8])
+{
+    return mxc_operands(2, ops);
+}
+
+/* Interval + error bound of a chroma row transform R (column n = 8 c' + u) */
+static Bnd mxc_row_bound(int sub, const MxcSplit &S, int n)
+{
+    long double loh = 0, hih = 0, lol = 0, hil = 0, sl = 0, rep = 0;
+    for (int k = 0; k < mxc_nk(sub); k++) {    /* bytes 0..255 */
         const long double bh = S.h[k][n], bo = S.l[k][n] + S.m[k][n];
         loh += std::min(0.0L, 255.0L * bh);
         hih += std::max(0.0L, 255.0L * bh);
         lol += std::min(0.0L, 255.0L * bo);
         hil += std::max(0.0L, 255.0L * bo);
         sl += 255.0L * (fabsl(S.l[k][n]) + fabsl(S.m[k][n]));
-        rep += 255.0L * fabsl(mx422_exact(k, n) - S.h[k][n] - S.l[k][n] - S.m[k][n]);
+        rep += 255.0L * fabsl(mxc_exact(sub, k, n) - S.h[k][n] - S.l[k][n] - S.m[k][n]);
     }
-    /* acc_l: per lo part two MFMAs of 32 products (49 weights, 15 zeros) plus the accumulator
-     * input, every addition charged one ulp of the magnitude bound, twice over (unknown
-     * summation tree and rounding mode) */
-    const double nadd = 2.0 * (65.0 * (JX_MX_PARTS - 1));
+    /* acc_l: per lo part mxc_ksteps MFMAs of 32 products plus the accumulator input, every
+     * addition charged one ulp of the magnitude bound, twice over (unknown summation tree and
+     * rounding mode) */
+    const double nadd = 2.0 * ((32.0 * mxc_ksteps(sub) + 1.0) * (JX_MX_PARTS - 1));
     const double el = (double)(nadd * sl * 0x1p-23L + rep);
     return BoundOps::add(Bnd{(double)loh, (double)hih, 0.0},
                          Bnd{(double)lol - el, (double)hil + el, el});
 }
 
-/* plan columns n = 8 c + u as jx_mxtab: c = 0 Y (k_mx's bound), 1 Cb, 2 Cr (4:2:2 rows) */
-extern "C" int jx_plan_tables_mx422(int quality, float w[24][8], float lim[24][8], int16_t q[2][64])
+/* plan columns n = 8 c + u as jx_mxtab: c = 0 Y (k_mx's bound), 1 Cb, 2 Cr (subsampled rows) */
+static int mxc_plan_tables(int sub, int quality, float w[24][8], float lim[24][8], int16_t q[2][64])
 {
     int qs[2][8][8];
     int rc = jpgx_scale_table(0, quality, qs[0]);
@@ -693,14 +705,14 @@ extern "C" int jx_plan_tables_mx422(int quality, float w[24][8], float lim[24][8
         for (int u = 0; u < 8; u++)
             for (int v = 0; v < 8; v++) q[t][u * 8 + v] = (int16_t)qs[t][u][v];
     static MxSplit S;
-    static Mx422Split C;
+    static MxcSplit C;
     rc = mx_split(S);
-    if (!rc) rc = mx422_split(C);
+    if (!rc) rc = mxc_split(sub, C);
     if (rc) return rc;
     const long double a0 = 1.0L / sqrtl(2.0L);
     for (int n = 0; n < 24; n++) {
         const int c = n / 8, u = n % 8, t = c == 0 ? 0 : 1;
-        const Bnd R = c == 0 ? mx_row_bound(S, n) : mx422_row_bound(C, n - 8);
+        const Bnd R = c == 0 ? mx_row_bound(S, n) : mxc_row_bound(sub, C, n - 8);
         Bnd col[8], out[8];
         for (int y = 0; y < 8; y++) col[y] = R;
         jx_fdct8<BoundOps>(col, out);
@@ -719,26 +731,37 @@ extern "C" int jx_plan_tables_mx422(int quality, float w[24][8], float lim[24][8
     return JPGX_OK;
 }
 
-/* Host emulation of k_mx422's chroma fast path (acc_h exact, acc_l in fp32, R = fl(acc_h +
- * 2^-12 acc_l), FOps column pass, quantiser) against the definition's exact quotient on random
- * 16 x 8 pixel pairs: unflagged mismatches (must be 0), flagged count, worst error / band. */
-extern "C" long long jx_selftest_mx422(long long nblocks, unsigned long long seed, int quality,
-                                       long long *flagged, double *ratio)
+extern "C" int jx_plan_tables_mx422(int quality, float w[24][8], float lim[24][8], int16_t q[2][64])
 {
-    static Mx422Split C;
-    if (mx422_split(C)) return -1;
+    return mxc_plan_tables(1, quality, w, lim, q);
+}
+
+extern "C" int jx_plan_tables_mx420(int quality, float w[24][8], float lim[24][8], int16_t q[2][64])
+{
+    return mxc_plan_tables(2, quality, w, lim, q);
+}
+
+/* Host emulation of the subsampled chroma fast path (acc_h exact, acc_l in fp32, R = fl(acc_h +
+ * 2^-12 acc_l), FOps column pass, quantiser) against the definition's exact quotient on random
+ * MCUs: unflagged mismatches (must be 0), flagged count, worst error / band. */
+static long long mxc_selftest(int sub, long long nblocks, unsigned long long seed, int quality,
+                              long long *flagged, double *ratio)
+{
+    static MxcSplit C;
+    if (mxc_split(sub, C)) return -1;
     float w[24][8], lim[24][8];
     int16_t q[2][64];
-    if (jx_plan_tables_mx422(quality, w, lim, q)) return -1;
+    if (mxc_plan_tables(sub, quality, w, lim, q)) return -1;
     const long double pi = 3.141592653589793238462643383279502884L;
     const long double a0 = 1.0L / sqrtl(2.0L);
+    const int nk = mxc_nk(sub);
     uint64_t s = seed;
     long long bad = 0, nfl = 0;
     double worst = 0;
     for (long long bk = 0; bk < nblocks; bk++) {
-        int px[8][48];
+        int px[8][96];                          /* chroma row y: [r][16 pixels][3] */
         for (int y = 0; y < 8; y++)
-            for (int k = 0; k < 48; k++) {
+            for (int k = 0; k < nk; k++) {
                 s = s * 6364136223846793005ULL + 1442695040888963407ULL;
                 px[y][k] = (int)(s >> 56);
                 if ((bk & 3) == 1) px[y][k] = px[0][k % 3];      /* flat blocks too */
@@ -748,9 +771,9 @@ extern "C" long long jx_selftest_mx422(long long nblocks, unsigned long long see
             const int c = 1 + n / 8, u = n % 8, pn = 8 + n;
             float R[8];
             for (int y = 0; y < 8; y++) {
-                long double ah = C.h[48][n];
-                float al = (float)(C.l[48][n] + C.m[48][n]);
-                for (int k = 0; k < 48; k++) {
+                long double ah = 0;
+                float al = 0.0f;
+                for (int k = 0; k < nk; k++) {
                     const int sv = px[y][k];
                     ah += sv * C.h[k][n];
                     al = al + (float)(sv * C.l[k][n]);
@@ -765,12 +788,14 @@ extern "C" long long jx_selftest_mx422(long long nblocks, unsigned long long see
                 for (int y = 0; y < 8; y++)
                     for (int X = 0; X < 8; X++) {
                         long double cs = 0;
-                        for (int h = 0; h < 2; h++) {
-                            const int x = 2 * X + h;
-                            cs += (long double)kMxA[c][0] * px[y][3 * x] + (long double)kMxA[c][1] * px[y][3 * x + 1] +
-                                  (long double)kMxA[c][2] * px[y][3 * x + 2];
-                        }
-                        sum += 0.5L * cs * cosl((2 * X + 1) * u * pi / 16) * cosl((2 * y + 1) * v * pi / 16);
+                        for (int r = 0; r < sub; r++)
+                            for (int h = 0; h < 2; h++) {
+                                const int x = 2 * X + h, o = 48 * r + 3 * x;
+                                cs += (long double)kMxA[c][0] * px[y][o] + (long double)kMxA[c][1] * px[y][o + 1] +
+                                      (long double)kMxA[c][2] * px[y][o + 2];
+                            }
+                        sum += (sub == 1 ? 0.5L : 0.25L) * cs * cosl((2 * X + 1) * u * pi / 16) *
+                               cosl((2 * y + 1) * v * pi / 16);
                     }
                 const long double au = u == 0 ? a0 : 1.0L, av = v == 0 ? a0 : 1.0L;
                 const long double qx = 0.25L * au * av * sum / q[1][u * 8 + v];
@@ -791,6 +816,18 @@ extern "C" long long jx_selftest_mx422(long long nblocks, unsigned long long see
     if (flagged) *flagged = nfl;
     if (ratio) *ratio = worst;
     return bad;
+}
+
+extern "C" long long jx_selftest_mx422(long long nblocks, unsigned long long seed, int quality,
+                                       long long *flagged, double *ratio)
+{
+    return mxc_selftest(1, nblocks, seed, quality, flagged, ratio);
+}
+
+extern "C" long long jx_selftest_mx420(long long nblocks, unsigned long long seed, int quality,
+                                       long long *flagged, double *ratio)
+{
+    return mxc_selftest(2, nblocks, seed, quality, flagged, ratio);
 }
 
 /* Host emulation of k_mx's fast path on random blocks (acc_h exact, acc_l summed in fp32,

@@ -201,6 +201,61 @@ def test_mx422_guard_band_holds_on_emulated_arithmetic(q):
     assert flagged.value < 600 * 128 // 100
 
 
+@pytest.mark.parametrize("q", [10, 50, 75, 90, 97])
+def test_mx420_guard_band_holds_on_emulated_arithmetic(q):
+    """k_mx420's chroma guard band (jx_plan_tables_mx420: 96-byte rows = two pixel rows of an
+    MCU, three K = 32 products per lo part) on the host emulation against the exact quad-averaged
+    definition: no unflagged coefficient rounds differently."""
+    import ctypes
+    f = jpgx.lib.jx_selftest_mx420
+    f.restype = ctypes.c_longlong
+    f.argtypes = [ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_int,
+                  ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
+    flagged, ratio = ctypes.c_longlong(), ctypes.c_double()
+    assert f(600, 53 + q, q, ctypes.byref(flagged), ctypes.byref(ratio)) == 0
+    assert ratio.value < 0.6
+    assert flagged.value < 600 * 128 // 100
+
+
+def test_mx420_operands_reconstruct_the_quad_matrix():
+    """k_mx420's B operands (jx_mx420_operands, [part][which][lane][e]): which 0 / 1 = k_mx422's Y
+    columns; which 2 / 3 / 4 = the chroma matrix over k = 0..95 (k = 48 r + 3x + p, r = the MCU
+    pixel row of the chroma row's pair): 0.25 a[c][p] cos((2 floor(x/2) + 1) u pi/16), stored x 2^15;
+    the hi part exact-accumulating."""
+    import ctypes
+    import math
+    parts_n = jpgx.lib.jx_mx_parts()
+    ops = np.zeros((parts_n, 5, 64, 8), np.uint16)
+    f = jpgx.lib.jx_mx420_operands
+    f.restype = ctypes.c_int
+    assert f(ops.ctypes.data_as(ctypes.c_void_p)) == 0
+    vals = ops.view(np.float16).astype(np.float64)
+    B = np.zeros((parts_n, 5, 32, 16))
+    for lane in range(64):
+        for e in range(8):
+            B[:, :, 8 * (lane >> 4) + e, lane & 15] = vals[:, :, lane, e]
+    ref422 = np.zeros((parts_n, 4, 64, 8), np.uint16)
+    g = jpgx.lib.jx_mx422_operands
+    g.restype = ctypes.c_int
+    assert g(ref422.ctypes.data_as(ctypes.c_void_p)) == 0
+    assert np.array_equal(ops[:, :2], ref422[:, :2])            # the same Y operands
+    C = np.concatenate([B[:, 2], B[:, 3], B[:, 4]], axis=1) * 2.0 ** -15   # [part][k 0..95][16]
+    hi, lo = C[0], C[1:].sum(axis=0) * 2.0 ** -12
+    assert np.all(hi * 2048 == np.round(hi * 2048))
+    assert np.all(255 * np.abs(hi).sum(axis=0) < 8192)
+    tol = 2 ** -30 if parts_n == 3 else 2 ** -23
+    a = [(-0.168736, 0.331264, -0.5), (0.5, -0.418688, -0.081312)]
+    for c in range(2):
+        for u in range(8):
+            n = 8 * c + u
+            for r in range(2):
+                for x in range(16):
+                    for p in range(3):
+                        k = 48 * r + 3 * x + p
+                        want = 0.25 * a[c][p] * math.cos((2 * (x // 2) + 1) * u * math.pi / 16)
+                        assert abs(hi[k, n] + lo[k, n] - want) < tol
+
+
 def test_mx422_operands_reconstruct_the_pair_matrix():
     """k_mx422's B operands (jx_mx422_operands, [part][which][lane][e]): which 0 / 1 = k_mx's Y
     columns for set 0 (C columns 0..7) / set 1 (8..15), K = 25 used; which 2 / 3 = the chroma

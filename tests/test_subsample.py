@@ -77,7 +77,7 @@ def _dev(a, cuda):
 
 @pytest.fixture(params=["fused", "two-pass"])
 def impl(request, monkeypatch):
-    """True 4:2:2 / 4:2:0 run as k_mx422 / k_sub420 (one pass: the product library) or as
+    """True 4:2:2 / 4:2:0 run as k_mx422 / k_mx420 (one pass: the product library) or as
     k_xform's Y + k_chroma<1> / <2> (the test-only cross-check library libjpgx_alt.so)."""
     if request.param == "two-pass":
         monkeypatch.setattr(jpgx, "lib", jpgx.alt_library())
@@ -239,6 +239,37 @@ def test_gpu_sub422_small_rows(cuda, impl, W, H, F, kind):
     for f in range(F):
         want = np.concatenate([O.blocks(frames[f], q, 1)[0],
                                O.chroma_sub(frames[f], q, 1).reshape(-1, 64)])
+        bad = np.argwhere(got[f * per * 64:(f + 1) * per * 64].reshape(per, 64) != want)
+        assert len(bad) == 0, f"frame {f}: {len(bad)} mismatches, first {bad[:4].tolist()}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,F", [(16, 16, 3), (48, 32, 3), (80, 16, 5), (144, 48, 1), (400, 32, 2)])
+@pytest.mark.parametrize("kind", ["random", "tie", "exact"])
+def test_gpu_sub420_small_rows(cuda, impl, W, H, F, kind):
+    """MCU rows of 1, 3, 5, 9 and 25 MCUs: every MCU or many of them the row's last (x0 = -8
+    quirk in both block rows of its right column), steps and step pairs across MCU rows and
+    frames, an odd MCU count (a pair whose second step lies past the end); tie frames flag
+    chroma coefficients (deferred exact pass from global memory), FORCE_EXACT sends every
+    coefficient through the inline pass; a sentinel region after the output must stay intact."""
+    import torch
+    q = 50 if kind == "tie" else 85
+    frames = [O.gen_tie(W, H) if kind == "tie" else O.gen_splitmix(700 + W + f, W, H)
+              for f in range(F)]
+    S = jpgx.FLAG_SUBSAMPLE
+    flags = S | (jpgx.FLAG_FORCE_EXACT if kind == "exact" else 0)
+    nb = (H // 8) * (W // 8)
+    per = nb + 2 * jpgx.chroma_blocks(W, 0, H // 8, 2, S)
+    guard = 2048
+    buf = torch.full((F * per * 64 + guard,), 0x7A7A, dtype=torch.int16, device=cuda)
+    fr = jpgx.frames(W, H, nframes=F, out_frame_stride=per * 64)
+    jpgx.blocks_gpu(fr, jpgx.default_params(W, H, q, 2, flags=flags), _dev(np.stack(frames), cuda),
+                    buf, 0)
+    got = buf.cpu().numpy()
+    assert (got[F * per * 64:] == 0x7A7A).all(), "write past the end of the output"
+    for f in range(F):
+        want = np.concatenate([O.blocks(frames[f], q, 2)[0],
+                               O.chroma_sub(frames[f], q, 2).reshape(-1, 64)])
         bad = np.argwhere(got[f * per * 64:(f + 1) * per * 64].reshape(per, 64) != want)
         assert len(bad) == 0, f"frame {f}: {len(bad)} mismatches, first {bad[:4].tolist()}"
 
