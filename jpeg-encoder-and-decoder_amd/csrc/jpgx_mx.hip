@@ -97,7 +97,7 @@ struct alignas(16) MxLds {          /* 16-byte aligned: every wave's DMA slots a
     uint8_t stage[kStageBytes];
     uint8_t pix[kSidePix][192];         /* deferred blocks' pixel rows, [y][24]              */
     uint32_t sblk[kSidePix];            /* and their launch-global block indices             */
-    uint16_t dtask[kSide];              /* deferred tasks: slot << 8 | c << 6 | v << 3 | u   */
+    uint16_t dtask[kSide];              /* deferred columns: slot << 13 | c << 11 | u << 8 | v-mask */
     uint16_t task[8];                   /* inline batch: source lane << 8 | column << 3 | v  */
     uint32_t dummy[64];                 /* landing area of padding DMA operations            */
 };
@@ -448,8 +448,9 @@ __device__ __forceinline__ void mx_exact_inline(MxLds &L, const uint8_t *slot, u
     }
 }
 
-/* Deferred exact pass: the queued tasks (pixels in L.pix), results straight to global memory
- * once the wave's earlier stores have landed. */
+/* Deferred exact pass: up to kSide queued columns (pixels in L.pix), one per 8-lane group, each
+ * group walking its column's flagged v's; results straight to global memory once the wave's
+ * earlier stores (of those blocks) have landed. */
 __device__ __forceinline__ void mx_flush(MxLds &L, int &nq, int &ns, const MxG &g, const jx_mxtab &T)
 {
     __builtin_amdgcn_s_waitcnt(0xF70);                 /* vmcnt(0): the tasks' blocks are stored */
@@ -457,20 +458,26 @@ __device__ __forceinline__ void mx_flush(MxLds &L, int &nq, int &ns, const MxG &
     const unsigned lane = mx_lane(), i = lane >> 3, x = lane & 7u;
     const bool live = (int)i < nq;
     const unsigned code = L.dtask[live ? i : 0u];
-    const unsigned slot = code >> 8, ch = (code >> 6) & 3u, v = (code >> 3) & 7u, u = code & 7u;
-    const int val = mx_exact_coef(mx_lds(L.pix[slot]), 24u, ch, u, v, x, T);
-    if (live && x == 7) {
-        const unsigned b = L.sblk[slot], f = b / g.nb, bi = b - f * g.nb;
-        g.out[(long long)f * g.ofstride + ((long long)ch * g.nb + bi) * 64 + kMxScan[v][u]] = (int16_t)val;
+    const unsigned slot = code >> 13, ch = (code >> 11) & 3u, u = (code >> 8) & 7u;
+    uint32_t vb = live ? (code & 0xffu) : 0u;
+    const unsigned b = L.sblk[slot], f = b / g.nb, bi = b - f * g.nb;
+    int16_t *const dst = g.out + (long long)f * g.ofstride + ((long long)ch * g.nb + bi) * 64;
+    while (__ballot(vb != 0)) {
+        const bool act = vb != 0;
+        const unsigned v = act ? (unsigned)__builtin_ctz(vb) : 0u;
+        vb &= vb - 1u;
+        const int val = mx_exact_coef(mx_lds(L.pix[slot]), 24u, ch, u, v, x, T);
+        if (act && x == 7) dst[kMxScan[v][u]] = (int16_t)val;
     }
     mx_wave_sync();
     nq = 0;
     ns = 0;
 }
 
-/* A step with flagged coefficients (bit 8 col + v of `bits`): queue them with their blocks'
- * pixels (flushing the queue first if it would overflow); a step with more tasks than the queue
- * holds is done inline. */
+/* A step with flagged coefficients (bit 8 col + v of `bits`): queue each flagged column (its
+ * v-mask) with its block's pixels, flushing the queue first if it would overflow; a step with more
+ * flagged columns or blocks than the queue holds is done inline.  Queue positions come from the
+ * three column ballots (mbcnt), no prefix sum. */
 __device__ __forceinline__ void mx_defer(MxLds &L, const uint8_t *sp, uint32_t bits, unsigned b0,
                                          int &nq, int &ns, const MxG &g, const jx_mxtab &T)
 {
@@ -484,7 +491,7 @@ __device__ __forceinline__ void mx_defer(MxLds &L, const uint8_t *sp, uint32_t b
         for (int k = 0; k < 3; k++)
             if (mx_col_block((unsigned)k, lane) >= nvalid) bits &= ~(0xffu << (8 * k));
     }
-    /* flagged blocks of the step, and the task count */
+    /* flagged columns (per column kind) and blocks of the step */
     const uint64_t m0 = __ballot((bits & 0xffu) != 0), m1 = __ballot((bits & 0xff00u) != 0),
                    m2 = __ballot((bits & 0xff0000u) != 0);
     uint32_t blk = 0;
@@ -495,18 +502,11 @@ __device__ __forceinline__ void mx_defer(MxLds &L, const uint8_t *sp, uint32_t b
         blk |= (((m2 >> (16 * gq)) & 0xffu) ? 1u : 0u) << gq;
         blk |= (((m2 >> (16 * gq + 8)) & 0xffu) ? 1u : 0u) << (4 + gq);
     }
-    const unsigned cnt = (unsigned)__popc(bits);
-    unsigned incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const unsigned o = __shfl_up(incl, d, 64);
-        if ((int)lane >= d) incl += o;
-    }
-    const int ntask = (int)__builtin_amdgcn_readlane(incl, 63);
+    const int n0 = __popcll(m0), n1 = __popcll(m1), ncol = n0 + n1 + __popcll(m2);
     const int nblk = __popc(blk);
-    if (nq + ntask > kSide || ns + nblk > kSidePix) {
+    if (nq + ncol > kSide || ns + nblk > kSidePix) {
         if (nq) mx_flush(L, nq, ns, g, T);
-        if (ntask > kSide || nblk > kSidePix) {
+        if (ncol > kSide || nblk > kSidePix) {
             mx_exact_inline(L, sp, bits, T);
             return;
         }
@@ -527,21 +527,23 @@ __device__ __forceinline__ void mx_defer(MxLds &L, const uint8_t *sp, uint32_t b
             t++;
         }
     }
-    /* this lane's tasks at queue positions nq + (exclusive prefix) */
+    /* this lane's flagged columns: kind-0 columns first, then kind 1, then Cr */
     {
-        unsigned pos = (unsigned)nq + incl - cnt;
         const unsigned jj = lane & 15u, u = jj & 7u;
-        while (bits) {
-            const unsigned b = (unsigned)__builtin_ctz(bits);
-            bits &= bits - 1u;
-            const unsigned k = b >> 3, v = b & 7u, ch = k < 2 ? (jj >> 3) : 2u;
-            const unsigned jb = mx_col_block(k, lane);
-            const unsigned slot = (unsigned)ns + (unsigned)__popc(blk & ((1u << jb) - 1u));
-            L.dtask[pos++] = (uint16_t)(slot << 8 | ch << 6 | v << 3 | u);
+        const int base[3] = {nq, nq + n0, nq + n0 + n1};
+        const uint64_t mk[3] = {m0, m1, m2};
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const uint32_t vb = (bits >> (8 * k)) & 0xffu;
+            if (vb) {
+                const unsigned jb = mx_col_block((unsigned)k, lane), ch = k < 2 ? (jj >> 3) : 2u;
+                const unsigned slot = (unsigned)ns + (unsigned)__popc(blk & ((1u << jb) - 1u));
+                L.dtask[base[k] + mx_rank(mk[k])] = (uint16_t)(slot << 13 | ch << 11 | u << 8 | vb);
+            }
         }
     }
     mx_wave_sync();
-    nq += ntask;
+    nq += ncol;
     ns += nblk;
 }
 
@@ -572,30 +574,44 @@ __device__ __forceinline__ void mx_combine(mx_f4 hl, mx_f4 ll, mx_f4 hh, mx_f4 l
     R[3] = __builtin_elementwise_fma(mx_f2{lh.z, lh.w}, s, mx_f2{hh.z, hh.w});
 }
 
-/* a column's scales and band limits from the workgroup table (W pairs then L pairs) */
-struct MxWL {
-    mx_f4 w01, w23, l01, l23;
+/* a column's scales from the workgroup table; t0 = 0 (k_mx: Y|Cb, k_mx422/420: Y) or 2 (k_mx: Cr,
+ * k_mx422/420: chroma); its squared band limits are table t0 + 1 */
+struct MxW {
+    mx_f4 w01, w23;
 };
-/* t0 = 0 (k_mx: Y|Cb, k_mx422: Y) or 2 (k_mx: Cr, k_mx422: chroma) */
-__device__ __forceinline__ MxWL mx_wl(const MxTab &tb, unsigned t0, unsigned j)
+__device__ __forceinline__ MxW mx_w(const MxTab &tb, unsigned t0, unsigned j)
 {
-    return MxWL{tb.wl[t0][0][j], tb.wl[t0][1][j], tb.wl[t0 + 1][0][j], tb.wl[t0 + 1][1][j]};
+    return MxW{tb.wl[t0][0][j], tb.wl[t0][1][j]};
+}
+
+/*
+ * One limit per lane and column kind for the hot path's band test: a float <= the square root
+ * of the smallest of the column's eight squared limits (-1 with FORCE_EXACT: every column takes
+ * the rare path).  |d| >= limc is implied by d * d - lsq >= 0 for each of the eight, so testing
+ * max |d| >= limc first and the per-coefficient limits only when it fires (mx_flags) flags
+ * exactly the same coefficients with two fewer instructions per coefficient pair.
+ */
+__device__ __forceinline__ float mx_limc(const MxTab &tb, unsigned t, unsigned j)
+{
+    const mx_f4 a = tb.wl[t][0][j], b = tb.wl[t][1][j];
+    const float mn = fminf(fminf(fminf(a.x, a.y), fminf(a.z, a.w)), fminf(fminf(b.x, b.y), fminf(b.z, b.w)));
+    if (!(mn >= 0.0f)) return -1.0f;
+    return (float)sqrt((double)mn) * (1.0f - 0x1p-20f);
 }
 
 /* Column pass of one column (R pairs), quantiser, stage writes at za[v] + OFF, band flags (rare
- * path) into fl */
+ * path: the exact per-coefficient test with the limits of table t0 + 1) into fl */
 template <unsigned OFF>
-__device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxWL &t, const uint32_t (&za)[8],
-                                             uint32_t &fl, int kc)
+__device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, float limc, const MxTab &tb,
+                                             unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc)
 {
     mx_f2 F[4];
     jx_fdct8_pk<MxPair>(R, F);
-    const mx_f4 w01 = t.w01, w23 = t.w23, l01 = t.l01, l23 = t.l23;
+    const mx_f4 w01 = t.w01, w23 = t.w23;
     const mx_f2 W[4] = {mx_f2{w01.x, w01.y}, mx_f2{w01.z, w01.w}, mx_f2{w23.x, w23.y}, mx_f2{w23.z, w23.w}};
-    const mx_f2 Lq[4] = {mx_f2{l01.x, l01.y}, mx_f2{l01.z, l01.w}, mx_f2{l23.x, l23.y}, mx_f2{l23.z, l23.w}};
     const mx_f2 M2 = {kMagic, kMagic};
     typedef __attribute__((address_space(3))) uint16_t l16;
-    float em = -1.0f;
+    float em = 0.0f;
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
@@ -603,20 +619,23 @@ __device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxWL &t, 
         *(l16 *)(uintptr_t)(za[jx_pk_k(p, 1)] + OFF) = (uint16_t)__float_as_uint(tm.y);
         const mx_f2 rr = tm - M2;
         const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
-        const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
-        em = __builtin_fmaxf(__builtin_fmaxf(em, e.x), e.y);
+        em = __builtin_fmaxf(__builtin_fmaxf(em, __builtin_fabsf(d.x)), __builtin_fabsf(d.y));
     }
-    if (__builtin_expect(__ballot(em >= 0.0f) != 0, 0)) fl |= mx_flags(F, W, Lq) << (8 * kc);
+    if (__builtin_expect(__ballot(em >= limc) != 0, 0)) {
+        const mx_f4 l01 = tb.wl[t0 + 1][0][j], l23 = tb.wl[t0 + 1][1][j];
+        const mx_f2 Lq[4] = {mx_f2{l01.x, l01.y}, mx_f2{l01.z, l01.w}, mx_f2{l23.x, l23.y}, mx_f2{l23.z, l23.w}};
+        fl |= mx_flags(F, W, Lq) << (8 * kc);
+    }
 }
 
 /* the same from the hi / lo accumulator tiles of rows 0..3 and 4..7 */
 template <unsigned OFF>
-__device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxWL &t, const uint32_t (&za)[8],
-                                             uint32_t &fl, int kc)
+__device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t, float limc, const MxTab &tb,
+                                             unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc)
 {
     mx_f2 R[4];
     mx_combine(acc[0], acc[1], acc[2], acc[3], R);
-    mx_column_r<OFF>(R, t, za, fl, kc);
+    mx_column_r<OFF>(R, t, limc, tb, t0, j, za, fl, kc);
 }
 
 __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
@@ -660,6 +679,8 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         s_tab.wl[t][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
     }
     __syncthreads();
+    /* hot-path band limits of this lane's two column kinds (mx_limc) */
+    const float limc0 = mx_limc(s_tab, 1, threadIdx.x & 15u), limc2 = mx_limc(s_tab, 3, threadIdx.x & 15u);
     const unsigned nw = gridDim.x * 4u;
     const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (kCB * wv >= g.total) return;
@@ -779,7 +800,8 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         __builtin_amdgcn_sched_barrier(0);
         mma_set(acc[1], A10, A11);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0>(acc[0], mx_wl(s_tab, 0, j), za, fl, 0);
+        const MxW w0 = mx_w(s_tab, 0, j);
+        mx_column_t<0>(acc[0], w0, limc0, s_tab, 0, j, za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
         acc[2][0] = mx_mma(A00, B[0][1], z);
         acc[2][2] = mx_mma(A01, B[0][1], z);
@@ -803,9 +825,9 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             acc[2][3] = mx_mma(A11, B[kParts - 1][2], acc[2][3]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<4 * kBS>(acc[1], mx_wl(s_tab, 0, j), za, fl, 1);
+        mx_column_t<4 * kBS>(acc[1], w0, limc0, s_tab, 0, j, za, fl, 1);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<8 * kBS>(acc[2], mx_wl(s_tab, 2, j), za, fl, 2);
+        mx_column_t<8 * kBS>(acc[2], mx_w(s_tab, 2, j), limc2, s_tab, 2, j, za, fl, 2);
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
             mx_defer(L, sp, fl, b0, nq, ns, g, T);
@@ -1183,6 +1205,8 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
         s_tab.wl[t][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
     }
     __syncthreads();
+    /* hot-path band limits of this lane's two column kinds (mx_limc) */
+    const float limc0 = mx_limc(s_tab, 1, threadIdx.x & 15u), limc2 = mx_limc(s_tab, 3, threadIdx.x & 15u);
     const unsigned nw = gridDim.x * 4u;
     const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (kCB422 * wv >= g.total) return;
@@ -1323,9 +1347,9 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
         mma2(acc[1], mx_aop(c00, kSelLo, kSelHi, kSelLo), mx_aop(c01, kSelLo, kSelHi, kSelLo),
              mx_aop(c10, t0, t1, t2), mx_aop(c11, t0, t1, t2), 2);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0>(acc[0], mx_wl(s_tab, 0, j), za, fl, 0);
+        mx_column_t<0>(acc[0], mx_w(s_tab, 0, j), limc0, s_tab, 0, j, za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<kSt422C>(acc[1], mx_wl(s_tab, 2, j), za, fl, 1);
+        mx_column_t<kSt422C>(acc[1], mx_w(s_tab, 2, j), limc2, s_tab, 2, j, za, fl, 1);
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx422_defer_step(L, sp, qmask, fl, b0, nq, ns, g, T);
         /* always two store instructions per step (the vmcnt accounting counts on it) */
@@ -1761,6 +1785,8 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
         s_tab.wl[t][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
     }
     __syncthreads();
+    /* hot-path band limits of this lane's two column kinds (mx_limc) */
+    const float limc0 = mx_limc(s_tab, 1, threadIdx.x & 15u), limc2 = mx_limc(s_tab, 3, threadIdx.x & 15u);
     const unsigned nw = gridDim.x * 4u;
     const unsigned wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (kCM420 * wv >= h.tm) return;
@@ -1902,7 +1928,7 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0>(accY, mx_wl(s_tab, 0, j), za, fl, 0);
+        mx_column_t<0>(accY, mx_w(s_tab, 0, j), limc0, s_tab, 0, j, za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
         const mx_f4 s12 = {0x1p-12f, 0x1p-12f, 0x1p-12f, 0x1p-12f};
         const mx_f4 rc4 = __builtin_elementwise_fma(accC[1], s12, accC[0]);
@@ -1923,7 +1949,7 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
             R[1] = mx_f2{lo4[2], lo4[3]};
             R[2] = mx_f2{hi4[0], hi4[1]};
             R[3] = mx_f2{hi4[2], hi4[3]};
-            mx_column_r<kSt420C>(R, mx_wl(s_tab, 2, j), za, fl, 1);
+            mx_column_r<kSt420C>(R, mx_w(s_tab, 2, j), limc2, s_tab, 2, j, za, fl, 1);
         } else {
             rA = rc4;
         }
