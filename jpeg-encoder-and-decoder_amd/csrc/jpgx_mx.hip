@@ -599,11 +599,31 @@ __device__ __forceinline__ float mx_limc(const MxTab &tb, unsigned t, unsigned j
     return (float)sqrt((double)mn) * (1.0f - 0x1p-20f);
 }
 
+/*
+ * MFMA operand rule (tools/mfma_war_check.py, run by the CPU tests on the built ISA): no load may
+ * write a VGPR that an issued MFMA may still read.  The register allocator treats an MFMA's
+ * operands as dead once the MFMA is issued -- for a chained product whose destination differs
+ * from its SrcC, the SrcC registers -- and may hand them to an LDS read a few instructions later,
+ * whose data can land before the MFMA has read its last 16-lane group (C rows 12..15) when the
+ * matrix pipe is backed up: nondeterministic wrong rows 12..15 (profiles/r03_mfma_war.txt).  So
+ * every LDS read of a step (A operands, scale tables) is issued before the step's first MFMA,
+ * behind a scheduling barrier; a load that must follow an MFMA (a rare-path limit read) first
+ * waits for the newest MFMA's result (mx_fence: a VALU read of it, which the compiler's wait
+ * states hold until the MFMA is done -- and with it every older one of this wave).
+ */
+__device__ __forceinline__ void mx_fence(const mx_f4 &r)
+{
+    const uint32_t v = __builtin_amdgcn_readfirstlane(__float_as_uint(r.w));
+    asm volatile("" ::"s"(v) : "memory");
+}
+
 /* Column pass of one column (R pairs), quantiser, stage writes at za[v] + OFF, band flags (rare
- * path: the exact per-coefficient test with the limits of table t0 + 1) into fl */
+ * path: the exact per-coefficient test with the limits of table t0 + 1, after mx_fence(*fence)
+ * when an MFMA may be in flight) into fl */
 template <unsigned OFF>
 __device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, float limc, const MxTab &tb,
-                                             unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc)
+                                             unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc,
+                                             const mx_f4 *fence = nullptr)
 {
     mx_f2 F[4];
     jx_fdct8_pk<MxPair>(R, F);
@@ -622,20 +642,28 @@ __device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, f
         em = __builtin_fmaxf(__builtin_fmaxf(em, __builtin_fabsf(d.x)), __builtin_fabsf(d.y));
     }
     if (__builtin_expect(__ballot(em >= limc) != 0, 0)) {
+        if (fence) mx_fence(*fence);
         const mx_f4 l01 = tb.wl[t0 + 1][0][j], l23 = tb.wl[t0 + 1][1][j];
         const mx_f2 Lq[4] = {mx_f2{l01.x, l01.y}, mx_f2{l01.z, l01.w}, mx_f2{l23.x, l23.y}, mx_f2{l23.z, l23.w}};
         fl |= mx_flags(F, W, Lq) << (8 * kc);
     }
 }
 
-/* the same from the hi / lo accumulator tiles of rows 0..3 and 4..7 */
-template <unsigned OFF>
+/* the same from the hi / lo accumulator tiles of rows 0..3 and 4..7; LAZY: the column's scales
+ * are read here, after the tiles (the step's last MFMAs) have been read -- no MFMA in flight */
+template <unsigned OFF, bool LAZY = false>
 __device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t, float limc, const MxTab &tb,
-                                             unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc)
+                                             unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc,
+                                             const mx_f4 *fence = nullptr)
 {
     mx_f2 R[4];
     mx_combine(acc[0], acc[1], acc[2], acc[3], R);
-    mx_column_r<OFF>(R, t, limc, tb, t0, j, za, fl, kc);
+    if (LAZY) {
+        __builtin_amdgcn_sched_barrier(0);
+        mx_column_r<OFF>(R, mx_w(tb, t0, j), limc, tb, t0, j, za, fl, kc, fence);
+    } else {
+        mx_column_r<OFF>(R, t, limc, tb, t0, j, za, fl, kc, fence);
+    }
 }
 
 __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
@@ -772,8 +800,11 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         const mx_u2 d01 = *(const mx_u2 *)(sp + aoff + 768u);
         const mx_u2 d10 = *(const mx_u2 *)(sp + aoff + 96u);
         const mx_u2 d11 = *(const mx_u2 *)(sp + aoff + 864u);
+        /* the step's scale reads too, before any MFMA (MFMA operand rule, mx_fence) */
+        const MxW w0 = mx_w(s_tab, 0, j);
         const mx_h8 A00 = mx_aop(d00, s0, s1, s2), A01 = mx_aop(d01, s0, s1, s2);
         const mx_h8 A10 = mx_aop(d10, s0, s1, s2), A11 = mx_aop(d11, s0, s1, s2);
+        __builtin_amdgcn_sched_barrier(0);
         const mx_f4 z = {};
         uint32_t fl = 0;                               /* bit 8 col + v: flagged (rare) */
         /* MFMAs one column ahead of the VALU work: MFMA(c0), MFMA(c1), VALU(c0), MFMA(c2),
@@ -800,7 +831,6 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         __builtin_amdgcn_sched_barrier(0);
         mma_set(acc[1], A10, A11);
         __builtin_amdgcn_sched_barrier(0);
-        const MxW w0 = mx_w(s_tab, 0, j);
         mx_column_t<0>(acc[0], w0, limc0, s_tab, 0, j, za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
         acc[2][0] = mx_mma(A00, B[0][1], z);
@@ -825,9 +855,9 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
             acc[2][3] = mx_mma(A11, B[kParts - 1][2], acc[2][3]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<4 * kBS>(acc[1], w0, limc0, s_tab, 0, j, za, fl, 1);
+        mx_column_t<4 * kBS>(acc[1], w0, limc0, s_tab, 0, j, za, fl, 1, &acc[2][3]);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<8 * kBS>(acc[2], mx_w(s_tab, 2, j), limc2, s_tab, 2, j, za, fl, 2);
+        mx_column_t<8 * kBS, true>(acc[2], w0, limc2, s_tab, 2, j, za, fl, 2);
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
             mx_defer(L, sp, fl, b0, nq, ns, g, T);
@@ -917,7 +947,7 @@ struct alignas(16) Mx422Lds {
     uint8_t pix[kSide][192];            /* deferred blocks: Y [y][24] in one slot, an MCU [y][48]
                                            in two                                                */
     uint32_t sblk[kSide];               /* launch-global Y block (an MCU: its left block)        */
-    uint16_t dtask[kSide];              /* slot << 8 | ch << 6 | v << 3 | u                      */
+    uint16_t dtask[kSide];              /* a flagged column: slot << 13 | ch << 11 | u << 8 | v-mask */
     uint16_t task[8];
     uint32_t dummy[64];
 };
@@ -1017,14 +1047,19 @@ __device__ __forceinline__ void mx422_flush(Mx422Lds &L, int &nq, int &ns, const
     const unsigned lane = mx_lane(), i = lane >> 3, x = lane & 7u;
     const bool live = (int)i < nq;
     const unsigned code = L.dtask[live ? i : 0u];
-    const unsigned slot = code >> 8, ch = (code >> 6) & 3u, v = (code >> 3) & 7u, u = code & 7u;
+    const unsigned slot = code >> 13, ch = (code >> 11) & 3u, u = (code >> 8) & 7u;
+    uint32_t vb = live ? (code & 0xffu) : 0u;
     const lds_u8 *px = mx_lds(L.pix[slot]);
-    const int val = ch == 0 ? mx_exact_pair(px + 3u * x, 24u, 0u, 0u, u, v, x, T)
-                            : mx_exact_pair(px + 6u * x, 48u, 3u, ch, u, v, x, T);
-    if (live && x == 7) {
-        const unsigned b = L.sblk[slot], f = b / g.nb, bi = b - f * g.nb;
-        const long long blk = ch == 0 ? (long long)bi : (long long)g.nb + (ch - 1u) * (g.nb / 2u) + bi / 2u;
-        g.out[(long long)f * g.ofstride + blk * 64 + kMxScan[v][u]] = (int16_t)val;
+    const unsigned b = L.sblk[slot], f = b / g.nb, bi = b - f * g.nb;
+    const long long blk = ch == 0 ? (long long)bi : (long long)g.nb + (ch - 1u) * (g.nb / 2u) + bi / 2u;
+    int16_t *const dst = g.out + (long long)f * g.ofstride + blk * 64;
+    while (__ballot(vb != 0)) {
+        const bool act = vb != 0;
+        const unsigned v = act ? (unsigned)__builtin_ctz(vb) : 0u;
+        vb &= vb - 1u;
+        const int val = ch == 0 ? mx_exact_pair(px + 3u * x, 24u, 0u, 0u, u, v, x, T)
+                                : mx_exact_pair(px + 6u * x, 48u, 3u, ch, u, v, x, T);
+        if (act && x == 7) dst[kMxScan[v][u]] = (int16_t)val;
     }
     mx_wave_sync();
     nq = 0;
@@ -1051,18 +1086,11 @@ __device__ __forceinline__ void mx422_defer(Mx422Lds &L, const uint8_t *sp, uint
         yblk |= (((m0 >> (16 * gq + 8)) & 0xffu) ? 1u : 0u) << (4 + gq);
         cblk |= (((m1 >> (16 * gq)) & 0xffffu) ? 1u : 0u) << gq;
     }
-    const unsigned cnt = (unsigned)__popc(bits);
-    unsigned incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const unsigned o = __shfl_up(incl, d, 64);
-        if ((int)lane >= d) incl += o;
-    }
-    const int ntask = (int)__builtin_amdgcn_readlane(incl, 63);
+    const int n0 = __popcll(m0), ncol = n0 + __popcll(m1);
     const int ny = __popc(yblk), nslot = ny + 2 * __popc(cblk);
-    if (nq + ntask > kSide || ns + nslot > kSide) {
+    if (nq + ncol > kSide || ns + nslot > kSide) {
         if (nq) mx422_flush(L, nq, ns, g, T);
-        if (ntask > kSide || nslot > kSide) {
+        if (ncol > kSide || nslot > kSide) {
             mx422_exact_inline(L, sp, qmask, bits, T);
             return;
         }
@@ -1097,28 +1125,22 @@ __device__ __forceinline__ void mx422_defer(Mx422Lds &L, const uint8_t *sp, uint
             t += 2;
         }
     }
-    {
-        unsigned pos = (unsigned)nq + incl - cnt;
+    {   /* this lane's flagged columns (Y first, then chroma), one queue entry each */
         const unsigned jj = lane & 15u, u = jj & 7u;
-        while (bits) {
-            const unsigned b = (unsigned)__builtin_ctz(bits);
-            bits &= bits - 1u;
-            const unsigned v = b & 7u;
-            unsigned slot, ch;
-            if (b < 8) {
-                const unsigned jb = mx422_yblock(lane);
-                slot = (unsigned)ns + (unsigned)__popc(yblk & ((1u << jb) - 1u));
-                ch = 0;
-            } else {
-                const unsigned cb = lane >> 4;
-                slot = (unsigned)(ns + ny) + 2u * (unsigned)__popc(cblk & ((1u << cb) - 1u));
-                ch = 1u + (jj >> 3);
-            }
-            L.dtask[pos++] = (uint16_t)(slot << 8 | ch << 6 | v << 3 | u);
+        const uint32_t vy = bits & 0xffu, vc = (bits >> 8) & 0xffu;
+        if (vy) {
+            const unsigned jb = mx422_yblock(lane);
+            const unsigned slot = (unsigned)ns + (unsigned)__popc(yblk & ((1u << jb) - 1u));
+            L.dtask[nq + mx_rank(m0)] = (uint16_t)(slot << 13 | u << 8 | vy);
+        }
+        if (vc) {
+            const unsigned cb = lane >> 4;
+            const unsigned slot = (unsigned)(ns + ny) + 2u * (unsigned)__popc(cblk & ((1u << cb) - 1u));
+            L.dtask[nq + n0 + mx_rank(m1)] = (uint16_t)(slot << 13 | (1u + (jj >> 3)) << 11 | u << 8 | vc);
         }
     }
     mx_wave_sync();
-    nq += ntask;
+    nq += ncol;
     ns += nslot;
 }
 
@@ -1313,8 +1335,8 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
                 o[3] = mx_mma(Ah1, B[kParts - 1][w0 + 1], o[3]);
             }
         };
-        /* every LDS read of the step is issued ahead of the work that waits for it: the A
-         * operands first, a column's scales / limits one phase before the column */
+        /* every LDS read of the step -- A operands and the two columns' scales -- is issued before
+         * the step's first MFMA (MFMA operand rule, mx_fence) */
         const mx_u2 y00 = *(const mx_u2 *)(sp + aoff);
         const mx_u2 y01 = *(const mx_u2 *)(sp + aoff + 768u);
         const mx_u2 y10 = *(const mx_u2 *)(sp + aoff + 96u);
@@ -1341,15 +1363,17 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
                 c11 = *(const mx_u2 *)(p1 + h1);
             }
         }
+        const MxW wy = mx_w(s_tab, 0, j);
+        __builtin_amdgcn_sched_barrier(0);
         mma2(acc[0], mx_aop(y00, s0, s1, s2), mx_aop(y01, s0, s1, s2), mx_aop(y10, s0, s1, s2),
              mx_aop(y11, s0, s1, s2), 0);
         __builtin_amdgcn_sched_barrier(0);
         mma2(acc[1], mx_aop(c00, kSelLo, kSelHi, kSelLo), mx_aop(c01, kSelLo, kSelHi, kSelLo),
              mx_aop(c10, t0, t1, t2), mx_aop(c11, t0, t1, t2), 2);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0>(acc[0], mx_w(s_tab, 0, j), limc0, s_tab, 0, j, za, fl, 0);
+        mx_column_t<0>(acc[0], wy, limc0, s_tab, 0, j, za, fl, 0, &acc[1][3]);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<kSt422C>(acc[1], mx_w(s_tab, 2, j), limc2, s_tab, 2, j, za, fl, 1);
+        mx_column_t<kSt422C, true>(acc[1], wy, limc2, s_tab, 2, j, za, fl, 1);
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx422_defer_step(L, sp, qmask, fl, b0, nq, ns, g, T);
         /* always two store instructions per step (the vmcnt accounting counts on it) */
@@ -1427,7 +1451,8 @@ struct alignas(16) Mx420Lds {
     uint8_t pix[kSide][192];            /* deferred Y blocks' pixel rows [y][24] */
     uint32_t sblk[kSide];               /* their launch-global Y block (frame-concatenated) */
     uint32_t tmcu[kSide];               /* chroma task: launch-global MCU */
-    uint16_t dtask[kSide];              /* Y: slot << 8 | v << 3 | u; chroma: 0x8000 | c << 6 | v << 3 | u */
+    uint16_t dtask[kSide];              /* a flagged column: slot << 13 | ch << 11 | u << 8 | v-mask
+                                           (chroma: ch 1 / 2, its MCU in tmcu) */
     uint16_t task[8];
     uint32_t dummy[64];
 };
@@ -1639,23 +1664,28 @@ __device__ __forceinline__ void mx420_flush(Mx420Lds &L, int &nq, int &ns, const
     const unsigned lane = mx_lane(), i = lane >> 3, x = lane & 7u;
     const bool live = (int)i < nq;
     const unsigned code = L.dtask[live ? i : 0u];
-    const unsigned v = (code >> 3) & 7u, u = code & 7u;
-    int val;
+    const unsigned slot = code >> 13, ch = (code >> 11) & 3u, u = (code >> 8) & 7u;
+    uint32_t vb = live ? (code & 0xffu) : 0u;
     long long dst;
-    if (code & 0x8000u) {
-        const unsigned ch = (code >> 6) & 3u, m = L.tmcu[live ? i : 0u];
+    const uint8_t *src = g.rgb;
+    if (ch) {
+        const unsigned m = L.tmcu[live ? i : 0u];
         unsigned f, mi, my, mx;
         mx420_mcu(h, m, f, mi, my, mx);
-        val = mx_exact_quad(g.rgb + (long long)f * g.fstride + 16ll * my * g.pitch + 48ll * mx, g.pitch, ch, u,
-                            v, x, T);
+        src = g.rgb + (long long)f * g.fstride + 16ll * my * g.pitch + 48ll * mx;
         dst = (long long)f * g.ofstride + ((long long)g.nb + (ch - 1u) * h.nmcu + mi) * 64;
     } else {
-        const unsigned slot = code >> 8;
-        val = mx_exact_pair(mx_lds(L.pix[slot]) + 3u * x, 24u, 0u, 0u, u, v, x, T);
         const unsigned b = L.sblk[slot], f = b / g.nb, bi = b - f * g.nb;
         dst = (long long)f * g.ofstride + (long long)bi * 64;
     }
-    if (live && x == 7) g.out[dst + kMxScan[v][u]] = (int16_t)val;
+    while (__ballot(vb != 0)) {
+        const bool act = vb != 0;
+        const unsigned v = act ? (unsigned)__builtin_ctz(vb) : 0u;
+        vb &= vb - 1u;
+        const int val = ch ? mx_exact_quad(src, g.pitch, ch, u, v, x, T)
+                           : mx_exact_pair(mx_lds(L.pix[slot]) + 3u * x, 24u, 0u, 0u, u, v, x, T);
+        if (act && x == 7) g.out[dst + kMxScan[v][u]] = (int16_t)val;
+    }
     mx_wave_sync();
     nq = 0;
     ns = 0;
@@ -1688,18 +1718,12 @@ __device__ __forceinline__ void mx420_defer(Mx420Lds &L, const uint8_t *sp, uint
         yblk |= (((m0b >> (16 * gq)) & 0xffu) ? 1u : 0u) << gq;              /* set 0, block gq */
         yblk |= (((m0b >> (16 * gq + 8)) & 0xffu) ? 1u : 0u) << (4 + gq);    /* set 1 */
     }
-    const unsigned cnt = (unsigned)__popc(bits);
-    unsigned incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const unsigned o = __shfl_up(incl, d, 64);
-        if ((int)lane >= d) incl += o;
-    }
-    const int ntask = (int)__builtin_amdgcn_readlane(incl, 63);
+    const uint64_t m1b = __ballot((bits & 0xff00u) != 0);
+    const int n0 = __popcll(m0b), ncol = n0 + __popcll(m1b);
     const int ny = __popc(yblk);
-    if (nq + ntask > kSide || ns + ny > kSide) {
+    if (nq + ncol > kSide || ns + ny > kSide) {
         if (nq) mx420_flush(L, nq, ns, g, h, T);
-        if (ntask > kSide) {
+        if (ncol > kSide) {
             mx420_exact_inline(L, sp, bits, mp, g, h, T);
             return;
         }
@@ -1719,26 +1743,22 @@ __device__ __forceinline__ void mx420_defer(Mx420Lds &L, const uint8_t *sp, uint
             t++;
         }
     }
-    {
-        unsigned pos = (unsigned)nq + incl - cnt;
+    {   /* this lane's flagged columns (Y first, then chroma), one queue entry each */
         const unsigned jj = lane & 15u, u = jj & 7u, gq = lane >> 4;
-        while (bits) {
-            const unsigned b = (unsigned)__builtin_ctz(bits);
-            bits &= bits - 1u;
-            const unsigned v = b & 7u;
-            if (b < 8) {
-                const unsigned yb = 4u * (jj >> 3) + gq;
-                const unsigned slot = (unsigned)ns + (unsigned)__popc(yblk & ((1u << yb) - 1u));
-                L.dtask[pos] = (uint16_t)(slot << 8 | v << 3 | u);
-            } else {
-                L.dtask[pos] = (uint16_t)(0x8000u | (1u + (jj >> 3)) << 6 | v << 3 | u);
-                L.tmcu[pos] = mp + mx420_pm(gq);
-            }
-            pos++;
+        const uint32_t vy = bits & 0xffu, vc = (bits >> 8) & 0xffu;
+        if (vy) {
+            const unsigned yb = 4u * (jj >> 3) + gq;
+            const unsigned slot = (unsigned)ns + (unsigned)__popc(yblk & ((1u << yb) - 1u));
+            L.dtask[nq + mx_rank(m0b)] = (uint16_t)(slot << 13 | u << 8 | vy);
+        }
+        if (vc) {
+            const unsigned pos = (unsigned)(nq + n0) + (unsigned)mx_rank(m1b);
+            L.dtask[pos] = (uint16_t)((1u + (jj >> 3)) << 11 | u << 8 | vc);
+            L.tmcu[pos] = mp + mx420_pm(gq);
         }
     }
     mx_wave_sync();
-    nq += ntask;
+    nq += ncol;
     ns += ny;
 }
 
@@ -1893,6 +1913,10 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
             c1 = *(const mx_u2 *)p1;
             c2 = *(const mx_u2 *)p2;
         }
+        /* the Y column's scales before the first MFMA; the chroma column's after the chroma
+         * tiles have been read (MFMA operand rule, mx_fence) */
+        const MxW wy = mx_w(s_tab, 0, j);
+        __builtin_amdgcn_sched_barrier(0);
         {
             const mx_h8 Al0 = mx_aop(y00, s0, s1, s2), Ah0 = mx_aop(y01, s0, s1, s2);
             const mx_h8 Al1 = mx_aop(y10, s0, s1, s2), Ah1 = mx_aop(y11, s0, s1, s2);
@@ -1928,10 +1952,11 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0>(accY, mx_w(s_tab, 0, j), limc0, s_tab, 0, j, za, fl, 0);
+        mx_column_t<0>(accY, wy, limc0, s_tab, 0, j, za, fl, 0, &accC[1]);
         __builtin_amdgcn_sched_barrier(0);
         const mx_f4 s12 = {0x1p-12f, 0x1p-12f, 0x1p-12f, 0x1p-12f};
         const mx_f4 rc4 = __builtin_elementwise_fma(accC[1], s12, accC[0]);
+        __builtin_amdgcn_sched_barrier(0);
         const bool second = (k & 1u) != 0;
         if (second) {
             /* rows Y' 0..3 / 4..7 of the lane's pair-MCU column: lanes in even 16-lane rows take

@@ -1,0 +1,39 @@
+"""ISA-level checks of the built MFMA kernels (CPU: hipcc cross-compiles gfx950 here).
+
+The MFMA operand rule (jpgx_mx.hip, mx_fence; tools/mfma_war_check.py): no load may write a VGPR
+that an issued MFMA may still read.  A chained product whose SrcC registers the allocator reuses
+for an LDS read gave nondeterministic wrong C rows 12..15 (profiles/r03_mfma_war.txt), which
+parity tests only catch by luck -- so the property is checked on the ISA of every build."""
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "jpeg-encoder-and-decoder_amd")
+
+
+def test_mfma_operand_rule(tmp_path):
+    asm = tmp_path / "jpgx_mx-gfx950.s"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                    "-fno-slp-vectorize", "-I" + os.path.join(REPO, "include"), "--cuda-device-only", "-S",
+                    os.path.join(PKG, "csrc", "jpgx_mx.hip"), "-o", str(asm)],
+                   check=True, capture_output=True)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), str(asm),
+                        "k_mx", "k_mx422", "k_mx420"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert r.stdout.count("0 load(s) into live MFMA operands") == 3, r.stdout
+
+
+def test_mfma_operand_rule_catches_a_violation(tmp_path):
+    """the checker itself: an LDS read into the SrcC of a chained MFMA before its result is read"""
+    s = tmp_path / "fake.s"
+    s.write_text("\n".join([
+        "_ZN12_GLOBAL__N_14k_mxE13jx_xform_args:",
+        "\tv_mfma_f32_16x16x32_f16 v[8:11], v[0:3], v[4:7], 0",
+        "\tv_mfma_f32_16x16x32_f16 v[12:15], v[0:3], v[4:7], v[8:11]",
+        "\tds_read_b64 v[8:9], v20",
+        "\tv_add_f32_e32 v30, v12, v13",
+        ".Lfunc_end0:", ""]))
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), str(s), "k_mx"],
+                       capture_output=True, text=True)
+    assert r.returncode == 1 and "1 load(s)" in r.stdout, r.stdout
