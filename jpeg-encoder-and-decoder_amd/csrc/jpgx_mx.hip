@@ -650,7 +650,8 @@ __device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, f
 }
 
 /* the same from the hi / lo accumulator tiles of rows 0..3 and 4..7; LAZY: the column's scales
- * are read here, after the tiles (the step's last MFMAs) have been read -- no MFMA in flight */
+ * are read here, after the tiles have been read (and after mx_fence(*fence) when a later MFMA may
+ * still be in flight) -- no load meets an MFMA operand */
 template <unsigned OFF, bool LAZY = false>
 __device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t, float limc, const MxTab &tb,
                                              unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc,
@@ -660,7 +661,8 @@ __device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t,
     mx_combine(acc[0], acc[1], acc[2], acc[3], R);
     if (LAZY) {
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_r<OFF>(R, mx_w(tb, t0, j), limc, tb, t0, j, za, fl, kc, fence);
+        if (fence) mx_fence(*fence);              /* a later MFMA may still be in flight */
+        mx_column_r<OFF>(R, mx_w(tb, t0, j), limc, tb, t0, j, za, fl, kc, nullptr);
     } else {
         mx_column_r<OFF>(R, t, limc, tb, t0, j, za, fl, kc, fence);
     }
@@ -1335,8 +1337,9 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
                 o[3] = mx_mma(Ah1, B[kParts - 1][w0 + 1], o[3]);
             }
         };
-        /* every LDS read of the step -- A operands and the two columns' scales -- is issued before
-         * the step's first MFMA (MFMA operand rule, mx_fence) */
+        /* every LDS read of the step's A operands is issued before its first MFMA; each column
+         * reads its scales after its tiles (the Y column after a fence on the chroma products)
+         * (MFMA operand rule, mx_fence) */
         const mx_u2 y00 = *(const mx_u2 *)(sp + aoff);
         const mx_u2 y01 = *(const mx_u2 *)(sp + aoff + 768u);
         const mx_u2 y10 = *(const mx_u2 *)(sp + aoff + 96u);
@@ -1363,7 +1366,6 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
                 c11 = *(const mx_u2 *)(p1 + h1);
             }
         }
-        const MxW wy = mx_w(s_tab, 0, j);
         __builtin_amdgcn_sched_barrier(0);
         mma2(acc[0], mx_aop(y00, s0, s1, s2), mx_aop(y01, s0, s1, s2), mx_aop(y10, s0, s1, s2),
              mx_aop(y11, s0, s1, s2), 0);
@@ -1371,9 +1373,9 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
         mma2(acc[1], mx_aop(c00, kSelLo, kSelHi, kSelLo), mx_aop(c01, kSelLo, kSelHi, kSelLo),
              mx_aop(c10, t0, t1, t2), mx_aop(c11, t0, t1, t2), 2);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0>(acc[0], wy, limc0, s_tab, 0, j, za, fl, 0, &acc[1][3]);
+        mx_column_t<0, true>(acc[0], MxW{}, limc0, s_tab, 0, j, za, fl, 0, &acc[1][3]);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<kSt422C, true>(acc[1], wy, limc2, s_tab, 2, j, za, fl, 1);
+        mx_column_t<kSt422C, true>(acc[1], MxW{}, limc2, s_tab, 2, j, za, fl, 1);
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) mx422_defer_step(L, sp, qmask, fl, b0, nq, ns, g, T);
         /* always two store instructions per step (the vmcnt accounting counts on it) */
@@ -1913,9 +1915,8 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
             c1 = *(const mx_u2 *)p1;
             c2 = *(const mx_u2 *)p2;
         }
-        /* the Y column's scales before the first MFMA; the chroma column's after the chroma
-         * tiles have been read (MFMA operand rule, mx_fence) */
-        const MxW wy = mx_w(s_tab, 0, j);
+        /* A operands before the first MFMA; each column reads its scales after its tiles (the Y
+         * column after a fence on the chroma products) (MFMA operand rule, mx_fence) */
         __builtin_amdgcn_sched_barrier(0);
         {
             const mx_h8 Al0 = mx_aop(y00, s0, s1, s2), Ah0 = mx_aop(y01, s0, s1, s2);
@@ -1952,7 +1953,7 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0>(accY, wy, limc0, s_tab, 0, j, za, fl, 0, &accC[1]);
+        mx_column_t<0, true>(accY, MxW{}, limc0, s_tab, 0, j, za, fl, 0, &accC[1]);
         __builtin_amdgcn_sched_barrier(0);
         const mx_f4 s12 = {0x1p-12f, 0x1p-12f, 0x1p-12f, 0x1p-12f};
         const mx_f4 rc4 = __builtin_elementwise_fma(accC[1], s12, accC[0]);
