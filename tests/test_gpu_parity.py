@@ -94,6 +94,26 @@ def test_tie_frame_every_dc_is_a_tie(cuda):
     assert np.array_equal(_gpu(rgb, 50, cuda), O.blocks(rgb, 50))
 
 
+def _sparse_tie(W, H, seed, every):
+    """Random frame with every `every`-th block replaced by a flat tie block (gen_tie): at q50 its
+    Y DC is an exact .5 tie, so steps carry a few flagged columns -- the deferred exact pass
+    (queue of flagged columns, flushes between steps) rather than the inline one."""
+    rgb = O.gen_splitmix(seed, W, H)
+    tie = O.gen_tie(W, H)
+    bpr = W // 8
+    for bi in range(3, (W // 8) * (H // 8), every):
+        r, c = divmod(bi, bpr)
+        rgb[8 * r:8 * r + 8, 8 * c:8 * c + 8] = tie[8 * r:8 * r + 8, 8 * c:8 * c + 8]
+    return rgb
+
+
+@pytest.mark.parametrize("every", [5, 13, 61])
+def test_deferred_exact_queue(cuda, every):
+    rgb = _sparse_tie(1024, 256, 77 + every, every)
+    for q in (50, 90, 97):
+        assert np.array_equal(_gpu(rgb, q, cuda), O.blocks(rgb, q)), f"q{q}"
+
+
 @pytest.mark.parametrize("W,F", [(8, 1), (24, 1), (520, 1), (24, 3), (40, 5)])
 def test_tail_step_guard_region(cuda, W, F):
     """Launches whose block count is not a multiple of 8 (the last step's missing blocks are

@@ -122,6 +122,21 @@ def test_gpu_subsample_tie_and_flat(cuda, impl, sr):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sr", [1, 2])
+@pytest.mark.parametrize("every", [5, 29])
+def test_gpu_subsample_deferred_queue(cuda, impl, sr, every):
+    """sparse flat tie blocks in a random frame: few flagged columns per step (the deferred
+    queue of flagged columns and its flushes), Y and chroma"""
+    rgb = O.gen_splitmix(500 + every, 1024, 256)
+    tie = O.gen_tie(1024, 256)
+    for bi in range(3, 128 * 32, every):
+        r, c = divmod(bi, 128)
+        rgb[8 * r:8 * r + 8, 8 * c:8 * c + 8] = tie[8 * r:8 * r + 8, 8 * c:8 * c + 8]
+    for q in (50, 97):
+        _check(rgb, q, sr, cuda)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sr", [1, 2])
 def test_gpu_subsample_1080p_class(cuda, impl, sr):
     _check(O.gen_splitmix(2, 1920, 1072), 90, sr, cuda)
 
