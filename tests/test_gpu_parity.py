@@ -107,6 +107,26 @@ def _sparse_tie(W, H, seed, every):
     return rgb
 
 
+# Gray blocks whose rows are constant across x (only column u = 0 non-zero) with two coefficients
+# of that column at (or within 1e-5 of) a .5 boundary: at q50 v = 0 and v = 4 are both exact ties
+# (found by a search over the reference's double arithmetic), at q90 v = 1 and v = 2 -- one
+# deferred column with a multi-bit v-mask per such block.
+MULTI_V = {50: [[182, 101, 34, 200, 52, 82, 221, 160], [143, 34, 169, 120, 73, 231, 148, 66], [80, 198, 94, 81, 204, 128, 10, 29], [165, 172, 249, 77, 160, 231, 2, 120], [115, 230, 107, 220, 81, 126, 15, 122], [93, 65, 27, 115, 251, 160, 158, 227]],
+           90: [[53, 16, 72, 210, 179, 226, 163, 184]]}
+
+
+@pytest.mark.parametrize("q", [50, 90])
+def test_deferred_multi_v_columns(cuda, q):
+    rgb = O.gen_splitmix(900 + q, 1024, 128)
+    pats = MULTI_V[q]
+    bpr = 1024 // 8
+    for i, bi in enumerate(range(5, bpr * 16, 11)):
+        r, c = divmod(bi, bpr)
+        col = np.array(pats[i % len(pats)], np.uint8)[:, None, None]
+        rgb[8 * r:8 * r + 8, 8 * c:8 * c + 8] = col
+    assert np.array_equal(_gpu(rgb, q, cuda), O.blocks(rgb, q))
+
+
 @pytest.mark.parametrize("every", [5, 13, 61])
 def test_deferred_exact_queue(cuda, every):
     rgb = _sparse_tie(1024, 256, 77 + every, every)

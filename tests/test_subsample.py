@@ -137,6 +137,20 @@ def test_gpu_subsample_deferred_queue(cuda, impl, sr, every):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sr", [1, 2])
+def test_gpu_subsample_deferred_multi_v(cuda, impl, sr):
+    """Y blocks whose column u = 0 holds two flagged coefficients (test_gpu_parity.MULTI_V at q50):
+    deferred Y columns with multi-bit v-masks beside the chroma of the same MCUs"""
+    from test_gpu_parity import MULTI_V
+    rgb = O.gen_splitmix(940 + sr, 1024, 128)
+    pats = MULTI_V[50]
+    for i, bi in enumerate(range(5, 128 * 16, 11)):
+        r, c = divmod(bi, 128)
+        rgb[8 * r:8 * r + 8, 8 * c:8 * c + 8] = np.array(pats[i % len(pats)], np.uint8)[:, None, None]
+    _check(rgb, 50, sr, cuda)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sr", [1, 2])
 def test_gpu_subsample_1080p_class(cuda, impl, sr):
     _check(O.gen_splitmix(2, 1920, 1072), 90, sr, cuda)
 
