@@ -294,6 +294,8 @@ def main():
         sys.exit(launch_ranks(args.gpus))
     if args.kernel == "xform":
         os.environ["JPGX_LIB"] = ALT_LIB
+    elif args.kernel == "mx" and alt_selected():
+        os.environ.pop("JPGX_LIB")                # --kernel mx: the product library, whatever the env said
     kname = "k_xform" if alt_selected() else "k_mx"
 
     import torch

@@ -87,7 +87,7 @@ typedef struct jpgx_frames {
     int width, height;        /* full-frame pixel geometry                                */
     int row_begin, row_end;   /* block rows processed; 0 and height/8 for whole frames    */
     int nframes;              /* frames in the batch (>= 1)                               */
-    size_t in_pitch;          /* bytes between pixel rows (multiple of 8)                 */
+    size_t in_pitch;          /* bytes between pixel rows (multiple of 8, at most 2^27)   */
     size_t in_frame_stride;   /* bytes between frames (multiple of 8)                     */
     size_t out_frame_stride;  /* int16 elements between frames' outputs                   */
 } jpgx_frames;

@@ -167,6 +167,16 @@ int jpgx_write_jfif(const int16_t *coef, int width, int height, int quality, uin
 int jpgx_write_jfif_sub(const int16_t *coef, int width, int height, int quality,
                         int sample_ratio, uint8_t *out, size_t cap, size_t *len);
 
+/* The same with restart intervals, coded on host threads: `restart_rows` MCU rows per interval
+ * (0: none, the single-interval stream of jpgx_write_jfif_sub; -1: about four intervals per
+ * thread; the interval, rows x MCUs per row, must fit DRI's 16 bits), a DRI segment, DC
+ * predictors reset and an RSTm marker at every interval boundary (T.81 F.1.2.1.3, B.2.4.4);
+ * `nthreads` threads (0: one per online CPU, at most 64) code contiguous runs of intervals
+ * into their own buffers, concatenated in order -- e.g. the 8 GPU stripes of a 16384^2 frame.
+ * Returns as jpgx_write_jfif_sub, or JPGX_ENOMEM. */
+int jpgx_write_jfif_ex(const int16_t *coef, int width, int height, int quality, int sample_ratio,
+                       int restart_rows, int nthreads, uint8_t *out, size_t cap, size_t *len);
+
 /* encode_bmp_to_jpeg with flags: JPGX_FLAG_SUBSAMPLE and sample_ratio 1/2 write a truly
  * subsampled JFIF (extension); otherwise exactly jpgx_encode_bmp_to_jpeg.  GPU `device`. */
 int jpgx_encode_bmp_to_jpeg_ex(const char *input, const char *output, int quality,

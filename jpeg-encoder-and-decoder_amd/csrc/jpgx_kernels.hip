@@ -820,6 +820,7 @@ int resident_waves()
 #define JPGX_ALT_DISPATCH 0
 #endif
 constexpr bool kAltDispatch = JPGX_ALT_DISPATCH != 0;
+constexpr size_t kMaxPitch = (size_t)1 << 27;     /* 16 rows x pitch + 256 < 2^32 */
 
 }  // namespace
 
@@ -849,6 +850,8 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     if (fr->in_pitch < (size_t)fr->width * 3 || fr->in_pitch % 8 || fr->in_frame_stride % 8 ||
         ((uintptr_t)d_rgb & 7) || ((uintptr_t)d_out & 15) || fr->out_frame_stride % 8)
         return JPGX_EARG;
+    /* the MFMA kernels address a step's pixel rows (up to 16 of them) with 32-bit lane offsets */
+    if (fr->in_pitch > kMaxPitch) return JPGX_EARG;
     const int bpr = fr->width / 8;
     const size_t nb = (size_t)(fr->row_end - fr->row_begin) * bpr;
     const size_t total = nb * fr->nframes;

@@ -40,7 +40,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "jpgx_internal.h"
@@ -418,7 +420,8 @@ __device__ __forceinline__ unsigned mx_col_block(unsigned k, unsigned sl)
 /* Inline exact pass of one step (a step with more tasks than the deferred queue holds, e.g.
  * FLAG_FORCE_EXACT): every flagged coefficient (bit 8 col + v of a lane's `bits`), eight at a
  * time, patching the stage. */
-__device__ __forceinline__ void mx_exact_inline(MxLds &L, const uint8_t *slot, uint32_t bits,
+template <class Lds>
+__device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uint32_t bits,
                                                 const jx_mxtab &T)
 {
     const unsigned lane = mx_lane();
@@ -591,7 +594,7 @@ __device__ __forceinline__ MxW mx_w(const MxTab &tb, unsigned t0, unsigned j)
  * max |d| >= limc first and the per-coefficient limits only when it fires (mx_flags) flags
  * exactly the same coefficients with two fewer instructions per coefficient pair.
  */
-__device__ __forceinline__ float mx_limc(const MxTab &tb, unsigned t, unsigned j)
+__host__ __device__ __forceinline__ float mx_limc(const MxTab &tb, unsigned t, unsigned j)
 {
     const mx_f4 a = tb.wl[t][0][j], b = tb.wl[t][1][j];
     const float mn = fminf(fminf(fminf(a.x, a.y), fminf(a.z, a.w)), fminf(fminf(b.x, b.y), fminf(b.z, b.w)));
@@ -917,6 +920,382 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
         }
     }
     if (nq) mx_flush(L, nq, ns, g, T);
+}
+
+/* ==== k_mxs: k_mx's transform in short-lived waves (round 4) =================================
+ *
+ * The same per-step arithmetic as k_mx (MFMA rows, packed-VALU columns, band, zig-zag stage,
+ * inline exact pass), but the launch is NOT persistent: wave w of the grid computes the C
+ * consecutive steps w C .. w C + C - 1 (8 C blocks) and exits, so the hardware dispatcher hands
+ * the chip one compact, advancing window of the batch (the persistent grid-stride layout drifts:
+ * instruction arbitration favours older waves, profiles/r03_skeleton_wgrank.txt; the memory
+ * skeleton reads 0.72-0.76 non-persistent vs 0.67-0.70 persistent, profiles/r04_*).  What a
+ * short wave needs is a cheap start:
+ *   - its pixel DMA for all C steps is issued first (no ring reuse: step k lives in slot k);
+ *   - the B operands (6 KiB, quality-independent) and this quality's scale / limit table with
+ *     the hot-path band limits (2.1 KiB) are one pre-laid-out image (g_mxs_img) that the
+ *     workgroup's four waves copy into LDS with LDS-DMA (16-byte pieces), one s_barrier;
+ *   - the exact pass runs inline per step on the stage (no cross-step queue, no side buffer).
+ * vmcnt bookkeeping: every step issues exactly two DMA operations up front (padding operations
+ * for general / absent steps) and three stores, so step k waits with vmcnt(2 (C - 1 - k) + 3 k).
+ */
+#ifndef JX_MXS_C
+#define JX_MXS_C 3                      /* steps per wave */
+#endif
+constexpr unsigned kMxsC = JX_MXS_C;
+static_assert(kMxsC >= 1, "k_mxs: at least one step per wave");
+/* up to three steps: every step's DMA up front, step k in slot k; more: a ring of three slots,
+ * DMA two steps ahead (k_mx's scheme), step k in slot k % 3 */
+constexpr unsigned kMxsR = kMxsC < 3 ? kMxsC : 3;
+constexpr bool kMxsRing = kMxsC > 3;
+
+struct alignas(16) MxsLds {
+    uint8_t ring[kMxsR][kSlot];         /* pixels, [y][24 jb + k]                       */
+    uint8_t stage[kStageBytes];         /* zig-zag stage (k_mx's layout, mx_pos)        */
+    uint16_t task[8];                   /* inline exact batch                           */
+};
+static_assert(sizeof(MxsLds) % 16 == 0, "16-byte aligned LDS regions");
+/* the workgroup image: B operands, scale / limit table, hot-path limits (mx_limc) per lane
+ * profile and column kind */
+struct alignas(16) MxsImg {
+    mx_u4 B[3 * JX_MX_PARTS][64];
+    MxTab tab;
+    float limc[2][16];
+};
+constexpr unsigned kMxsPieces = sizeof(MxsImg) / 16;
+static_assert(sizeof(MxsImg) % 16 == 0 && kMxsPieces <= 768, "three 16-byte pieces per thread");
+static_assert(sizeof(MxsLds) * 4 + sizeof(MxsImg) <= 40 * 1024, "4 workgroups of 4 waves per CU");
+__device__ MxsImg g_mxs_img[2][JX_MAXQ + 1];     /* [force][quality] */
+#ifdef JX_MXS_STAMP                    /* timing probe builds only: per-wave timestamps */
+__device__ unsigned long long g_mxs_ts[1u << 20];
+#define JX_MXS_TS(i, v) do { if (lane == 0 && 8u * wv + 8u <= (1u << 20)) g_mxs_ts[8u * wv + (i)] = (v); } while (0)
+#else
+#define JX_MXS_TS(i, v) do { } while (0)
+#endif
+
+template <unsigned N>
+__device__ __forceinline__ void mx_wait_vm()
+{
+    static_assert(N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((int)((N & 15u) | ((N >> 4) << 14) | 0xF70u));
+}
+
+/* a step cursor (wave-uniform): launch-global first block, whether the step is simple (one
+ * block-row of one frame, not the row's last block, in range: two LDS-DMA operations and three
+ * stores off its pointers), its column, pixel (8c, 8r) and channel-0 output pointers */
+struct MxsCur {
+    unsigned b, c;
+    bool simple;
+    const uint8_t *src;
+    int16_t *dst;
+};
+
+__device__ __forceinline__ void mxs_simple(MxsCur &P, const MxG &g)
+{
+    P.simple = P.c + 8u < g.bpr && P.b + 8u <= g.total && g.lin_store;
+}
+
+__device__ __forceinline__ void mxs_at(MxsCur &P, const MxG &g, unsigned b)
+{
+    P.b = b;
+    P.simple = false;
+    if (b >= g.total) return;
+    MxCur X;
+    mx_seek(X, g, b);
+    P.c = X.c;
+    P.src = X.src;
+    P.dst = X.dst;
+    mxs_simple(P, g);
+}
+
+/* the next step: a simple step's successor is in the same block-row (no division) */
+__device__ __forceinline__ void mxs_next(MxsCur &P, const MxG &g)
+{
+    if (!P.simple) {
+        mxs_at(P, g, P.b + 8u);
+        return;
+    }
+    P.b += 8u;
+    P.c += 8u;
+    P.src += 192;
+    P.dst += 512;
+    mxs_simple(P, g);
+}
+
+/* two VMEM operations into `slot`: the step's pixels, or padding (a general step's slot is
+ * filled through registers at compute time after a vmcnt(0); an absent step's is never read) */
+__device__ __forceinline__ void mxs_issue(const MxsCur &P, const MxG &g, uint8_t *slot, uint32_t off0,
+                                          uint32_t off1, unsigned lane)
+{
+    if (P.simple) {
+        __builtin_amdgcn_global_load_lds((mx_gp)(P.src + off0), (mx_lp)slot, 16, 0, 0);
+        if (lane < 32) __builtin_amdgcn_global_load_lds((mx_gp)(P.src + off1), (mx_lp)(slot + 1024u), 16, 0, 0);
+    } else {
+        __builtin_amdgcn_global_load_lds((mx_gp)g.rgb, (mx_lp)slot, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((mx_gp)g.rgb, (mx_lp)slot, 4, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(256, JX_MX_WPE) void k_mxs(const jx_xform_args a)
+{
+    __shared__ __attribute__((aligned(16))) MxsLds s_lds[4];
+    __shared__ __attribute__((aligned(16))) MxsImg s_img;
+    MxG g;
+    g.rgb = a.g.rgb;
+    g.out = a.g.out;
+    g.pitch = a.g.in_pitch;
+    g.fstride = a.g.in_fstride;
+    g.ofstride = a.g.out_fstride;
+    g.bpr = (unsigned)a.g.bpr;
+    g.nb = (unsigned)a.g.nb;
+    g.total = (unsigned)a.g.nb * (unsigned)a.g.nframes;
+    g.row0 = a.g.row0;
+    g.quality = a.quality;
+    g.force = a.force_exact;
+    g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
+#pragma unroll
+    for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+
+#ifdef JX_MXS_STAMP
+    const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime(), cs0 = __builtin_amdgcn_s_memtime();
+#endif
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    MxsLds &L = s_lds[wave];
+    /* the workgroup image into LDS (LDS-DMA: piece p of thread t lands at 16 p) */
+    {
+        const uint8_t *img = (const uint8_t *)&g_mxs_img[g.force ? 1 : 0][g.quality];
+#pragma unroll
+        for (unsigned i = 0; i < 3; i++) {
+            const unsigned piece = 256u * i + threadIdx.x;
+            if (256u * i + 64u * wave < kMxsPieces && piece < kMxsPieces)
+                __builtin_amdgcn_global_load_lds((mx_gp)(img + 16u * piece),
+                                                 (mx_lp)((uint8_t *)&s_img + 16u * (256u * i + 64u * wave)), 16, 0, 0);
+        }
+    }
+    /* this wave's first steps' DMA (kMxsR of them; ring mode: two) */
+    const unsigned wv = blockIdx.x * 4u + wave;
+    const uint32_t off0 = (uint32_t)((lane / 12u) * (unsigned)g.pitch + 16u * (lane % 12u));
+    const uint32_t off1 = (uint32_t)(((64u + lane) / 12u) * (unsigned)g.pitch + 16u * ((64u + lane) % 12u));
+    MxsCur iss;                                  /* issue cursor */
+    mxs_at(iss, g, 8u * kMxsC * wv);
+    MxsCur cmp = iss;                            /* compute cursor */
+    constexpr unsigned kPro = kMxsRing ? 2u : kMxsR;
+#pragma unroll
+    for (unsigned k = 0; k < kPro; k++) {
+        mxs_issue(iss, g, L.ring[k], off0, off1, lane);
+        mxs_next(iss, g);
+    }
+
+    /* lane constants (k_mx's) */
+    const unsigned m = lane & 15u, q = lane >> 4;
+    const uint32_t aoff = 192u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 0u);
+    const uint32_t s0 = q < 3 ? kSelLo : kSelOne;
+    const uint32_t s1 = q < 3 ? kSelHi : kSelZero;
+    const uint32_t s2 = q < 3 ? kSelLo : kSelZero;
+    const uint32_t so0 = lane * 16u, so1 = so0 + g.nb * 128u, so2 = so1 + g.nb * 128u;
+    const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
+    const uint32_t rr = ro + ((lane >> 3) < 4 ? 8u : 16u) * kBS;
+    const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
+    uint32_t za[8];
+    {
+        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * mx_pos(j >> 3, gq);
+#pragma unroll
+        for (int v = 0; v < 8; v++) za[v] = base + 2u * (unsigned)kMxScan[v][u];
+    }
+    const jx_mxtab &T = g_mxtab[g.force ? 1 : 0][g.quality];
+
+    /* the image has landed (it is older than the prologue's pixel operations), in every wave */
+    mx_wait_vm<2u * kPro>();
+    __builtin_amdgcn_s_barrier();
+    mx_wave_sync();
+    if (cmp.b >= g.total) return;
+    mx_u4 B[kParts][3];
+#pragma unroll
+    for (int p = 0; p < kParts; p++)
+#pragma unroll
+        for (int w = 0; w < 3; w++) B[p][w] = s_img.B[3 * p + w][lane];
+    const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
+    const MxTab &tb = s_img.tab;
+#ifdef JX_MXS_STAMP
+    {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        JX_MXS_TS(0, ts0);
+        JX_MXS_TS(1, t1);
+        JX_MXS_TS(5, cs0);
+        JX_MXS_TS(7, ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                         (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+    }
+#endif
+
+    /* one step from `sp` (its DMA has landed): transform, inline exact pass, three stores */
+    const auto body = [&](const MxsCur &S, uint8_t *sp) __attribute__((always_inline)) {
+        if (!S.simple) {
+            MxCur P;
+            mx_seek(P, g, S.b);
+            mx_issue(g, P, S.b, false, off0, off1, sp);      /* register path; waits vmcnt(0) */
+        }
+        mx_wave_sync();
+#ifdef JX_MXS_NOCOMP                    /* timing probe only: the memory pattern without the transform */
+        const uint8_t *const ob = (const uint8_t *)S.dst;
+        const bool early = false;
+        {
+            const mx_u2 d = *(const mx_u2 *)(sp + aoff);
+            *(__attribute__((address_space(3))) uint32_t *)(uintptr_t)za[0] = d.x ^ d.y;
+            mx_wave_sync();
+        }
+#else
+        const mx_u2 d00 = *(const mx_u2 *)(sp + aoff);
+        const mx_u2 d01 = *(const mx_u2 *)(sp + aoff + 768u);
+        const mx_u2 d10 = *(const mx_u2 *)(sp + aoff + 96u);
+        const mx_u2 d11 = *(const mx_u2 *)(sp + aoff + 864u);
+        const MxW w0 = mx_w(tb, 0, j);
+        const mx_h8 A00 = mx_aop(d00, s0, s1, s2), A01 = mx_aop(d01, s0, s1, s2);
+        const mx_h8 A10 = mx_aop(d10, s0, s1, s2), A11 = mx_aop(d11, s0, s1, s2);
+        __builtin_amdgcn_sched_barrier(0);
+        const mx_f4 z = {};
+        uint32_t fl = 0;
+        mx_f4 acc[3][4];
+        const auto mma_set = [&](mx_f4(&o)[4], const mx_h8 &Alo, const mx_h8 &Ahi) __attribute__((always_inline)) {
+            o[0] = mx_mma(Alo, B[0][0], z);
+            o[2] = mx_mma(Ahi, B[0][0], z);
+            o[1] = mx_mma(Alo, B[1][0], z);
+            o[3] = mx_mma(Ahi, B[1][0], z);
+            if (kParts == 3) {
+                o[1] = mx_mma(Alo, B[kParts - 1][0], o[1]);
+                o[3] = mx_mma(Ahi, B[kParts - 1][0], o[3]);
+            }
+        };
+        mma_set(acc[0], A00, A01);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_set(acc[1], A10, A11);
+        __builtin_amdgcn_sched_barrier(0);
+        mx_column_t<0>(acc[0], w0, limc0, tb, 0, j, za, fl, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[2][0] = mx_mma(A00, B[0][1], z);
+        acc[2][2] = mx_mma(A01, B[0][1], z);
+        acc[2][1] = mx_mma(A00, B[1][1], z);
+        acc[2][3] = mx_mma(A01, B[1][1], z);
+        acc[2][0] = mx_mma(A10, B[0][2], acc[2][0]);
+        acc[2][2] = mx_mma(A11, B[0][2], acc[2][2]);
+        acc[2][1] = mx_mma(A10, B[1][2], acc[2][1]);
+        acc[2][3] = mx_mma(A11, B[1][2], acc[2][3]);
+        if (kParts == 3) {
+            acc[2][1] = mx_mma(A00, B[kParts - 1][1], acc[2][1]);
+            acc[2][3] = mx_mma(A01, B[kParts - 1][1], acc[2][3]);
+            acc[2][1] = mx_mma(A10, B[kParts - 1][2], acc[2][1]);
+            acc[2][3] = mx_mma(A11, B[kParts - 1][2], acc[2][3]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mx_column_t<4 * kBS>(acc[1], w0, limc0, tb, 0, j, za, fl, 1, &acc[2][3]);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint8_t *const ob = (const uint8_t *)S.dst;
+        const bool early = S.simple && __ballot((fl & 0xffffu) != 0) == 0;
+        if (early) {
+            mx_fence(acc[2][3]);                       /* the Cr products are done (operand rule) */
+            mx_wave_sync();
+            const mx_u4 v0 = *(const mx_u4 *)(L.stage + ro);
+            const mx_u4 v1 = *(const mx_u4 *)(L.stage + 12u * kBS + ro);
+            __builtin_nontemporal_store(v0, (mx_u4 *)(ob + so0));
+            __builtin_nontemporal_store(v1, (mx_u4 *)(ob + so1));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mx_column_t<8 * kBS, true>(acc[2], w0, limc2, tb, 2, j, za, fl, 2);
+        mx_wave_sync();
+        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
+            /* the launch's last step: flags of its clamped copies are dropped (never stored) */
+            if (S.b + 8u > g.total) {
+                const unsigned nvalid = g.total - S.b;
+#pragma unroll
+                for (int kk = 0; kk < 3; kk++)
+                    if (mx_col_block((unsigned)kk, lane) >= nvalid) fl &= ~(0xffu << (8 * kk));
+            }
+            mx_exact_inline(L, sp, fl, T);
+        }
+#endif
+        /* stores: always three store instructions (the vmcnt accounting counts on it) */
+        if (early) {
+            const mx_u4 v2 = *(const mx_u4 *)(L.stage + rr);
+            __builtin_nontemporal_store(v2, (mx_u4 *)(ob + so2));
+        } else if (S.simple) {
+            const mx_u4 v0 = *(const mx_u4 *)(L.stage + ro);
+            const mx_u4 v1 = *(const mx_u4 *)(L.stage + 12u * kBS + ro);
+            const mx_u4 v2 = *(const mx_u4 *)(L.stage + rr);
+            __builtin_nontemporal_store(v0, (mx_u4 *)(ob + so0));
+            __builtin_nontemporal_store(v1, (mx_u4 *)(ob + so1));
+            __builtin_nontemporal_store(v2, (mx_u4 *)(ob + so2));
+        } else {
+            const unsigned l = mx_lane();
+            const unsigned bl = S.b + (l >> 3), b = bl < g.total ? bl : g.total - 1u;
+            const unsigned f = b / g.nb, bi = b - f * g.nb;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const mx_u4 val = *(const mx_u4 *)(L.stage + kBS * mx_pos((unsigned)c, l >> 3) + (l & 7u) * 16u);
+                if (bl < g.total)
+                    __builtin_nontemporal_store(
+                        val, (mx_u4 *)(g.out + (long long)f * g.ofstride +
+                                       ((long long)c * g.nb + bi) * 64 + (l & 7u) * 8));
+            }
+        }
+        mx_wave_sync();
+    };
+
+    if constexpr (!kMxsRing) {
+        /* step k waits for its DMA: younger are kMxsR - 1 - k steps' two DMA operations and k
+         * steps' three stores */
+        const auto step = [&](auto kc) __attribute__((always_inline)) {
+            constexpr unsigned k = decltype(kc)::value < kMxsR ? decltype(kc)::value : kMxsR - 1;
+            if (cmp.b >= g.total) return;
+            mx_wait_vm<2 * (kMxsR - 1 - k) + 3 * k>();
+            body(cmp, L.ring[k]);
+            mxs_next(cmp, g);
+        };
+        step(std::integral_constant<unsigned, 0>{});
+#ifdef JX_MXS_STAMP
+        JX_MXS_TS(2, __builtin_amdgcn_s_memrealtime());
+#endif
+        if constexpr (kMxsR > 1) step(std::integral_constant<unsigned, 1>{});
+        if constexpr (kMxsR > 2) step(std::integral_constant<unsigned, 2>{});
+    } else {
+        unsigned slot = 0;
+        for (unsigned k = 0; k < kMxsC; k++) {
+            if (cmp.b >= g.total) break;
+            /* younger than this step's DMA: the step after it (two DMA operations) and the steps
+             * since its issue (three stores each): 2 at step 0, 2 + 3 at step 1, then 3 + 2 + 3.
+             * (No padding in the prologue: its target slot would also receive a later DMA.) */
+            if (k == 0)
+                mx_wait_vm<2>();
+            else if (k == 1)
+                mx_wait_vm<5>();
+            else
+                mx_wait_vm<8>();
+            mx_wave_sync();
+            uint8_t *const sp = L.ring[0] + kSlot * slot;
+            /* the step two ahead into the slot of the step before (consumed) */
+            const unsigned s2 = slot == 0 ? 2u : slot - 1u;
+            if (k + 2 < kMxsC) {
+                mxs_issue(iss, g, L.ring[0] + kSlot * s2, off0, off1, lane);
+                mxs_next(iss, g);
+            } else {
+                /* padding (two operations keep the count): the slot of step k - 1, never read again */
+                __builtin_amdgcn_global_load_lds((mx_gp)g.rgb, (mx_lp)(L.ring[0] + kSlot * s2), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((mx_gp)g.rgb, (mx_lp)(L.ring[0] + kSlot * s2), 4, 0, 0);
+            }
+            body(cmp, sp);
+            mxs_next(cmp, g);
+            slot = slot == 2 ? 0u : slot + 1u;
+#ifdef JX_MXS_STAMP
+            if (k == 0) JX_MXS_TS(2, __builtin_amdgcn_s_memrealtime());
+#endif
+        }
+    }
+#ifdef JX_MXS_STAMP
+    JX_MXS_TS(3, __builtin_amdgcn_s_memrealtime());
+    JX_MXS_TS(4, __builtin_amdgcn_s_memtime());
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    JX_MXS_TS(6, __builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 /* ==== k_mx422: true 4:2:2 (extension, JPGX_FLAG_SUBSAMPLE, sample_ratio 1) ==================
@@ -2089,11 +2468,41 @@ int mx_tables_for_current_device(int *waves)
                     }
             }
         }
-        static uint16_t ops[3 * JX_MX_PARTS][64][8];
+        std::unique_ptr<uint16_t[][64][8]> opsp(new uint16_t[3 * JX_MX_PARTS][64][8]);   /* heap: reentrant */
+        auto ops = opsp.get();
         if (!rc) rc = jx_mx_operands(ops);
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxtab), tab.data(),
                                               tab.size() * sizeof(jx_mxtab)));
-        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxB), ops, sizeof ops));
+        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxB), ops, sizeof(uint16_t) * 3 * JX_MX_PARTS * 64 * 8));
+        if (!rc) {
+            /* k_mxs's workgroup images: B operands, the LDS table as k_mx's wave 0 lays it out, and
+             * the hot-path limits mx_limc computes from it */
+            std::vector<MxsImg> img(2 * (JX_MAXQ + 1));
+            memset(img.data(), 0, img.size() * sizeof(MxsImg));
+            for (int f = 0; f < 2; f++)
+                for (int q = 1; q <= JX_MAXQ; q++) {
+                    MxsImg &I = img[f * (JX_MAXQ + 1) + q];
+                    const jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
+                    memcpy(I.B, ops, sizeof I.B);
+                    for (unsigned tt = 0; tt < 4; tt++)
+                        for (unsigned jp = 0; jp < 16; jp++) {
+                            const unsigned n = tt < 2 ? jp : 16u + (jp & 7u);
+                            float x[8];
+                            for (int pp = 0; pp < 4; pp++)
+                                for (int h = 0; h < 2; h++) {
+                                    const int v = jx_pk_k(pp, h);
+                                    x[2 * pp + h] = (tt & 1u) ? t.lsq[n][v] : t.w[n][v];
+                                }
+                            I.tab.wl[tt][0][jp] = mx_f4{x[0], x[1], x[2], x[3]};
+                            I.tab.wl[tt][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
+                        }
+                    for (unsigned jp = 0; jp < 16; jp++) {
+                        I.limc[0][jp] = mx_limc(I.tab, 1, jp);
+                        I.limc[1][jp] = mx_limc(I.tab, 3, jp);
+                    }
+                }
+            rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs_img), img.data(), img.size() * sizeof(MxsImg)));
+        }
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
@@ -2133,11 +2542,12 @@ int mx422_tables_for_current_device(int *waves)
                     }
             }
         }
-        static uint16_t ops[JX_MX_PARTS][4][64][8];
+        std::unique_ptr<uint16_t[][4][64][8]> opsp(new uint16_t[JX_MX_PARTS][4][64][8]);   /* heap: reentrant */
+        auto ops = opsp.get();
         if (!rc) rc = jx_mx422_operands(ops);
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx422tab), tab.data(),
                                               tab.size() * sizeof(jx_mxtab)));
-        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx422B), ops, sizeof ops));
+        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx422B), ops, sizeof(uint16_t) * JX_MX_PARTS * 4 * 64 * 8));
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
@@ -2177,11 +2587,12 @@ int mx420_tables_for_current_device(int *waves)
                     }
             }
         }
-        static uint16_t ops[JX_MX_PARTS][5][64][8];
+        std::unique_ptr<uint16_t[][5][64][8]> opsp(new uint16_t[JX_MX_PARTS][5][64][8]);   /* heap: reentrant */
+        auto ops = opsp.get();
         if (!rc) rc = jx_mx420_operands(ops);
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx420tab), tab.data(),
                                               tab.size() * sizeof(jx_mxtab)));
-        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx420B), ops, sizeof ops));
+        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx420B), ops, sizeof(uint16_t) * JX_MX_PARTS * 5 * 64 * 8));
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
@@ -2231,6 +2642,13 @@ extern "C" int jx_launch_mx422(const jx_xform_args *xa, void *stream)
 
 
 /* k_mx over every frame of the stripe (4:4:4 / reference-parity output); no workspace. */
+#ifdef JX_MXS_STAMP
+extern "C" int jx_mxs_stamps(unsigned long long *host, size_t n)
+{
+    return mx_rc(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_mxs_ts), std::min<size_t>(n, 1u << 20) * 8));
+}
+#endif
+
 extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)
 {
     int waves = 0;
@@ -2241,6 +2659,14 @@ extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)
 #ifndef JX_MX_NP
 #define JX_MX_NP 0
 #endif
+#ifndef JX_MX_SHORT
+#define JX_MX_SHORT 1                   /* 1: k_mxs (short waves), 0: the persistent k_mx */
+#endif
+    if (JX_MX_SHORT) {
+        const size_t w = (nsteps + kMxsC - 1) / kMxsC;
+        hipLaunchKernelGGL(k_mxs, dim3((unsigned)((w + 3) / 4)), dim3(256), JX_MX_DYNLDS, (hipStream_t)stream, *xa);
+        return mx_rc(hipGetLastError());
+    }
     const size_t w = JX_MX_NP ? (nsteps + JX_MX_NP - 1) / JX_MX_NP
                               : std::min<size_t>(nsteps, (size_t)std::max(waves, 4));
     const unsigned grid = (unsigned)((w + 3) / 4);

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 
 #include "jpgx_internal.h"
 #include "jx_consts.h"
@@ -209,7 +210,7 @@ int jx_plan_tables_mode(int quality, int sub, float w[3][64], float lim[3][64], 
                 /* error of t_fp vs the reference's real-arithmetic quotient, plus the final
                  * fma rounding of d (< 2^-25), plus slack for the reference's own double
                  * rounding (< 1e-10) and for this bound's own double arithmetic */
-                double et = b.E * (double)wf + mF * (double)fabsl((long double)wf - ws) + 0x1p-25;
+                double et = b.E * fabs((double)wf) + mF * (double)fabsl((long double)wf - ws) + 0x1p-25;
                 et = et * 1.01 + 1e-7;
                 w[ch][v * 8 + u] = wf;
                 lim[ch][v * 8 + u] = (float)(0.5 - et);
@@ -487,7 +488,8 @@ extern "C" int jx_mx_parts(void) { return JX_MX_PARTS; }
 
 extern "C" int jx_mx_operands(uint16_t ops[3 * JX_MX_PARTS][64][8])
 {
-    static MxSplit S;
+    std::unique_ptr<MxSplit> S_(new MxSplit);   /* heap, per call: reentrant across threads */
+    MxSplit &S = *S_;
     const int rc = mx_split(S);
     if (rc) return rc;
     /* operand 3 * part + which; lane l holds B[k = 8 (l >> 4) + e][plan column of l & 15] */
@@ -543,7 +545,8 @@ extern "C" int jx_plan_tables_mx(int quality, float w[24][8], float lim[24][8], 
     for (int t = 0; t < 2; t++)
         for (int u = 0; u < 8; u++)
             for (int v = 0; v < 8; v++) q[t][u * 8 + v] = (int16_t)qs[t][u][v];
-    static MxSplit S;
+    std::unique_ptr<MxSplit> S_(new MxSplit);   /* heap, per call: reentrant across threads */
+    MxSplit &S = *S_;
     rc = mx_split(S);
     if (rc) return rc;
     const long double a0 = 1.0L / sqrtl(2.0L);
@@ -559,7 +562,7 @@ extern "C" int jx_plan_tables_mx(int quality, float w[24][8], float lim[24][8], 
             const float wf = (float)ws;
             const Bnd &b = out[v];
             const double mF = BoundOps::mag(b) + b.E;
-            double et = b.E * (double)wf + mF * (double)fabsl((long double)wf - ws) + 0x1p-25;
+            double et = b.E * fabs((double)wf) + mF * (double)fabsl((long double)wf - ws) + 0x1p-25;
             et = et * 1.01 + 1e-7;
             w[n][v] = wf;
             lim[n][v] = (float)(0.5 - et);
@@ -631,8 +634,10 @@ static int mxc_split(int sub, MxcSplit &S)
  * 2.. = chroma k-steps (k = 32 (which - 2) + 8 (l >> 4) + e); lane l holds B[k][column l & 15] */
 static int mxc_operands(int sub, uint16_t (*ops)[5][64][8])
 {
-    static MxSplit S;
-    static MxcSplit C;
+    std::unique_ptr<MxSplit> S_(new MxSplit);   /* heap, per call: reentrant across threads */
+    MxSplit &S = *S_;
+    std::unique_ptr<MxcSplit> C_(new MxcSplit);
+    MxcSplit &C = *C_;
     int rc = mx_split(S);
     if (!rc) rc = mxc_split(sub, C);
     if (rc) return rc;
@@ -660,8 +665,8 @@ static int mxc_operands(int sub, uint16_t (*ops)[5][64][8])
 
 extern "C" int jx_mx422_operands(uint16_t ops[JX_MX_PARTS][4][64][8])
 {
-    static uint16_t o5[JX_MX_PARTS][5][64][8];
-    const int rc = mxc_operands(1, o5);
+    std::unique_ptr<uint16_t[][5][64][8]> o5(new uint16_t[JX_MX_PARTS][5][64][8]);
+    const int rc = mxc_operands(1, o5.get());
     if (rc) return rc;
     for (int part = 0; part < JX_MX_PARTS; part++) memcpy(ops[part], o5[part], sizeof ops[part]);
     return JPGX_OK;
@@ -704,8 +709,10 @@ static int mxc_plan_tables(int sub, int quality, float w[24][8], float lim[24][8
     for (int t = 0; t < 2; t++)
         for (int u = 0; u < 8; u++)
             for (int v = 0; v < 8; v++) q[t][u * 8 + v] = (int16_t)qs[t][u][v];
-    static MxSplit S;
-    static MxcSplit C;
+    std::unique_ptr<MxSplit> S_(new MxSplit);   /* heap, per call: reentrant across threads */
+    MxSplit &S = *S_;
+    std::unique_ptr<MxcSplit> C_(new MxcSplit);
+    MxcSplit &C = *C_;
     rc = mx_split(S);
     if (!rc) rc = mxc_split(sub, C);
     if (rc) return rc;
@@ -722,7 +729,7 @@ static int mxc_plan_tables(int sub, int quality, float w[24][8], float lim[24][8
             const float wf = (float)ws;
             const Bnd &b = out[v];
             const double mF = BoundOps::mag(b) + b.E;
-            double et = b.E * (double)wf + mF * (double)fabsl((long double)wf - ws) + 0x1p-25;
+            double et = b.E * fabs((double)wf) + mF * (double)fabsl((long double)wf - ws) + 0x1p-25;
             et = et * 1.01 + 1e-7;
             w[n][v] = wf;
             lim[n][v] = (float)(0.5 - et);
@@ -747,7 +754,8 @@ extern "C" int jx_plan_tables_mx420(int quality, float w[24][8], float lim[24][8
 static long long mxc_selftest(int sub, long long nblocks, unsigned long long seed, int quality,
                               long long *flagged, double *ratio)
 {
-    static MxcSplit C;
+    std::unique_ptr<MxcSplit> C_(new MxcSplit);
+    MxcSplit &C = *C_;
     if (mxc_split(sub, C)) return -1;
     float w[24][8], lim[24][8];
     int16_t q[2][64];
@@ -837,7 +845,8 @@ extern "C" long long jx_selftest_mx420(long long nblocks, unsigned long long see
 extern "C" long long jx_selftest_mx(long long nblocks, unsigned long long seed, int quality,
                                     long long *flagged, double *ratio)
 {
-    static MxSplit S;
+    std::unique_ptr<MxSplit> S_(new MxSplit);   /* heap, per call: reentrant across threads */
+    MxSplit &S = *S_;
     if (mx_split(S)) return -1;
     float w[24][8], lim[24][8];
     int16_t q[2][64];

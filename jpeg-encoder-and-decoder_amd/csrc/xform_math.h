@@ -11,8 +11,8 @@
  *   pixel:  preprocess.c:160-162 then level_shift preprocess.c:186-188
  *   DCT:    dct.c:43-56   F(u,v) = 1/4 a(u) a(v) sum_x sum_y X[y][x] cos((2x+1)u pi/16) cos((2y+1)v pi/16)
  * The 1-D transform below is the unnormalised 8-point DCT-II computed by an even/odd
- * decomposition; out[4] omits its cos(pi/4) factor and nothing is normalised: both factors
- * and the quantiser divisor are folded into one per-coefficient scale w(u,v) on the host.
+ * decomposition with each output scaled by a constant (jx_fdct8); nothing is normalised: the
+ * scale factors and the quantiser divisor are folded into one per-coefficient w(u,v) on the host.
  */
 #ifndef JPGX_XFORM_MATH_H
 #define JPGX_XFORM_MATH_H
@@ -65,7 +65,15 @@ JX_HD typename O::T jx_pixel(typename O::T r, typename O::T g, typename O::T b)
     return O::fmac(r, JX_K(0.5), O::fmac(g, JX_K(-0.418688), O::mulc(b, JX_K(-0.081312))));
 }
 
-/* Unnormalised 8-point DCT-II, even/odd split; out[4] lacks its cos(pi/4) factor. 34 ops. */
+/*
+ * Unnormalised, SCALED 8-point DCT-II, even/odd split, 28 ops: out[k] = sum_x in[x]
+ * cos((2x+1)k pi/16) / f(k), with f(0) = 1, f(4) = C4, f(2) = C2, f(6) = -C2, f(k odd) = Ck.
+ * Each output's factor is the one that makes its first term a plain addend (no product): the
+ * odd outputs are d0 + (Ck'/Ck) d1 + ..., the (2, 6) rotation e2 + (C6/C2) e3 and
+ * e3 - (C6/C2) e2.  The factors go into the per-coefficient scale w(u,v) on the host
+ * (jpgx_plan.cpp dct_kfactor evaluates them from this very code).  Round 4: 34 -> 28 ops.
+ */
+#define JX_KR(a, b) jx_const{(float)((a) / (b)), (double)((a) / (b))}
 template <class O>
 JX_HD void jx_fdct8(const typename O::T *in, typename O::T *out)
 {
@@ -78,17 +86,13 @@ JX_HD void jx_fdct8(const typename O::T *in, typename O::T *out)
     const T e2 = O::sub(s0, s3), e3 = O::sub(s1, s2);
     out[0] = O::add(e0, e1);
     out[4] = O::sub(e0, e1);
-    out[2] = O::fmac(e2, JX_K(JX_C2), O::mulc(e3, JX_K(JX_C6)));
-    out[6] = O::fmac(e2, JX_K(JX_C6), O::mulc(e3, JX_K(-JX_C2)));
-    out[1] = O::fmac(d0, JX_K(JX_C1), O::fmac(d1, JX_K(JX_C3), O::fmac(d2, JX_K(JX_C5), O::mulc(d3, JX_K(JX_C7)))));
-    out[3] = O::fmac(d0, JX_K(JX_C3), O::fmac(d1, JX_K(-JX_C7), O::fmac(d2, JX_K(-JX_C1), O::mulc(d3, JX_K(-JX_C5)))));
-    out[5] = O::fmac(d0, JX_K(JX_C5), O::fmac(d1, JX_K(-JX_C1), O::fmac(d2, JX_K(JX_C7), O::mulc(d3, JX_K(JX_C3)))));
-    out[7] = O::fmac(d0, JX_K(JX_C7), O::fmac(d1, JX_K(-JX_C5), O::fmac(d2, JX_K(JX_C3), O::mulc(d3, JX_K(-JX_C1)))));
+    out[2] = O::fmac(e3, JX_KR(JX_C6, JX_C2), e2);
+    out[6] = O::fmac(e2, JX_KR(-JX_C6, JX_C2), e3);
+    out[1] = O::fmac(d3, JX_KR(JX_C7, JX_C1), O::fmac(d2, JX_KR(JX_C5, JX_C1), O::fmac(d1, JX_KR(JX_C3, JX_C1), d0)));
+    out[3] = O::fmac(d3, JX_KR(-JX_C5, JX_C3), O::fmac(d2, JX_KR(-JX_C1, JX_C3), O::fmac(d1, JX_KR(-JX_C7, JX_C3), d0)));
+    out[5] = O::fmac(d3, JX_KR(JX_C3, JX_C5), O::fmac(d2, JX_KR(JX_C7, JX_C5), O::fmac(d1, JX_KR(-JX_C1, JX_C5), d0)));
+    out[7] = O::fmac(d3, JX_KR(-JX_C1, JX_C7), O::fmac(d2, JX_KR(JX_C3, JX_C7), O::fmac(d1, JX_KR(-JX_C5, JX_C7), d0)));
 }
-
-
-/* Factor the computed out[k] must be multiplied by to give sum_x in[x] cos((2x+1)k pi/16). */
-JX_HD double jx_dct_kfactor(int k) { return k == 4 ? JX_C4 : 1.0; }
 
 /* ---- packed pairs ------------------------------------------------------------------------
  * The same fp32 operations, two per instruction (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32 on
@@ -112,8 +116,8 @@ struct PairOps {
 };
 
 /*
- * One 8-point jx_fdct8 with its work split over the two lanes of every pair: 17 packed
- * operations instead of 34 scalar ones.  in = (x0,x1),(x2,x3),(x4,x5),(x6,x7); out = the
+ * One 8-point jx_fdct8 with its work split over the two lanes of every pair: 14 packed
+ * operations instead of 28 scalar ones.  in = (x0,x1),(x2,x3),(x4,x5),(x6,x7); out = the
  * pairs (out0,out4),(out2,out6),(out1,out3),(out5,out7).  Swapped and broadcast operands
  * become op_sel modifiers, negated ones neg modifiers (a + (-b) == a - b exactly).
  */
@@ -121,7 +125,7 @@ template <class P>
 JX_HD void jx_fdct8_pk(const typename P::V *in, typename P::V *out)
 {
     typedef typename P::V V;
-#define JX_F(c) ((float)(c))
+#define JX_F(a, b) (JX_KR(a, b)).f
     const V x76 = P::mk(P::hi(in[3]), P::lo(in[3])), x54 = P::mk(P::hi(in[2]), P::lo(in[2]));
     const V s01 = P::add(in[0], x76), d01 = P::sub(in[0], x76);   /* (s0,s1), (d0,d1) */
     const V s23 = P::add(in[1], x54), d23 = P::sub(in[1], x54);   /* (s2,s3), (d2,d3) */
@@ -130,18 +134,16 @@ JX_HD void jx_fdct8_pk(const typename P::V *in, typename P::V *out)
     /* (e0+e1, e0-e1) as fma(e1, (1,-1), e0): fma(x, +-1, y) rounds y +- x once, exactly as
      * the scalar add/sub (a lane-dependent sign has no neg modifier) */
     out[0] = P::fma(P::mk(P::hi(e01), P::hi(e01)), P::mk(1.0f, -1.0f), P::mk(P::lo(e01), P::lo(e01)));
-    const V e2 = P::mk(P::lo(e23), P::lo(e23)), e3 = P::mk(P::hi(e23), P::hi(e23));
-    out[1] = P::fma(e2, P::mk(JX_F(JX_C2), JX_F(JX_C6)), P::mul(e3, P::mk(JX_F(JX_C6), JX_F(-JX_C2))));
+    /* (e2 + k e3, e3 - k e2) */
+    out[1] = P::fma(P::mk(P::hi(e23), P::lo(e23)), P::mk(JX_F(JX_C6, JX_C2), JX_F(-JX_C6, JX_C2)), e23);
     const V d0 = P::mk(P::lo(d01), P::lo(d01)), d1 = P::mk(P::hi(d01), P::hi(d01));
     const V d2 = P::mk(P::lo(d23), P::lo(d23)), d3 = P::mk(P::hi(d23), P::hi(d23));
-    out[2] = P::fma(d0, P::mk(JX_F(JX_C1), JX_F(JX_C3)),
-             P::fma(d1, P::mk(JX_F(JX_C3), JX_F(-JX_C7)),
-             P::fma(d2, P::mk(JX_F(JX_C5), JX_F(-JX_C1)),
-             P::mul(d3, P::mk(JX_F(JX_C7), JX_F(-JX_C5))))));
-    out[3] = P::fma(d0, P::mk(JX_F(JX_C5), JX_F(JX_C7)),
-             P::fma(d1, P::mk(JX_F(-JX_C1), JX_F(-JX_C5)),
-             P::fma(d2, P::mk(JX_F(JX_C7), JX_F(JX_C3)),
-             P::mul(d3, P::mk(JX_F(JX_C3), JX_F(-JX_C1))))));
+    out[2] = P::fma(d3, P::mk(JX_F(JX_C7, JX_C1), JX_F(-JX_C5, JX_C3)),
+             P::fma(d2, P::mk(JX_F(JX_C5, JX_C1), JX_F(-JX_C1, JX_C3)),
+             P::fma(d1, P::mk(JX_F(JX_C3, JX_C1), JX_F(-JX_C7, JX_C3)), d0)));
+    out[3] = P::fma(d3, P::mk(JX_F(JX_C3, JX_C5), JX_F(-JX_C1, JX_C7)),
+             P::fma(d2, P::mk(JX_F(JX_C7, JX_C5), JX_F(JX_C3, JX_C7)),
+             P::fma(d1, P::mk(JX_F(-JX_C1, JX_C5), JX_F(-JX_C5, JX_C7)), d0)));
 #undef JX_F
 }
 

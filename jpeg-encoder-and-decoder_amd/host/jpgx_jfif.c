@@ -16,9 +16,12 @@
  * (src/preprocess.c:161) and of the x0 = -8 last-column quirk.  AC magnitudes above 1023
  * (possible only for chroma at q >= 93 with the sign error) are clamped to the baseline range.
  */
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "../../include/jpgx_compat.h"
 #include "../csrc/jx_consts.h"
@@ -54,30 +57,10 @@ static const uint8_t kAcChrVals[162] = {
     0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7,
     0xe8, 0xe9, 0xea, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
 
-/* canonical Huffman codes (T.81 Annex C) indexed by symbol */
-typedef struct {
-    uint16_t code[256];
-    uint8_t len[256];
-} HuffCodes;
-
-static void build_codes(const uint8_t bits[16], const uint8_t *vals, HuffCodes *h)
-{
-    memset(h, 0, sizeof(*h));
-    unsigned code = 0, k = 0;
-    for (int l = 1; l <= 16; l++) {
-        for (int i = 0; i < bits[l - 1]; i++, k++) {
-            h->code[vals[k]] = (uint16_t)code++;
-            h->len[vals[k]] = (uint8_t)l;
-        }
-        code <<= 1;
-    }
-}
-
+/* ---- header bytes (fixed-size segments before the scan) ------------------------------------ */
 typedef struct {
     uint8_t *p;
     size_t n, cap;
-    uint32_t acc;     /* pending bits, MSB first */
-    int nacc;
     int overflow;
 } Out;
 
@@ -94,35 +77,6 @@ static void put_u16(Out *o, unsigned v)
     put_byte(o, (uint8_t)v);
 }
 
-static void put_bits(Out *o, unsigned v, int nbits)
-{
-    for (int i = nbits - 1; i >= 0; i--) {
-        o->acc = (o->acc << 1) | ((v >> i) & 1u);
-        if (++o->nacc == 8) {
-            const uint8_t b = (uint8_t)o->acc;
-            put_byte(o, b);
-            if (b == 0xff) put_byte(o, 0x00);            /* byte stuffing (T.81 F.1.2.3) */
-            o->acc = 0;
-            o->nacc = 0;
-        }
-    }
-}
-
-static void flush_bits(Out *o)
-{
-    if (o->nacc) put_bits(o, 0x7fu, 8 - o->nacc);      /* pad with 1-bits */
-}
-
-/* magnitude category and the value's additional bits (T.81 F.1.2.1) */
-static int category(int v, unsigned *extra)
-{
-    const int a = v < 0 ? -v : v;
-    int s = 0;
-    while ((1 << s) <= a) s++;
-    *extra = (unsigned)(v < 0 ? v + (1 << s) - 1 : v) & ((1u << s) - 1u);
-    return s;
-}
-
 static void put_dht(Out *o, int cls_id, const uint8_t bits[16], const uint8_t *vals)
 {
     int n = 0;
@@ -134,59 +88,223 @@ static void put_dht(Out *o, int cls_id, const uint8_t bits[16], const uint8_t *v
     for (int i = 0; i < n; i++) put_byte(o, vals[i]);
 }
 
-size_t jpgx_jfif_bound(int width, int height)
+/* ---- entropy-coded data: a word-at-a-time bit writer into a growable buffer ---------------
+ * Bits accumulate MSB first in a 64-bit register; every 32 bits leave as four bytes at once
+ * unless one of them is 0xFF (then byte by byte with the 0x00 stuffing of T.81 F.1.2.3). */
+typedef struct {
+    uint8_t *p;
+    size_t n, cap;
+    uint64_t acc;     /* the low nacc bits are pending */
+    int nacc;
+    int oom;
+} BW;
+
+static int bw_reserve(BW *w, size_t more)
 {
-    if (width <= 0 || height <= 0) return 0;
-    /* headers + worst case per block (DC 2+11 bits, 63 AC x (16+10 bits)) + stuffing x2 */
-    const size_t blocks = (size_t)(width / 8 + 1) * (height / 8 + 1) * 3;
-    return 1024 + blocks * 2 * (13 + 63 * 26 + 7) / 8;
+    if (w->n + more <= w->cap) return 1;
+    size_t nc = w->cap ? w->cap : 1u << 16;
+    while (nc < w->n + more) nc *= 2;
+    uint8_t *q = (uint8_t *)realloc(w->p, nc);
+    if (!q) {
+        w->oom = 1;
+        return 0;
+    }
+    w->p = q;
+    w->cap = nc;
+    return 1;
 }
 
-/* one block's Huffman-coded data (T.81 F.1.2): DC difference against *pred, AC run/size */
-static void encode_block(Out *o, const int16_t *z, int *pred, const HuffCodes *dc,
-                         const HuffCodes *ac)
+static inline void bw_byte(BW *w, uint8_t b)
 {
-    unsigned extra;
+    w->p[w->n++] = b;
+    if (b == 0xff) w->p[w->n++] = 0x00;
+}
+
+/* v < 2^nb, nb <= 32 (a Huffman code and its additional bits in one call); the caller has
+ * reserved room (bw_reserve) */
+static inline void bw_bits(BW *w, uint32_t v, int nb)
+{
+    w->acc = (w->acc << nb) | v;
+    w->nacc += nb;
+    if (w->nacc >= 32) {
+        w->nacc -= 32;
+        const uint32_t x = (uint32_t)(w->acc >> w->nacc);
+        if (((~x - 0x01010101u) & x & 0x80808080u) == 0) {       /* no 0xFF byte in x */
+            uint8_t *d = w->p + w->n;
+            d[0] = (uint8_t)(x >> 24);
+            d[1] = (uint8_t)(x >> 16);
+            d[2] = (uint8_t)(x >> 8);
+            d[3] = (uint8_t)x;
+            w->n += 4;
+        } else {
+            bw_byte(w, (uint8_t)(x >> 24));
+            bw_byte(w, (uint8_t)(x >> 16));
+            bw_byte(w, (uint8_t)(x >> 8));
+            bw_byte(w, (uint8_t)x);
+        }
+    }
+}
+
+/* pad to a byte boundary with 1-bits and emit the pending bytes */
+static void bw_flush(BW *w)
+{
+    const int pad = (8 - (w->nacc & 7)) & 7;
+    if (pad) {
+        w->acc = (w->acc << pad) | ((1u << pad) - 1u);
+        w->nacc += pad;
+    }
+    while (w->nacc >= 8) {
+        w->nacc -= 8;
+        bw_byte(w, (uint8_t)(w->acc >> w->nacc));
+    }
+}
+
+/* magnitude category and the value's additional bits (T.81 F.1.2.1) */
+static inline int category(int v, uint32_t *extra)
+{
+    const unsigned a = (unsigned)(v < 0 ? -v : v);
+    const int s = a ? 32 - __builtin_clz(a) : 0;
+    *extra = (uint32_t)(v < 0 ? v + (1 << s) - 1 : v) & ((1u << s) - 1u);
+    return s;
+}
+
+/* canonical Huffman codes (T.81 Annex C) indexed by symbol, packed: code << 8 | length */
+typedef struct {
+    uint32_t cl[256];
+} HuffCodes;
+
+static void build_codes(const uint8_t bits[16], const uint8_t *vals, HuffCodes *h)
+{
+    memset(h, 0, sizeof(*h));
+    unsigned code = 0, k = 0;
+    for (int l = 1; l <= 16; l++) {
+        for (int i = 0; i < bits[l - 1]; i++, k++) h->cl[vals[k]] = (code++) << 8 | (unsigned)l;
+        code <<= 1;
+    }
+}
+
+/* worst-case coded bytes of one block, stuffing included */
+#define JX_BLOCK_MAX (2 * (22 + 63 * 26 + 11 + 8) / 8 + 16)
+
+/* one block's Huffman-coded data (T.81 F.1.2): DC difference against *pred, AC run/size */
+static void encode_block(BW *w, const int16_t *z, int *pred, const HuffCodes *dc, const HuffCodes *ac)
+{
+    uint32_t extra;
     int diff = z[0] - *pred;                       /* true DC prediction */
     if (diff > 2047) diff = 2047;                  /* (never reached: |DC| <= 1364) */
     if (diff < -2047) diff = -2047;
     *pred = z[0];
-    const int s = category(diff, &extra);
-    put_bits(o, dc->code[s], dc->len[s]);
-    put_bits(o, extra, s);
+    int s = category(diff, &extra);
+    uint32_t c = dc->cl[s];
+    bw_bits(w, (c >> 8) << s | extra, (int)(c & 0xff) + s);
+    int last = 63;
+    while (last > 0 && z[last] == 0) last--;
     int run = 0;
-    for (int k = 1; k < 64; k++) {
+    for (int k = 1; k <= last; k++) {
         int v = z[k];
-        if (v > 1023) v = 1023;
-        if (v < -1023) v = -1023;
         if (v == 0) {
             run++;
             continue;
         }
+        if (v > 1023) v = 1023;
+        if (v < -1023) v = -1023;
         while (run > 15) {                         /* ZRL */
-            put_bits(o, ac->code[0xf0], ac->len[0xf0]);
+            c = ac->cl[0xf0];
+            bw_bits(w, c >> 8, (int)(c & 0xff));
             run -= 16;
         }
-        const int sa = category(v, &extra);
-        const int sym = run << 4 | sa;
-        put_bits(o, ac->code[sym], ac->len[sym]);
-        put_bits(o, extra, sa);
+        s = category(v, &extra);
+        c = ac->cl[run << 4 | s];
+        bw_bits(w, (c >> 8) << s | extra, (int)(c & 0xff) + s);
         run = 0;
     }
-    if (run) put_bits(o, ac->code[0x00], ac->len[0x00]);   /* EOB */
+    if (last < 63) {                               /* EOB */
+        c = ac->cl[0x00];
+        bw_bits(w, c >> 8, (int)(c & 0xff));
+    }
+}
+
+size_t jpgx_jfif_bound(int width, int height)
+{
+    if (width <= 0 || height <= 0) return 0;
+    /* headers + worst case per block (DC 2+11 bits, 63 AC x (16+10 bits)) + stuffing x2, plus
+     * the restart markers (at most one per MCU row) */
+    const size_t blocks = (size_t)(width / 8 + 1) * (height / 8 + 1) * 3;
+    return 1024 + blocks * 2 * (13 + 63 * 26 + 7) / 8 + 2 * (size_t)(height / 8 + 1);
+}
+
+/* The scan's geometry and tables, shared by the coding threads */
+typedef struct {
+    const int16_t *coef;
+    int hs, vs;
+    size_t bpr, nb, cpr, nbc, mrows;
+    size_t rows_per_interval, nintervals;
+    HuffCodes dc[2], ac[2];
+} Scan;
+
+/* restart intervals [i0, i1) into w: DC predictors reset at each, RSTm after each but the
+ * scan's last (T.81 F.1.2.1.3, B.2.4.4) */
+static void code_intervals(const Scan *S, size_t i0, size_t i1, BW *w)
+{
+    for (size_t iv = i0; iv < i1 && !w->oom; iv++) {
+        int pred[3] = {0, 0, 0};
+        const size_t r0 = iv * S->rows_per_interval;
+        size_t r1 = r0 + S->rows_per_interval;
+        if (r1 > S->mrows) r1 = S->mrows;
+        for (size_t my = r0; my < r1; my++) {
+            if (!bw_reserve(w, S->cpr * (size_t)(S->hs * S->vs + 2) * JX_BLOCK_MAX)) return;
+            for (size_t mx = 0; mx < S->cpr; mx++) {
+                /* MCU: hs x vs luma blocks (raster within the MCU), then Cb, then Cr (T.81 A.2.3) */
+                for (int dy = 0; dy < S->vs; dy++)
+                    for (int dx = 0; dx < S->hs; dx++) {
+                        const size_t yb = (my * S->vs + dy) * S->bpr + mx * S->hs + dx;
+                        encode_block(w, S->coef + yb * 64, &pred[0], &S->dc[0], &S->ac[0]);
+                    }
+                const size_t cb = my * S->cpr + mx;
+                encode_block(w, S->coef + (S->nb + cb) * 64, &pred[1], &S->dc[1], &S->ac[1]);
+                encode_block(w, S->coef + (S->nb + S->nbc + cb) * 64, &pred[2], &S->dc[1], &S->ac[1]);
+            }
+        }
+        if (!bw_reserve(w, 16)) return;
+        bw_flush(w);
+        if (iv + 1 < S->nintervals) {
+            w->p[w->n++] = 0xff;
+            w->p[w->n++] = (uint8_t)(0xd0 + (iv & 7));
+        }
+    }
+}
+
+typedef struct {
+    const Scan *S;
+    size_t i0, i1;
+    BW w;
+} Job;
+
+static void *job_main(void *arg)
+{
+    Job *j = (Job *)arg;
+    code_intervals(j->S, j->i0, j->i1, &j->w);
+    return NULL;
 }
 
 int jpgx_write_jfif(const int16_t *coef, int width, int height, int quality, uint8_t *out,
                     size_t cap, size_t *len)
 {
-    return jpgx_write_jfif_sub(coef, width, height, quality, 0, out, cap, len);
+    return jpgx_write_jfif_ex(coef, width, height, quality, 0, 0, 1, out, cap, len);
 }
 
 int jpgx_write_jfif_sub(const int16_t *coef, int width, int height, int quality,
                         int sample_ratio, uint8_t *out, size_t cap, size_t *len)
 {
+    return jpgx_write_jfif_ex(coef, width, height, quality, sample_ratio, 0, 1, out, cap, len);
+}
+
+int jpgx_write_jfif_ex(const int16_t *coef, int width, int height, int quality, int sample_ratio,
+                       int restart_rows, int nthreads, uint8_t *out, size_t cap, size_t *len)
+{
     if (!coef || !out || width <= 0 || height <= 0 || width % 8 || height % 8 ||
-        width > 65535 || height > 65535 || sample_ratio < 0 || sample_ratio > 2)
+        width > 65535 || height > 65535 || sample_ratio < 0 || sample_ratio > 2 ||
+        restart_rows < -1 || nthreads < 0)
         return JPGX_EARG;
     const int hs = sample_ratio ? 2 : 1, vs = sample_ratio == 2 ? 2 : 1;   /* Y sampling */
     if (width % (8 * hs) || height % (8 * vs)) return JPGX_EGEOMETRY;
@@ -194,8 +312,43 @@ int jpgx_write_jfif_sub(const int16_t *coef, int width, int height, int quality,
     if (jpgx_scale_table(0, quality, qs[0]) || jpgx_scale_table(1, quality, qs[1]))
         return JPGX_EQUALITY;
     static const int scan[8][8] = JX_SCAN_ORDER_INIT;
-    Out o = {out, 0, cap, 0, 0, 0};
 
+    Scan S;
+    S.coef = coef;
+    S.hs = hs;
+    S.vs = vs;
+    S.bpr = (size_t)(width / 8);
+    S.nb = S.bpr * (size_t)(height / 8);
+    S.cpr = S.bpr / (size_t)hs;
+    S.mrows = (size_t)(height / 8 / vs);
+    S.nbc = S.cpr * S.mrows;                               /* chroma planes' blocks */
+    long T = nthreads;
+    if (T == 0) {
+        T = sysconf(_SC_NPROCESSORS_ONLN);
+        if (T < 1) T = 1;
+        if (T > 64) T = 64;
+    }
+    /* restart interval: rows of MCUs, Ri = rows x MCUs per row (a 16-bit field) */
+    const size_t maxrows = 65535 / S.cpr;
+    size_t rr = 0;
+    if (restart_rows > 0) {
+        rr = (size_t)restart_rows;
+        if (rr > maxrows) return JPGX_EARG;
+    } else if (restart_rows == -1) {                       /* auto: ~4 intervals per thread */
+        rr = (S.mrows + 4 * (size_t)T - 1) / (4 * (size_t)T);
+        if (rr > maxrows) rr = maxrows;
+        if (rr < 1) rr = 1;
+    }
+    S.rows_per_interval = rr ? rr : S.mrows;
+    S.nintervals = (S.mrows + S.rows_per_interval - 1) / S.rows_per_interval;
+    if ((size_t)T > S.nintervals) T = (long)S.nintervals;
+    build_codes(kDcLumBits, kDcVals, &S.dc[0]);
+    build_codes(kDcChrBits, kDcVals, &S.dc[1]);
+    build_codes(kAcLumBits, kAcLumVals, &S.ac[0]);
+    build_codes(kAcChrBits, kAcChrVals, &S.ac[1]);
+
+    /* headers */
+    Out o = {out, 0, cap, 0};
     put_u16(&o, 0xffd8);                                   /* SOI */
     put_u16(&o, 0xffe0);                                   /* APP0 JFIF 1.01 */
     put_u16(&o, 16);
@@ -243,6 +396,11 @@ int jpgx_write_jfif_sub(const int16_t *coef, int width, int height, int quality,
     put_dht(&o, 0x10, kAcLumBits, kAcLumVals);
     put_dht(&o, 0x01, kDcChrBits, kDcVals);
     put_dht(&o, 0x11, kAcChrBits, kAcChrVals);
+    if (rr) {                                              /* DRI (T.81 B.2.4.4) */
+        put_u16(&o, 0xffdd);
+        put_u16(&o, 4);
+        put_u16(&o, (unsigned)(rr * S.cpr));
+    }
     put_u16(&o, 0xffda);                                   /* SOS */
     put_u16(&o, 6 + 2 * 3);
     put_byte(&o, 3);
@@ -254,30 +412,38 @@ int jpgx_write_jfif_sub(const int16_t *coef, int width, int height, int quality,
     put_byte(&o, 63);
     put_byte(&o, 0);
 
-    HuffCodes dc[2], ac[2];
-    build_codes(kDcLumBits, kDcVals, &dc[0]);
-    build_codes(kDcChrBits, kDcVals, &dc[1]);
-    build_codes(kAcLumBits, kAcLumVals, &ac[0]);
-    build_codes(kAcChrBits, kAcChrVals, &ac[1]);
-    const size_t bpr = (size_t)(width / 8), nb = bpr * (height / 8);
-    const size_t cpr = bpr / hs, nbc = cpr * (height / 8 / vs);  /* chroma planes' blocks */
-    int pred[3] = {0, 0, 0};
-    /* MCU: hs x vs luma blocks (raster within the MCU), then Cb, then Cr (T.81 A.2.3) */
-    for (size_t my = 0; my < (size_t)(height / 8 / vs); my++)
-        for (size_t mx = 0; mx < cpr; mx++) {
-            for (int dy = 0; dy < vs; dy++)
-                for (int dx = 0; dx < hs; dx++) {
-                    const size_t yb = (my * vs + dy) * bpr + mx * hs + dx;
-                    encode_block(&o, coef + yb * 64, &pred[0], &dc[0], &ac[0]);
-                }
-            const size_t cb = my * cpr + mx;
-            encode_block(&o, coef + (nb + cb) * 64, &pred[1], &dc[1], &ac[1]);
-            encode_block(&o, coef + (nb + nbc + cb) * 64, &pred[2], &dc[1], &ac[1]);
+    /* the scan: thread t codes intervals [t NI / T, (t + 1) NI / T) into its own buffer */
+    Job *jobs = (Job *)calloc((size_t)T, sizeof(Job));
+    pthread_t *tid = (pthread_t *)calloc((size_t)T, sizeof(pthread_t));
+    int rc = (jobs && tid) ? JPGX_OK : JPGX_ENOMEM;
+    long started = 0;
+    for (long t = 0; t < T && !rc; t++) {
+        jobs[t].S = &S;
+        jobs[t].i0 = (size_t)t * S.nintervals / (size_t)T;
+        jobs[t].i1 = (size_t)(t + 1) * S.nintervals / (size_t)T;
+        if (t == 0) continue;                              /* the calling thread codes job 0 */
+        if (pthread_create(&tid[t], NULL, job_main, &jobs[t])) rc = JPGX_ENOMEM;
+        else started = t;
+    }
+    if (!rc) job_main(&jobs[0]);
+    for (long t = 1; t <= started; t++) pthread_join(tid[t], NULL);
+    for (long t = 0; t < T && !rc; t++)
+        if (jobs[t].w.oom) rc = JPGX_ENOMEM;
+    if (!rc) {
+        for (long t = 0; t < T; t++) {
+            if (o.n + jobs[t].w.n <= o.cap) memcpy(o.p + o.n, jobs[t].w.p, jobs[t].w.n);
+            else o.overflow = 1;
+            o.n += jobs[t].w.n;
         }
-    flush_bits(&o);
-    put_u16(&o, 0xffd9);                                   /* EOI */
-    if (len) *len = o.n;
-    return o.overflow ? JPGX_EARG : JPGX_OK;
+        put_u16(&o, 0xffd9);                               /* EOI */
+        if (len) *len = o.n;
+        if (o.overflow) rc = JPGX_EARG;
+    }
+    if (jobs)
+        for (long t = 0; t < T; t++) free(jobs[t].w.p);
+    free(jobs);
+    free(tid);
+    return rc;
 }
 
 int jpgx_encode_rgb_to_jpeg(const uint8_t *rgb, int width, int height, size_t pitch,

@@ -49,7 +49,7 @@ COMPAT_EXPORTS = [
     "jpgx_fill_jpgdata", "jpgx_free_jpgdata", "jpgx_dpcm", "jpgx_dpcm_dc", "jpgx_bmp_read",
     "jpgx_free", "jpgx_encode_bmp", "jpgx_jfif_bound", "jpgx_write_jfif",
     "jpgx_encode_bmp_to_jpeg", "jpgx_write_jfif_sub", "jpgx_encode_bmp_to_jpeg_ex",
-    "jpgx_encode_rgb_to_jpeg",
+    "jpgx_encode_rgb_to_jpeg", "jpgx_write_jfif_ex",
 ]
 
 
@@ -332,7 +332,8 @@ class HostContext:
             if len(devices) != nshards:
                 raise ValueError("one device per shard")
             arr = (ctypes.c_int * nshards)(*devices)
-        _check(lib.jpgx_host_create(ctypes.byref(self._h), nshards,
+        self._lib = lib                           # the library that owns the handle
+        _check(self._lib.jpgx_host_create(ctypes.byref(self._h), nshards,
                                     ctypes.cast(arr, ctypes.c_void_p) if arr is not None else None,
                                     chunk_rows), "jpgx_host_create")
         self.nshards = nshards
@@ -353,13 +354,13 @@ class HostContext:
             out = np.empty(shape, np.int16)
         elif out.shape != shape or out.dtype != np.int16 or not out.flags.c_contiguous:
             raise ValueError(f"out must be a contiguous int16 array of shape {shape}")
-        _check(lib.jpgx_host_blocks(self._h, rgb.ctypes.data, W, H, rgb.strides[0],
+        _check(self._lib.jpgx_host_blocks(self._h, rgb.ctypes.data, W, H, rgb.strides[0],
                                     ctypes.byref(p), out.ctypes.data), "jpgx_host_blocks")
         return out
 
     def close(self) -> None:
         if self._h:
-            lib.jpgx_host_destroy(self._h)
+            self._lib.jpgx_host_destroy(self._h)
             self._h = ctypes.c_void_p()
 
     def __enter__(self):

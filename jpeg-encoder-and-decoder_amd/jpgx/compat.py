@@ -87,6 +87,8 @@ def _setup(L):
     L.jpgx_write_jfif.argtypes = [vp, i, i, i, vp, ctypes.c_size_t,
                                   ctypes.POINTER(ctypes.c_size_t)]
     L.jpgx_encode_bmp_to_jpeg.argtypes = [ctypes.c_char_p, ctypes.c_char_p, i, i]
+    L.jpgx_write_jfif_ex.argtypes = [vp, i, i, i, i, i, i, vp, ctypes.c_size_t,
+                                     ctypes.POINTER(ctypes.c_size_t)]
     L.jpgx_encode_rgb_to_jpeg.argtypes = [vp, i, i, ctypes.c_size_t, ctypes.c_char_p, i, i,
                                           ctypes.c_uint, i]
 
@@ -232,6 +234,27 @@ def write_jfif(coef: np.ndarray, width: int, height: int, quality: int) -> bytes
                                ctypes.cast(buf, ctypes.c_void_p), cap, ctypes.byref(n)),
            "jpgx_write_jfif")
     return bytes(buf[:n.value])
+
+
+def write_jfif_ex(coef: np.ndarray, width: int, height: int, quality: int, sample_ratio: int = 0,
+                  restart_rows: int = -1, nthreads: int = 0, cap: int | None = None) -> bytes:
+    """jpgx_write_jfif_ex: restart intervals of `restart_rows` MCU rows (-1 auto, 0 none) coded on
+    `nthreads` host threads (0: one per CPU).  `cap`: output buffer size (default: grown on
+    demand from the size the library reports)."""
+    coef = np.ascontiguousarray(coef, np.int16)
+    n = ctypes.c_size_t()
+    cap = cap or max(1 << 20, coef.size // 2)
+    for _ in range(2):
+        buf = np.empty(cap, np.uint8)
+        rc = lib.jpgx_write_jfif_ex(coef.ctypes.data, width, height, quality, sample_ratio,
+                                    restart_rows, nthreads, buf.ctypes.data, cap, ctypes.byref(n))
+        if rc == 0:
+            return buf[:n.value].tobytes()
+        if rc != -4 or n.value <= cap:                      # JPGX_EARG with the size needed
+            break
+        cap = n.value
+    _check(rc, "jpgx_write_jfif_ex")
+    raise JpgxError(rc, "jpgx_write_jfif_ex")
 
 
 def write_jfif_sub(coef: np.ndarray, width: int, height: int, quality: int,

@@ -1,5 +1,5 @@
 """Minimal baseline-JPEG entropy decoder (test helper): parses the markers jpgx_write_jfif
-emits (SOF0, or SOF1 with 16-bit DQT, DHT, one interleaved SOS, no restart markers) and returns the quantised
+emits (SOF0, or SOF1 with 16-bit DQT, DHT, DRI with RSTm markers, one interleaved SOS) and returns the quantised
 zig-zag coefficients [ncomp][nblocks][64] (a list [Y, Cb, Cr] for 4:2:2 / 4:2:0) and the
 DQT tables -- an independent check of the
 writer, written from ITU-T T.81 (Annex C canonical codes, F.2.2 decoding, F.1.2.3 stuffing)."""
@@ -25,6 +25,13 @@ class _Bits:
             self.acc, self.n = b, 8
         self.n -= 1
         return (self.acc >> self.n) & 1
+
+    def restart(self, m):
+        """byte-align, then the RSTm marker (T.81 F.2.2.5)"""
+        self.n = 0
+        assert self.d[self.i] == 0xFF and self.d[self.i + 1] == 0xD0 + (m & 7), \
+            f"expected RST{m & 7} at {self.i}"
+        self.i += 2
 
     def bits(self, k):
         v = 0
@@ -62,7 +69,7 @@ def decode(data: bytes):
     b = bytes(data)
     assert b[:2] == b"\xff\xd8", "no SOI"
     i = 2
-    dqt, dht, comps, W, H, sof = {}, {}, [], 0, 0, None
+    dqt, dht, comps, W, H, sof, ri = {}, {}, [], 0, 0, None, 0
     while True:
         assert b[i] == 0xFF
         m = b[i + 1]
@@ -90,6 +97,8 @@ def decode(data: bytes):
             H, W = _u16(seg, 1), _u16(seg, 3)
             comps = [(seg[6 + 3 * k], seg[7 + 3 * k], seg[8 + 3 * k]) for k in range(seg[5])]
             assert all(c[1] == 0x11 for c in comps[1:]), "chroma must be sampled 1x1"
+        elif m == 0xDD:                                # DRI (T.81 B.2.4.4)
+            ri = _u16(seg, 0)
         elif m == 0xDA:
             ns = seg[0]
             sel = [(seg[1 + 2 * k], seg[2 + 2 * k]) for k in range(ns)]
@@ -123,8 +132,14 @@ def decode(data: bytes):
             dst[k] = _extend(br.bits(s), s)
             k += 1
 
+    nmcu, nrst = 0, 0
     for my in range(crows):                            # MCUs (T.81 A.2.3)
         for mx in range(cpr):
+            if ri and nmcu and nmcu % ri == 0:         # restart interval boundary
+                br.restart(nrst)
+                nrst += 1
+                pred = [0] * len(sel)
+            nmcu += 1
             for c, (_, tables) in enumerate(sel):
                 if c == 0:
                     for dy in range(vs):
@@ -137,4 +152,5 @@ def decode(data: bytes):
     rest = br.d[br.i:]
     assert rest[-2:] == b"\xff\xd9", "no EOI after the scan"
     return {"width": W, "height": H, "coef": out, "dqt": dqt, "sof": sof,
-            "qsel": [c[2] for c in comps], "sampling": (hs, vs)}
+            "qsel": [c[2] for c in comps], "sampling": (hs, vs), "restart_interval": ri,
+            "restarts": nrst}

@@ -109,3 +109,34 @@ def test_entropy_stats_stitch_across_stripes(frame):
     tot = ha.cpu().numpy().astype(np.int64) + hb.cpu().numpy()
     tot[:, 256] -= 1                        # freq[256] = 1 once per huffman_encode call
     assert np.array_equal(tot, hist_all.cpu().numpy())
+
+
+def test_jfif_stitch_of_the_stripes(frame, ref):
+    """The host entropy stage of configs[4]: the 16384^2 frame's coefficients
+    -> one JFIF with restart intervals of 16 MCU rows (DRI = 32768 MCUs; every GPU stripe
+    boundary, 256 rows, is an interval boundary), coded on 8 host threads -- one per stripe -- and
+    concatenated; the independent T.81 decoder (tests/c/jfif_dec.c, 8 threads over the RSTm
+    markers) returns every coefficient: the whole-frame hash of the real reference.  Parity of
+    the bitstream itself is unpinned (the reference's Huffman stage never terminates)."""
+    import time
+
+    import jpgx.compat as C
+    from test_jfif_restart import jfd_decode
+    import ctypes
+    import subprocess
+    from conftest import REPO
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "c"), "jfd"], check=True)
+    lib = ctypes.CDLL(os.path.join(REPO, "tests", "c", "_build", "libjfd.so"))
+    lib.jfd_decode.restype = ctypes.c_int
+    lib.jfd_decode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                               ctypes.c_int, ctypes.c_void_p]
+    _, out, _ = frame
+    coef = out.cpu().numpy()
+    t0 = time.perf_counter()
+    data = C.write_jfif_ex(coef, W, H, Q, 0, restart_rows=16, nthreads=NGPU, cap=coef.nbytes // 2)
+    dt = time.perf_counter() - t0
+    print(f"\n16384^2 q{Q}: JFIF {len(data) / 1e6:.1f} MB in {dt:.2f} s on {NGPU} threads "
+          f"({W * H / dt / 1e6:.0f} Mpx/s)")
+    got, info = jfd_decode(lib, data, coef.size, NGPU)
+    assert info[4] == 16 * (W // 8) and info[5] == (H // 8) // 16 - 1
+    assert hashlib.sha256(got.astype("<i2").tobytes()).hexdigest() == ref["coef_sha256"]

@@ -19,9 +19,9 @@ def test_mfma_operand_rule(tmp_path):
                     os.path.join(PKG, "csrc", "jpgx_mx.hip"), "-o", str(asm)],
                    check=True, capture_output=True)
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), str(asm),
-                        "k_mx", "k_mx422", "k_mx420"], capture_output=True, text=True)
+                        "k_mx", "k_mxs", "k_mx422", "k_mx420"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
-    assert r.stdout.count("0 load(s) into live MFMA operands") == 3, r.stdout
+    assert r.stdout.count(" 0 load(s) into live MFMA operands") == 4, r.stdout
 
 
 def test_mfma_operand_rule_catches_a_violation(tmp_path):
@@ -36,4 +36,54 @@ def test_mfma_operand_rule_catches_a_violation(tmp_path):
         ".Lfunc_end0:", ""]))
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), str(s), "k_mx"],
                        capture_output=True, text=True)
+    assert r.returncode == 1 and "1 load(s)" in r.stdout, r.stdout
+
+
+def _check_fake(tmp_path, lines):
+    s = tmp_path / "fake.s"
+    s.write_text("\n".join(["_ZN12_GLOBAL__N_14k_mxE13jx_xform_args:"] + lines + [".Lfunc_end0:", ""]))
+    return subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), str(s), "k_mx"],
+                          capture_output=True, text=True)
+
+
+def test_mfma_operand_rule_follows_branches_and_back_edges(tmp_path):
+    """the checker walks the control-flow graph: a load reached only through a taken branch, or
+    only around the loop back-edge (the next iteration's first loads into the previous MFMA's
+    operands), is a violation; the same load after a read of the result is not"""
+    taken = _check_fake(tmp_path, [
+        "\tv_mfma_f32_16x16x32_f16 v[8:11], v[0:3], v[4:7], 0",
+        "\ts_cbranch_vccnz .LBB0_2",
+        "\tv_add_f32_e32 v30, v8, v9",
+        "\ts_endpgm",
+        ".LBB0_2:",
+        "\tds_bpermute_b32 v4, v20, v21",
+        "\ts_endpgm"])
+    assert taken.returncode == 1 and "1 load(s)" in taken.stdout, taken.stdout
+    back = _check_fake(tmp_path, [
+        ".LBB0_1:",
+        "\tds_read_b128 v[0:3], v40",
+        "\ts_waitcnt lgkmcnt(0)",
+        "\tv_mfma_f32_16x16x32_f16 v[8:11], v[0:3], v[4:7], 0",
+        "\ts_add_u32 s0, s0, 1",
+        "\ts_cbranch_scc1 .LBB0_1",
+        "\tv_add_f32_e32 v30, v8, v9",
+        "\ts_endpgm"])
+    assert back.returncode == 1 and "1 load(s)" in back.stdout, back.stdout
+    ok = _check_fake(tmp_path, [
+        ".LBB0_1:",
+        "\tds_read_b128 v[0:3], v40",
+        "\ts_waitcnt lgkmcnt(0)",
+        "\tv_mfma_f32_16x16x32_f16 v[8:11], v[0:3], v[4:7], 0",
+        "\tv_mfma_f32_16x16x32_f16 v[12:15], v[0:3], v[4:7], 0",
+        "\tv_readfirstlane_b32 s2, v15",
+        "\ts_cbranch_scc1 .LBB0_1",
+        "\ts_endpgm"])
+    assert ok.returncode == 0, ok.stdout
+
+
+def test_mfma_operand_rule_covers_agprs_and_returning_atomics(tmp_path):
+    r = _check_fake(tmp_path, [
+        "\tv_mfma_f32_16x16x32_f16 a[8:11], v[0:3], v[4:7], a[8:11]",
+        "\tglobal_atomic_add_f32 a8, v[20:21], v22, off sc0",
+        "\tv_accvgpr_read_b32 v30, a8"])
     assert r.returncode == 1 and "1 load(s)" in r.stdout, r.stdout

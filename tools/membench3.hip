@@ -110,7 +110,7 @@ struct Q {
     }
 };
 
-template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM, int WPG = 4>
+template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM, int WPG = 4, int OP = 0>
 __global__ __launch_bounds__(WPG * 64) void k_skel(Args a)
 {
     static_assert(CH > DIST, "the issue cursor is at most one chunk ahead");
@@ -194,8 +194,13 @@ __global__ __launch_bounds__(WPG * 64) void k_skel(Args a)
         for (int i = 0; i < NM; i++)
             macc[i & 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, av, macc[i & 3], 0, 0, 0);
 #pragma unroll
-        for (int i = 0; i < NV; i++)
-            asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(acc[i & 7]) : "v"(k1), "v"(k2));
+        for (int i = 0; i < NV; i++) {
+            if (OP == 0) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(acc[i & 7]) : "v"(k1), "v"(k2));
+            if (OP == 1) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(acc[i & 7]) : "v"(k2));
+            if (OP == 2) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(acc[i & 7].x) : "v"(k1.x), "v"(k2.x));
+            if (OP == 3) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(acc[i & 7].x) : "v"(d.w), "v"(0x05040702u));
+            if (OP == 4) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(acc[i & 7]) : "v"(k1));
+        }
         if (NM) acc[2].x += macc[0].x + macc[1].y + macc[2].z + macc[3].w;
 #pragma unroll
         for (int i = 0; i < NL; i++)
@@ -301,16 +306,16 @@ static void timeit(const char *name, L launch)
 
 static unsigned g_ctr_val = 0, g_stride = 32;
 
-template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM, int WPG = 4>
+template <int NV, int NM, int NL, int CH, int DIST, int NT, int QM, int WPG = 4, int OP = 0>
 static void skel(int wpe, int grid_mult = 1, double static_frac = 0.0, int superchunk = 0)
 {
     char name[160];
-    snprintf(name, sizeof name, "skel v%d m%d l%d c%d d%d nt%d q%d w%d g%d sf%.2f wg%d sc%d", NV, NM, NL, CH, DIST,
-             NT, QM, wpe, grid_mult, static_frac, WPG, superchunk);
+    snprintf(name, sizeof name, "skel v%d m%d l%d c%d d%d nt%d q%d w%d g%d sf%.2f wg%d sc%d op%d", NV, NM, NL, CH, DIST,
+             NT, QM, wpe, grid_mult, static_frac, WPG, superchunk, OP);
     const size_t per_wg = WPG * ((DIST + 1) * kSlot + kStage + 256);
     /* wpe waves per SIMD: wpe * 4 / WPG workgroups per CU */
     const size_t lds = std::max(per_wg, (size_t)(160 * 1024 * WPG / (4 * wpe) - 64) & ~(size_t)15);
-    auto kern = k_skel<NV, NM, NL, CH, DIST, NT, QM, WPG>;
+    auto kern = k_skel<NV, NM, NL, CH, DIST, NT, QM, WPG, OP>;
     CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const unsigned nsteps = 8 * kStepsPerFrame, nchunks = nsteps / CH;
     unsigned grid = g_cus * wpe * 4 / WPG * grid_mult;
@@ -453,6 +458,50 @@ int main(int argc, char **argv)
         skel<192, 16, 24, 4, 2, 1, 0>(3);
         skel<192, 16, 24, 4, 2, 1, 10, 12>(3);
         skel<192, 16, 24, 4, 2, 1, 10, 16>(4);
+    }
+    if (!strcmp(which, "r4b")) {
+        /* the VALU cliff: persistent vs non-persistent at 64..192 packed FMAs, and op kinds */
+        skel<0, 0, 0, 3, 2, 1, 0>(4);
+        skel<64, 16, 24, 3, 2, 1, 0>(4);
+        skel<128, 16, 24, 3, 2, 1, 0>(4);
+        skel<160, 16, 24, 3, 2, 1, 0>(4);
+        skel<0, 0, 0, 4, 2, 1, 0>(4, 0);
+        skel<64, 16, 24, 4, 2, 1, 0>(4, 0);
+        skel<128, 16, 24, 4, 2, 1, 0>(4, 0);
+        skel<144, 16, 24, 4, 2, 1, 0>(4, 0);
+        skel<160, 16, 24, 4, 2, 1, 0>(4, 0);
+        skel<176, 16, 24, 4, 2, 1, 0>(4, 0);
+        skel<192, 16, 24, 4, 2, 1, 0>(4, 0);
+        skel<128, 16, 24, 2, 1, 1, 0>(4, 0);
+        skel<128, 16, 24, 6, 2, 1, 0>(4, 0);
+        skel<192, 16, 24, 4, 2, 1, 0, 4, 1>(4, 0);   /* pk_add */
+        skel<192, 16, 24, 4, 2, 1, 0, 4, 4>(4, 0);   /* pk_mul */
+        skel<192, 16, 24, 4, 2, 1, 0, 4, 2>(4, 0);   /* scalar fma */
+        skel<192, 16, 24, 4, 2, 1, 0, 4, 3>(4, 0);   /* perm */
+        skel<128, 16, 48, 4, 2, 1, 0>(4, 0);         /* 48 LDS writes */
+        skel<128, 16, 24, 4, 2, 1, 0>(3, 0);
+        skel<128, 16, 24, 4, 2, 1, 0>(2, 0);
+    }
+    if (!strcmp(which, "r4")) {
+        /* round 4: non-persistent grids (one chunk per wave) with random-operand compute, and the
+         * VALU -> MFMA trade (same memory pattern, 4 waves per SIMD) */
+        skel<0, 0, 0, 3, 2, 1, 0>(4);              /* persistent, memory only */
+        skel<192, 16, 24, 3, 2, 1, 0>(4);          /* persistent, k_mx-sized compute */
+        skel<0, 0, 0, 3, 2, 1, 0>(4, 0);           /* non-persistent, memory only */
+        skel<0, 0, 0, 8, 2, 1, 0>(4, 0);
+        skel<192, 16, 24, 3, 2, 1, 0>(4, 0);       /* non-persistent, k_mx-sized compute */
+        skel<192, 16, 24, 4, 2, 1, 0>(4, 0);
+        skel<192, 16, 24, 8, 2, 1, 0>(4, 0);
+        skel<192, 16, 24, 16, 2, 1, 0>(4, 0);
+        skel<128, 16, 24, 4, 2, 1, 0>(4, 0);
+        skel<96, 16, 24, 4, 2, 1, 0>(4, 0);
+        skel<64, 16, 24, 4, 2, 1, 0>(4, 0);
+        skel<96, 40, 24, 4, 2, 1, 0>(4, 0);        /* column pass on the matrix cores: fewer VALU, more MFMA */
+        skel<64, 64, 24, 4, 2, 1, 0>(4, 0);
+        skel<64, 88, 24, 4, 2, 1, 0>(4, 0);
+        skel<96, 40, 24, 3, 2, 1, 0>(4);
+        skel<64, 64, 24, 3, 2, 1, 0>(4);
+        skel<192, 16, 24, 4, 2, 2, 0>(4, 0);       /* zero operands */
     }
     return 0;
 }

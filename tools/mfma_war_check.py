@@ -8,25 +8,29 @@ the MFMA has read its last 16-lane group of SrcC (C rows 12..15) when the matrix
 up -- nondeterministic wrong rows 12..15 (Y blocks 3 / 7 of a step), seen in k_mx422 / k_mx420
 (profiles/r03_mfma_war.txt).  The compiler's wait states cover VALU writes, not this.
 
-Rule checked: between an MFMA and the first non-MFMA instruction that reads its result (which
-waits for it, so the MFMA has read every operand), no load (ds_read*, global_load*, buffer_load*,
-scratch_load*, flat_load*) may write any of its SrcA / SrcB / SrcC registers.  The scan follows
-the .s text linearly from each MFMA (fall-through order) for up to LIMIT instructions.
+Rule checked: on every control-flow path from an MFMA (fall-through, taken branches and loop
+back-edges: a walk over the .LBB basic blocks) up to the first non-MFMA instruction that reads its
+result or the result of a later MFMA (which waits for it; a wave's MFMAs complete in issue order,
+so then this one has read every operand), no instruction that writes VGPRs
+from memory -- LDS reads, permutes / swizzles, LDS or global atomics with return, global /
+buffer / flat / scratch / image loads -- may write any of its SrcA / SrcB / SrcC registers (VGPRs
+or AGPRs).  A path is followed for at most LIMIT instructions.
 Usage: python tools/mfma_war_check.py FILE.s [kernel ...]   (exit status 1 on a violation)
 """
 import re
 import sys
 
 LIMIT = 400
-LOADS = ("ds_read", "global_load", "buffer_load", "scratch_load", "flat_load")
+BRANCH = re.compile(r"^s_(c?branch\w*|setpc\w*|cbranch\w*)$")
 
 
 def regs(s):
+    """the register names an operand list mentions: ('v', n) and ('a', n)"""
     out = set()
-    for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", s):
-        out |= set(range(int(a), int(b) + 1))
-    for a in re.findall(r"\bv(\d+)\b", s):
-        out.add(int(a))
+    for k, a, b in re.findall(r"\b([va])\[(\d+):(\d+)\]", s):
+        out |= {(k, i) for i in range(int(a), int(b) + 1)}
+    for k, a in re.findall(r"\b([va])(\d+)\b", s):
+        out.add((k, int(a)))
     return out
 
 
@@ -37,47 +41,84 @@ def operands(t):
     return p[0], [o.strip() for o in re.split(r",(?![^\[]*\])", p[1])]
 
 
+def writes_from_memory(op):
+    """instructions whose VGPR destination is written when memory returns (asynchronously)"""
+    if op.startswith("ds_"):
+        return (op.startswith(("ds_read", "ds_bpermute", "ds_permute", "ds_swizzle", "ds_consume",
+                               "ds_append")) or "_rtn" in op)
+    if op.startswith(("global_", "buffer_", "flat_", "scratch_")):
+        return "load" in op or "atomic" in op
+    return op.startswith("image_")
+
+
 def kernel_body(text, name):
+    """(instructions, label -> index) of one kernel"""
     m = re.search(r"^(_Z[^\s:]*\d%sE[^\s:]*):" % re.escape(name), text, re.M)
     if not m:
-        return None
+        return None, None
     end = text.find(".Lfunc_end", m.end())
-    ins = []
+    ins, labels = [], {}
     for ln in text[m.end():end].splitlines():
         t = ln.split(";")[0].strip()
-        if not t or t.startswith("."):
+        if not t:
+            continue
+        lm = re.match(r"^(\.LBB\w+):", t)
+        if lm:
+            labels[lm.group(1)] = len(ins)
+            continue
+        if t.startswith("."):
             continue
         ins.append(t)
-    return ins
+    return ins, labels
 
 
-def check(ins):
+def successors(ins, labels, j):
+    """next instruction indices after ins[j] on any path"""
+    op, ops = operands(ins[j])
+    if op == "s_endpgm" or op.startswith("s_setpc") or op == "s_trap":
+        return []
+    if op == "s_branch":
+        return [labels[ops[0]]] if ops and ops[0] in labels else []
+    out = [j + 1] if j + 1 < len(ins) else []
+    if op.startswith("s_cbranch") and ops and ops[0] in labels:
+        out.append(labels[ops[0]])
+    return out
+
+
+def check(ins, labels):
     bad = []
     for i, t in enumerate(ins):
         op, ops = operands(t)
         if not op.startswith("v_mfma"):
             continue
-        dst = regs(ops[0])          # registers whose first VALU read implies this MFMA is done
         src = regs(",".join(ops[1:]))
-        for j in range(i + 1, min(len(ins), i + LIMIT)):
+        # paths: (next index, registers whose read implies completion, steps taken)
+        stack = [(k, frozenset(regs(ops[0])), 1) for k in successors(ins, labels, i)]
+        seen = set()
+        found = {}
+        while stack:
+            j, dst, n = stack.pop()
+            if n > LIMIT or (j, dst) in seen:
+                continue
+            seen.add((j, dst))
             u = ins[j]
             uop, uops = operands(u)
-            if not uops:
-                continue
+            done = False
             if uop.startswith("v_mfma"):
-                # a chained product reading this result: its completion implies this one's
-                if regs(",".join(uops[1:])) & dst:
-                    dst = dst | regs(uops[0])
-                continue
-            if uop.startswith(LOADS):
+                # a later product: the matrix pipe completes a wave's MFMAs in issue order, so
+                # a read of ITS result implies this one is done too (mx_fence relies on it)
+                dst = dst | frozenset(regs(uops[0]))
+            elif uops and writes_from_memory(uop):
                 hit = regs(uops[0]) & src
-                if hit:
-                    bad.append((i, j, t, u, sorted(hit)))
-                continue
-            if uop.startswith(("v_", "ds_write", "global_store", "buffer_store")):
+                if hit and j not in found:
+                    found[j] = (i, j, t, u, sorted(hit))
+            elif uop.startswith(("v_", "ds_write", "global_store", "buffer_store", "flat_store",
+                                 "scratch_store")) and uops:
                 reads = regs(",".join(uops[1:])) if uop.startswith("v_") else regs(",".join(uops))
-                if reads & dst:
-                    break      # the result is read: the MFMA has completed
+                done = bool(reads & dst)          # the result is read: the MFMA has completed
+            if not done:
+                stack.extend((k, dst, n + 1) for k in successors(ins, labels, j))
+        bad.extend(found[j] for j in sorted(found))
     return bad
 
 
@@ -87,15 +128,15 @@ def main():
     text = open(path).read()
     rc = 0
     for n in names:
-        ins = kernel_body(text, n)
+        ins, labels = kernel_body(text, n)
         if ins is None:
             print(f"{n}: not found")
             rc = 1
             continue
-        bad = check(ins)
+        bad = check(ins, labels)
         print(f"{n}: {sum(1 for x in ins if x.startswith('v_mfma'))} MFMAs, {len(bad)} load(s) into live MFMA operands")
         for i, j, t, u, hit in bad[:12]:
-            print(f"   {j - i - 1:3d} instrs after  {t[:64]}\n         {u[:64]}  -> v{hit}")
+            print(f"   at {j} after the MFMA at {i}: {t[:64]}\n         {u[:64]}  -> {hit}")
         rc |= 1 if bad else 0
     sys.exit(rc)
 
