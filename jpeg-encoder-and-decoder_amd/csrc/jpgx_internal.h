@@ -50,6 +50,12 @@ struct jx_limtab {
 #define JX_MX_PARTS 2       /* 2: hi + one lo part (band 1.28x that of 3 parts, 16 MFMAs per
                                8 blocks instead of 24: jpgx_plan.cpp's bound covers either) */
 #endif
+/* scale of the lo f16 parts of B (exponent): 0 stores them at the hi parts' scale, so R = acc_h +
+ * acc_l is one add (round 4); 12 stores them x 2^12 (R = fma(acc_l, 2^-12, acc_h), rounds 2-3).
+ * Either way R = fl(acc_h + acc_l) bit for bit. */
+#ifndef JX_MX_LOEXP
+#define JX_MX_LOEXP 0
+#endif
 struct jx_mxtab {
     float w[24][8];         /* 1/4 a(u) a(v) k(v) / Q[u][v] (row transform uses exact cosines) */
     float lsq[24][8];       /* a float <= lim^2 of the rigorous band (flag: d*d - lsq >= 0);
@@ -77,6 +83,7 @@ void jx_under_dwords(const uint8_t under[3][8], uint32_t out[6]);
 /* packed-pair vs scalar transform, bit for bit (host; returns the mismatch count) */
 long long jx_selftest_pk(long long nblocks, unsigned long long seed);
 int jx_mx_parts(void);
+int jx_mx_loexp(void);
 /* k_mx: tables and f16 B operands (host plan), launch (device side) */
 int jx_plan_tables_mx(int quality, float w[24][8], float lim[24][8], int16_t q[2][64]);
 int jx_mx_operands(uint16_t ops[3 * JX_MX_PARTS][64][8]);

@@ -570,6 +570,13 @@ __device__ __forceinline__ uint32_t mx_flags(const mx_f2 (&F)[4], const mx_f2 (&
 /* R pairs (y, y+1) of one column from the lo (rows 0..3) and hi (rows 4..7) tiles */
 __device__ __forceinline__ void mx_combine(mx_f4 hl, mx_f4 ll, mx_f4 hh, mx_f4 lh, mx_f2 (&R)[4])
 {
+    if (JX_MX_LOEXP == 0) {                     /* lo parts at the hi scale: fl(acc_h + acc_l) */
+        R[0] = mx_f2{ll.x, ll.y} + mx_f2{hl.x, hl.y};
+        R[1] = mx_f2{ll.z, ll.w} + mx_f2{hl.z, hl.w};
+        R[2] = mx_f2{lh.x, lh.y} + mx_f2{hh.x, hh.y};
+        R[3] = mx_f2{lh.z, lh.w} + mx_f2{hh.z, hh.w};
+        return;
+    }
     const mx_f2 s = {0x1p-12f, 0x1p-12f};
     R[0] = __builtin_elementwise_fma(mx_f2{ll.x, ll.y}, s, mx_f2{hl.x, hl.y});
     R[1] = __builtin_elementwise_fma(mx_f2{ll.z, ll.w}, s, mx_f2{hl.z, hl.w});
@@ -585,6 +592,28 @@ struct MxW {
 __device__ __forceinline__ MxW mx_w(const MxTab &tb, unsigned t0, unsigned j)
 {
     return MxW{tb.wl[t0][0][j], tb.wl[t0][1][j]};
+}
+/* the squared band limits of a column (table t0 + 1): rare path only */
+__device__ __forceinline__ MxW mx_l(const MxTab &tb, unsigned t0, unsigned j)
+{
+    return MxW{tb.wl[t0 + 1][0][j], tb.wl[t0 + 1][1][j]};
+}
+/* k_mxs with one-wave workgroups: the scales (tables 0 and 2) in the wave's LDS, the limits read
+ * from the global image on the rare path */
+struct MxsScales {
+    mx_f4 w[2][2][16];
+};
+struct MxsTabRef {
+    const MxsScales &s;
+    const MxTab &g;
+};
+__device__ __forceinline__ MxW mx_w(const MxsTabRef &tb, unsigned t0, unsigned j)
+{
+    return MxW{tb.s.w[t0 >> 1][0][j], tb.s.w[t0 >> 1][1][j]};
+}
+__device__ __forceinline__ MxW mx_l(const MxsTabRef &tb, unsigned t0, unsigned j)
+{
+    return MxW{tb.g.wl[t0 + 1][0][j], tb.g.wl[t0 + 1][1][j]};
 }
 
 /*
@@ -623,8 +652,8 @@ __device__ __forceinline__ void mx_fence(const mx_f4 &r)
 /* Column pass of one column (R pairs), quantiser, stage writes at za[v] + OFF, band flags (rare
  * path: the exact per-coefficient test with the limits of table t0 + 1, after mx_fence(*fence)
  * when an MFMA may be in flight) into fl */
-template <unsigned OFF>
-__device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, float limc, const MxTab &tb,
+template <unsigned OFF, class TB>
+__device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, float limc, const TB &tb,
                                              unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc,
                                              const mx_f4 *fence = nullptr)
 {
@@ -646,7 +675,8 @@ __device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, f
     }
     if (__builtin_expect(__ballot(em >= limc) != 0, 0)) {
         if (fence) mx_fence(*fence);
-        const mx_f4 l01 = tb.wl[t0 + 1][0][j], l23 = tb.wl[t0 + 1][1][j];
+        const MxW lw = mx_l(tb, t0, j);
+        const mx_f4 l01 = lw.w01, l23 = lw.w23;
         const mx_f2 Lq[4] = {mx_f2{l01.x, l01.y}, mx_f2{l01.z, l01.w}, mx_f2{l23.x, l23.y}, mx_f2{l23.z, l23.w}};
         fl |= mx_flags(F, W, Lq) << (8 * kc);
     }
@@ -655,8 +685,8 @@ __device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, f
 /* the same from the hi / lo accumulator tiles of rows 0..3 and 4..7; LAZY: the column's scales
  * are read here, after the tiles have been read (and after mx_fence(*fence) when a later MFMA may
  * still be in flight) -- no load meets an MFMA operand */
-template <unsigned OFF, bool LAZY = false>
-__device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t, float limc, const MxTab &tb,
+template <unsigned OFF, bool LAZY = false, class TB>
+__device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t, float limc, const TB &tb,
                                              unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc,
                                              const mx_f4 *fence = nullptr)
 {
@@ -961,11 +991,36 @@ struct alignas(16) MxsImg {
     mx_u4 B[3 * JX_MX_PARTS][64];
     MxTab tab;
     float limc[2][16];
+    uint8_t scan_t[8][8];               /* zig-zag position of (v, u) at [u][v] */
 };
 constexpr unsigned kMxsPieces = sizeof(MxsImg) / 16;
 static_assert(sizeof(MxsImg) % 16 == 0 && kMxsPieces <= 768, "three 16-byte pieces per thread");
 static_assert(sizeof(MxsLds) * 4 + sizeof(MxsImg) <= 40 * 1024, "4 workgroups of 4 waves per CU");
 __device__ MxsImg g_mxs_img[2][JX_MAXQ + 1];     /* [force][quality] */
+/* waves per workgroup: 4 (the image above shared through one s_barrier) or 1 (each wave its own
+ * small image -- the scales, hot-path limits and zig-zag positions -- and its B operands and band
+ * limits from the global image: no barrier, and a finished wave frees its slot at once) */
+#ifndef JX_MXS_WPG
+#define JX_MXS_WPG 4
+#endif
+constexpr unsigned kMxsWPG = JX_MXS_WPG;
+static_assert(kMxsWPG == 1 || kMxsWPG == 4, "k_mxs: 1 or 4 waves per workgroup");
+struct alignas(16) MxsImg1 {
+    MxsScales sc;
+    float limc[2][16];
+    uint8_t scan_t[8][8];
+};
+static_assert(sizeof(MxsImg1) % 16 == 0 && sizeof(MxsImg1) / 16 <= 128, "two 16-byte pieces per lane");
+static_assert(kMxsWPG == 4 || (sizeof(MxsLds) + sizeof(MxsImg1) + 511) / 512 * 512 * 16 <= 160 * 1024,
+              "16 one-wave workgroups per CU");
+__device__ MxsImg1 g_mxs_img1[2][JX_MAXQ + 1];
+using MxsShared = std::conditional<kMxsWPG == 1, MxsImg1, MxsImg>::type;
+/* where the B operands and the column tables come from (four-wave image / one-wave image) */
+typedef mx_u4 MxsBOps[3 * JX_MX_PARTS][64];
+__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg &l, const MxsImg &) { return l.B; }
+__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg1 &, const MxsImg &g) { return g.B; }
+__device__ __forceinline__ const MxTab &mxs_tb(const MxsImg &l, const MxsImg &) { return l.tab; }
+__device__ __forceinline__ MxsTabRef mxs_tb(const MxsImg1 &l, const MxsImg &g) { return MxsTabRef{l.sc, g.tab}; }
 #ifdef JX_MXS_STAMP                    /* timing probe builds only: per-wave timestamps */
 __device__ unsigned long long g_mxs_ts[1u << 20];
 #define JX_MXS_TS(i, v) do { if (lane == 0 && 8u * wv + 8u <= (1u << 20)) g_mxs_ts[8u * wv + (i)] = (v); } while (0)
@@ -978,6 +1033,34 @@ __device__ __forceinline__ void mx_wait_vm()
 {
     static_assert(N < 64, "vmcnt is 6 bits");
     __builtin_amdgcn_s_waitcnt((int)((N & 15u) | ((N >> 4) << 14) | 0xF70u));
+}
+
+/* LDS-DMA of 16 (or 4) bytes per lane to lds_base + 16 (4) lane.  JX_MXS_ASMDMA issues it from
+ * inline asm, which the compiler's wait-count pass does not see: then only k_mxs's own counted
+ * vmcnt waits order it (with the builtin, the compiler drains vmcnt(0) before the next LDS read
+ * of the wave, since it cannot tell which LDS bytes the DMA writes). */
+#ifndef JX_MXS_ASMDMA
+#define JX_MXS_ASMDMA 0
+#endif
+template <int SIZE>
+__device__ __forceinline__ void mxs_dma(const void *g, void *lds)
+{
+    static_assert(SIZE == 16 || SIZE == 4, "dwordx4 or dword pieces");
+#if JX_MXS_ASMDMA
+    const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)mx_lds(lds));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    if (SIZE == 16)
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+    else
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+#pragma clang diagnostic pop
+#else
+    if constexpr (SIZE == 16)
+        __builtin_amdgcn_global_load_lds((mx_gp)g, (mx_lp)lds, 16, 0, 0);
+    else
+        __builtin_amdgcn_global_load_lds((mx_gp)g, (mx_lp)lds, 4, 0, 0);
+#endif
 }
 
 /* a step cursor (wave-uniform): launch-global first block, whether the step is simple (one
@@ -1028,18 +1111,18 @@ __device__ __forceinline__ void mxs_issue(const MxsCur &P, const MxG &g, uint8_t
                                           uint32_t off1, unsigned lane)
 {
     if (P.simple) {
-        __builtin_amdgcn_global_load_lds((mx_gp)(P.src + off0), (mx_lp)slot, 16, 0, 0);
-        if (lane < 32) __builtin_amdgcn_global_load_lds((mx_gp)(P.src + off1), (mx_lp)(slot + 1024u), 16, 0, 0);
+        mxs_dma<16>(P.src + off0, slot);
+        if (lane < 32) mxs_dma<16>(P.src + off1, slot + 1024u);
     } else {
-        __builtin_amdgcn_global_load_lds((mx_gp)g.rgb, (mx_lp)slot, 4, 0, 0);
-        __builtin_amdgcn_global_load_lds((mx_gp)g.rgb, (mx_lp)slot, 4, 0, 0);
+        mxs_dma<4>(g.rgb, slot);
+        mxs_dma<4>(g.rgb, slot);
     }
 }
 
-__global__ __launch_bounds__(256, JX_MX_WPE) void k_mxs(const jx_xform_args a)
+__global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_args a)
 {
-    __shared__ __attribute__((aligned(16))) MxsLds s_lds[4];
-    __shared__ __attribute__((aligned(16))) MxsImg s_img;
+    __shared__ __attribute__((aligned(16))) MxsLds s_lds[kMxsWPG];
+    __shared__ __attribute__((aligned(16))) MxsShared s_img;
     MxG g;
     g.rgb = a.g.rgb;
     g.out = a.g.out;
@@ -1060,21 +1143,26 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mxs(const jx_xform_args a)
     const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime(), cs0 = __builtin_amdgcn_s_memtime();
 #endif
     const unsigned lane = threadIdx.x & 63u;
-    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned wave = kMxsWPG == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     MxsLds &L = s_lds[wave];
-    /* the workgroup image into LDS (LDS-DMA: piece p of thread t lands at 16 p) */
-    {
-        const uint8_t *img = (const uint8_t *)&g_mxs_img[g.force ? 1 : 0][g.quality];
+    const MxsImg &gimg = g_mxs_img[g.force ? 1 : 0][g.quality];
+    /* the image into LDS (LDS-DMA: piece p of thread t lands at 16 p) */
+    if constexpr (kMxsWPG == 4) {
+        const uint8_t *img = (const uint8_t *)&gimg;
 #pragma unroll
         for (unsigned i = 0; i < 3; i++) {
             const unsigned piece = 256u * i + threadIdx.x;
             if (256u * i + 64u * wave < kMxsPieces && piece < kMxsPieces)
-                __builtin_amdgcn_global_load_lds((mx_gp)(img + 16u * piece),
-                                                 (mx_lp)((uint8_t *)&s_img + 16u * (256u * i + 64u * wave)), 16, 0, 0);
+                mxs_dma<16>(img + 16u * piece, (uint8_t *)&s_img + 16u * (256u * i + 64u * wave));
         }
+    } else {
+        constexpr unsigned kP1 = sizeof(MxsImg1) / 16;
+        const uint8_t *img = (const uint8_t *)&g_mxs_img1[g.force ? 1 : 0][g.quality];
+        mxs_dma<16>(img + 16u * lane, &s_img);
+        if (lane < kP1 - 64u) mxs_dma<16>(img + 16u * (64u + lane), (uint8_t *)&s_img + 1024u);
     }
     /* this wave's first steps' DMA (kMxsR of them; ring mode: two) */
-    const unsigned wv = blockIdx.x * 4u + wave;
+    const unsigned wv = blockIdx.x * kMxsWPG + wave;
     const uint32_t off0 = (uint32_t)((lane / 12u) * (unsigned)g.pitch + 16u * (lane % 12u));
     const uint32_t off1 = (uint32_t)(((64u + lane) / 12u) * (unsigned)g.pitch + 16u * ((64u + lane) % 12u));
     MxsCur iss;                                  /* issue cursor */
@@ -1097,26 +1185,32 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mxs(const jx_xform_args a)
     const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
     const uint32_t rr = ro + ((lane >> 3) < 4 ? 8u : 16u) * kBS;
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
-    uint32_t za[8];
-    {
-        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * mx_pos(j >> 3, gq);
-#pragma unroll
-        for (int v = 0; v < 8; v++) za[v] = base + 2u * (unsigned)kMxScan[v][u];
-    }
     const jx_mxtab &T = g_mxtab[g.force ? 1 : 0][g.quality];
 
     /* the image has landed (it is older than the prologue's pixel operations), in every wave */
+    if constexpr (kMxsWPG == 1) {
+        if (cmp.b >= g.total) return;
+    }
     mx_wait_vm<2u * kPro>();
-    __builtin_amdgcn_s_barrier();
+    if constexpr (kMxsWPG == 4) __builtin_amdgcn_s_barrier();
     mx_wave_sync();
     if (cmp.b >= g.total) return;
+    /* stage addresses of this lane's column at v = 0..7: the zig-zag positions from the image (no
+     * global load: its wait would drain the pixel DMA too) */
+    uint32_t za[8];
+    {
+        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * mx_pos(j >> 3, gq);
+        const mx_u2 sc = *(const mx_u2 *)&s_img.scan_t[u][0];
+#pragma unroll
+        for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
+    }
     mx_u4 B[kParts][3];
 #pragma unroll
     for (int p = 0; p < kParts; p++)
 #pragma unroll
-        for (int w = 0; w < 3; w++) B[p][w] = s_img.B[3 * p + w][lane];
+        for (int w = 0; w < 3; w++) B[p][w] = mxs_B(s_img, gimg)[3 * p + w][lane];
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
-    const MxTab &tb = s_img.tab;
+    const auto &tb = mxs_tb(s_img, gimg);
 #ifdef JX_MXS_STAMP
     {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1279,8 +1373,8 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mxs(const jx_xform_args a)
                 mxs_next(iss, g);
             } else {
                 /* padding (two operations keep the count): the slot of step k - 1, never read again */
-                __builtin_amdgcn_global_load_lds((mx_gp)g.rgb, (mx_lp)(L.ring[0] + kSlot * s2), 4, 0, 0);
-                __builtin_amdgcn_global_load_lds((mx_gp)g.rgb, (mx_lp)(L.ring[0] + kSlot * s2), 4, 0, 0);
+                mxs_dma<4>(g.rgb, L.ring[0] + kSlot * s2);
+                mxs_dma<4>(g.rgb, L.ring[0] + kSlot * s2);
             }
             body(cmp, sp);
             mxs_next(cmp, g);
@@ -2350,8 +2444,9 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
         __builtin_amdgcn_sched_barrier(0);
         mx_column_t<0, true>(accY, MxW{}, limc0, s_tab, 0, j, za, fl, 0, &accC[1]);
         __builtin_amdgcn_sched_barrier(0);
-        const mx_f4 s12 = {0x1p-12f, 0x1p-12f, 0x1p-12f, 0x1p-12f};
-        const mx_f4 rc4 = __builtin_elementwise_fma(accC[1], s12, accC[0]);
+        const float sl = JX_MX_LOEXP == 0 ? 1.0f : 0x1p-12f;
+        const mx_f4 s12 = {sl, sl, sl, sl};
+        const mx_f4 rc4 = JX_MX_LOEXP == 0 ? accC[1] + accC[0] : __builtin_elementwise_fma(accC[1], s12, accC[0]);
         __builtin_amdgcn_sched_barrier(0);
         const bool second = (k & 1u) != 0;
         if (second) {
@@ -2500,8 +2595,24 @@ int mx_tables_for_current_device(int *waves)
                         I.limc[0][jp] = mx_limc(I.tab, 1, jp);
                         I.limc[1][jp] = mx_limc(I.tab, 3, jp);
                     }
+                    static const int scan[8][8] = JX_SCAN_ORDER_INIT;
+                    for (int uu = 0; uu < 8; uu++)
+                        for (int v = 0; v < 8; v++) I.scan_t[uu][v] = (uint8_t)scan[v][uu];
                 }
             rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs_img), img.data(), img.size() * sizeof(MxsImg)));
+            std::vector<MxsImg1> img1(img.size());
+            memset(img1.data(), 0, img1.size() * sizeof(MxsImg1));
+            for (size_t i = 0; i < img.size(); i++) {
+                for (int h = 0; h < 2; h++)
+                    for (int jp = 0; jp < 16; jp++) {
+                        img1[i].sc.w[0][h][jp] = img[i].tab.wl[0][h][jp];
+                        img1[i].sc.w[1][h][jp] = img[i].tab.wl[2][h][jp];
+                    }
+                memcpy(img1[i].limc, img[i].limc, sizeof img1[i].limc);
+                memcpy(img1[i].scan_t, img[i].scan_t, sizeof img1[i].scan_t);
+            }
+            if (!rc)
+                rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs_img1), img1.data(), img1.size() * sizeof(MxsImg1)));
         }
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -2664,7 +2775,8 @@ extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)
 #endif
     if (JX_MX_SHORT) {
         const size_t w = (nsteps + kMxsC - 1) / kMxsC;
-        hipLaunchKernelGGL(k_mxs, dim3((unsigned)((w + 3) / 4)), dim3(256), JX_MX_DYNLDS, (hipStream_t)stream, *xa);
+        hipLaunchKernelGGL(k_mxs, dim3((unsigned)((w + kMxsWPG - 1) / kMxsWPG)), dim3(64 * kMxsWPG), JX_MX_DYNLDS,
+                           (hipStream_t)stream, *xa);
         return mx_rc(hipGetLastError());
     }
     const size_t w = JX_MX_NP ? (nsteps + JX_MX_NP - 1) / JX_MX_NP

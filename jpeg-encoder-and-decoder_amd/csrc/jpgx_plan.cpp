@@ -467,13 +467,13 @@ static int mx_split(MxSplit &S)
             const long double hv = mx_enc(bias ? B : rintl(ldexpl(B, 11)) / 2048.0L, bias, &S.bh[k][n]);
             if (ldexpl(hv, 11) != rintl(ldexpl(hv, 11))) return JPGX_EARG;
             S.h[k][n] = hv;
-            /* the lo parts are stored scaled by 2^12; k_mx takes R = acc_h + 2^-12 acc_l, exact
-             * scaling.  S.l / S.m hold the unscaled values. */
-            const long double ls = mx_enc(ldexpl(B - hv, 12), bias, &S.bl[k][n]);
-            S.l[k][n] = ldexpl(ls, -12);
+            /* the lo parts are stored scaled by 2^JX_MX_LOEXP (round 4: 2^0); k_mx takes R =
+             * acc_h + 2^-LOEXP acc_l, exact scaling.  S.l / S.m hold the unscaled values. */
+            const long double ls = mx_enc(ldexpl(B - hv, JX_MX_LOEXP), bias, &S.bl[k][n]);
+            S.l[k][n] = ldexpl(ls, -JX_MX_LOEXP);
             if (JX_MX_PARTS == 3) {
-                const long double ms = mx_enc(ldexpl(B - hv, 12) - ls, bias, &S.bm[k][n]);
-                S.m[k][n] = ldexpl(ms, -12);
+                const long double ms = mx_enc(ldexpl(B - hv, JX_MX_LOEXP) - ls, bias, &S.bm[k][n]);
+                S.m[k][n] = ldexpl(ms, -JX_MX_LOEXP);
             }
         }
     for (int n = 0; n < 24; n++) {              /* acc_h exactness: partial sums < 2^13 */
@@ -485,6 +485,7 @@ static int mx_split(MxSplit &S)
 }
 
 extern "C" int jx_mx_parts(void) { return JX_MX_PARTS; }
+extern "C" int jx_mx_loexp(void) { return JX_MX_LOEXP; }
 
 extern "C" int jx_mx_operands(uint16_t ops[3 * JX_MX_PARTS][64][8])
 {
@@ -615,11 +616,11 @@ static int mxc_split(int sub, MxcSplit &S)
             const long double hv = mx_enc(rintl(ldexpl(B, 11)) / 2048.0L, false, &S.bh[k][n]);
             if (ldexpl(hv, 11) != rintl(ldexpl(hv, 11))) return JPGX_EARG;
             S.h[k][n] = hv;
-            const long double ls = mx_enc(ldexpl(B - hv, 12), false, &S.bl[k][n]);
-            S.l[k][n] = ldexpl(ls, -12);
+            const long double ls = mx_enc(ldexpl(B - hv, JX_MX_LOEXP), false, &S.bl[k][n]);
+            S.l[k][n] = ldexpl(ls, -JX_MX_LOEXP);
             if (JX_MX_PARTS == 3) {
-                const long double ms = mx_enc(ldexpl(B - hv, 12) - ls, false, &S.bm[k][n]);
-                S.m[k][n] = ldexpl(ms, -12);
+                const long double ms = mx_enc(ldexpl(B - hv, JX_MX_LOEXP) - ls, false, &S.bm[k][n]);
+                S.m[k][n] = ldexpl(ms, -JX_MX_LOEXP);
             }
         }
     for (int n = 0; n < 16; n++) {              /* acc_h exactness: partial sums < 2^13 */

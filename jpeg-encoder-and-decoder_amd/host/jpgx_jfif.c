@@ -22,6 +22,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
+#ifdef __SSE2__
+#include <emmintrin.h>
+#endif
 
 #include "../../include/jpgx_compat.h"
 #include "../csrc/jx_consts.h"
@@ -186,6 +189,26 @@ static void build_codes(const uint8_t bits[16], const uint8_t *vals, HuffCodes *
 /* worst-case coded bytes of one block, stuffing included */
 #define JX_BLOCK_MAX (2 * (22 + 63 * 26 + 11 + 8) / 8 + 16)
 
+/* bit k set: z[k] != 0 */
+static inline uint64_t nonzero_mask(const int16_t *z)
+{
+#ifdef __SSE2__
+    const __m128i zero = _mm_setzero_si128();
+    uint64_t m = 0;
+    for (int i = 0; i < 4; i++) {
+        const __m128i a = _mm_loadu_si128((const __m128i *)(z + 16 * i));
+        const __m128i b = _mm_loadu_si128((const __m128i *)(z + 16 * i + 8));
+        const __m128i e = _mm_packs_epi16(_mm_cmpeq_epi16(a, zero), _mm_cmpeq_epi16(b, zero));
+        m |= (uint64_t)(uint16_t)~_mm_movemask_epi8(e) << (16 * i);
+    }
+    return m;
+#else
+    uint64_t m = 0;
+    for (int k = 0; k < 64; k++) m |= (uint64_t)(z[k] != 0) << k;
+    return m;
+#endif
+}
+
 /* one block's Huffman-coded data (T.81 F.1.2): DC difference against *pred, AC run/size */
 static void encode_block(BW *w, const int16_t *z, int *pred, const HuffCodes *dc, const HuffCodes *ac)
 {
@@ -197,15 +220,14 @@ static void encode_block(BW *w, const int16_t *z, int *pred, const HuffCodes *dc
     int s = category(diff, &extra);
     uint32_t c = dc->cl[s];
     bw_bits(w, (c >> 8) << s | extra, (int)(c & 0xff) + s);
-    int last = 63;
-    while (last > 0 && z[last] == 0) last--;
-    int run = 0;
-    for (int k = 1; k <= last; k++) {
+    uint64_t nz = nonzero_mask(z) & ~1ull;         /* the nonzero AC coefficients */
+    int prev = 0;
+    while (nz) {
+        const int k = __builtin_ctzll(nz);
+        nz &= nz - 1;
+        int run = k - prev - 1;
+        prev = k;
         int v = z[k];
-        if (v == 0) {
-            run++;
-            continue;
-        }
         if (v > 1023) v = 1023;
         if (v < -1023) v = -1023;
         while (run > 15) {                         /* ZRL */
@@ -216,9 +238,8 @@ static void encode_block(BW *w, const int16_t *z, int *pred, const HuffCodes *dc
         s = category(v, &extra);
         c = ac->cl[run << 4 | s];
         bw_bits(w, (c >> 8) << s | extra, (int)(c & 0xff) + s);
-        run = 0;
     }
-    if (last < 63) {                               /* EOB */
+    if (prev < 63) {                               /* EOB */
         c = ac->cl[0x00];
         bw_bits(w, c >> 8, (int)(c & 0xff));
     }

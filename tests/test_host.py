@@ -169,7 +169,7 @@ def test_mx_operands_make_the_hi_product_exact():
     # plan columns n = 8c + u: Y|Cb from which 0, Cr from which 1
     M = np.concatenate([B[:, 0], B[:, 1, :, :8]], axis=2)      # [part][k][24]
     hi = M[0]
-    lo = M[1:].sum(axis=0) * 2.0 ** -12                        # lo parts stored x 2^12
+    lo = M[1:].sum(axis=0) * 2.0 ** -jpgx.lib.jx_mx_loexp()    # lo parts stored x 2^LOEXP
     assert np.all(hi * 2048 == np.round(hi * 2048))
     assert np.all(255 * np.abs(hi[:24]).sum(axis=0) + np.abs(hi[24]) < 8192)
     tol = 2 ** -30 if parts_n == 3 else 2 ** -23
@@ -240,7 +240,7 @@ def test_mx420_operands_reconstruct_the_quad_matrix():
     assert g(ref422.ctypes.data_as(ctypes.c_void_p)) == 0
     assert np.array_equal(ops[:, :2], ref422[:, :2])            # the same Y operands
     C = np.concatenate([B[:, 2], B[:, 3], B[:, 4]], axis=1) * 2.0 ** -15   # [part][k 0..95][16]
-    hi, lo = C[0], C[1:].sum(axis=0) * 2.0 ** -12
+    hi, lo = C[0], C[1:].sum(axis=0) * 2.0 ** -jpgx.lib.jx_mx_loexp()
     assert np.all(hi * 2048 == np.round(hi * 2048))
     assert np.all(255 * np.abs(hi).sum(axis=0) < 8192)
     tol = 2 ** -30 if parts_n == 3 else 2 ** -23
@@ -283,7 +283,7 @@ def test_mx422_operands_reconstruct_the_pair_matrix():
     assert not np.any(B[:, :2, 25:, :])
     C = np.concatenate([B[:, 2], B[:, 3]], axis=1)              # [part][k 0..63][16]
     assert not np.any(C[:, 48:, :])
-    hi, lo = C[0], C[1:].sum(axis=0) * 2.0 ** -12
+    hi, lo = C[0], C[1:].sum(axis=0) * 2.0 ** -jpgx.lib.jx_mx_loexp()
     assert np.all(hi * 2048 == np.round(hi * 2048))
     assert np.all(255 * np.abs(hi[:48]).sum(axis=0) < 8192)
     tol = 2 ** -30 if parts_n == 3 else 2 ** -23
