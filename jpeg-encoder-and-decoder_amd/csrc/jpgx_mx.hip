@@ -1071,6 +1071,7 @@ struct MxsCur {
     bool simple;
     const uint8_t *src;
     int16_t *dst;
+    int16_t *cdst;                      /* k_mxs422: its first chroma block's Cb output */
 };
 
 __device__ __forceinline__ void mxs_simple(MxsCur &P, const MxG &g)
@@ -1088,6 +1089,7 @@ __device__ __forceinline__ void mxs_at(MxsCur &P, const MxG &g, unsigned b)
     P.c = X.c;
     P.src = X.src;
     P.dst = X.dst;
+    P.cdst = g.out + (long long)X.f * g.ofstride + 64ll * (g.nb + X.bi / 2u);
     mxs_simple(P, g);
 }
 
@@ -1102,6 +1104,7 @@ __device__ __forceinline__ void mxs_next(MxsCur &P, const MxG &g)
     P.c += 8u;
     P.src += 192;
     P.dst += 512;
+    P.cdst += 256;
     mxs_simple(P, g);
 }
 
@@ -1480,7 +1483,8 @@ __device__ __forceinline__ int mx_exact_pair(const lds_u8 *row0, unsigned rs, un
 
 /* lane x's first pixel (row 0) and row stride of chroma block cb in a step's slot; the right
  * Y block's rows come from L.qtrue when it is a row-last block (bit cb of qmask) */
-__device__ __forceinline__ const lds_u8 *mx422_mcu_row0(Mx422Lds &L, const uint8_t *sp, uint32_t qmask,
+template <class Lds>
+__device__ __forceinline__ const lds_u8 *mx422_mcu_row0(Lds &L, const uint8_t *sp, uint32_t qmask,
                                                         unsigned cb, unsigned x, unsigned &rs)
 {
     const bool q = ((qmask >> cb) & 1u) && x >= 4;
@@ -1489,7 +1493,8 @@ __device__ __forceinline__ const lds_u8 *mx422_mcu_row0(Mx422Lds &L, const uint8
 }
 
 /* Inline exact pass of one step: bit 8 col + v of a lane's bits (col 0 Y, 1 chroma) */
-__device__ __forceinline__ void mx422_exact_inline(Mx422Lds &L, const uint8_t *sp, uint32_t qmask,
+template <class Lds>
+__device__ __forceinline__ void mx422_exact_inline(Lds &L, const uint8_t *sp, uint32_t qmask,
                                                    uint32_t bits, const jx_mxtab &T)
 {
     const unsigned lane = mx_lane();
@@ -1646,7 +1651,8 @@ __device__ __forceinline__ void mx422_defer_step(Mx422Lds &L, const uint8_t *sp,
 
 /* a general step's row-last Y blocks (always odd: bpr is even): their true pixel rows 8r..8r+7
  * into L.qtrue[cb]; returns the mask of chroma blocks cb that have one */
-__device__ __forceinline__ uint32_t mx422_true_rows(Mx422Lds &L, const MxG &g, unsigned b0)
+template <class Lds>
+__device__ __forceinline__ uint32_t mx422_true_rows(Lds &L, const MxG &g, unsigned b0)
 {
     const unsigned l = mx_lane(), y = l & 7u, cb = (l >> 3) & 3u;
     const unsigned b = b0 + 2u * cb + 1u;
@@ -1902,6 +1908,216 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
     if (nq) mx422_flush(L, nq, ns, g, T);
 }
 
+/* ==== k_mxs422: k_mx422's transform in short-lived one-wave workgroups (round 4) =============
+ *
+ * k_mxs's scheme (three steps per wave, their DMA up front, step k in slot k, a 1.2-KiB per-wave
+ * image of scales / hot-path limits / zig-zag positions by LDS-DMA, the B operands and band limits
+ * from the global image, the exact pass inline on the stage) around k_mx422's step: 8 Y blocks =
+ * 4 MCUs, Y and chroma row transforms on the matrix cores (16 MFMAs), two column DCTs per lane,
+ * two stores (Y 1 KiB; lanes 0..31 Cb, 32..63 Cr).  Two stores per step: step k waits with
+ * vmcnt(2 (C - 1 - k) + 2 k).  The quirk (a general step holding a row-last Y block) loads that
+ * block's true rows into L.qtrue for its MCU's chroma, as k_mx422.
+ */
+constexpr unsigned kMxs422C = 3;
+struct alignas(16) Mxs422Lds {
+    uint8_t ring[kMxs422C][kSlot];
+    uint8_t stage[16 * kBS];
+    uint8_t qtrue[4][192];
+    uint16_t task[8];
+};
+static_assert(sizeof(Mxs422Lds) % 16 == 0 &&
+                  (sizeof(Mxs422Lds) + sizeof(MxsImg1) + 511) / 512 * 512 * 16 <= 160 * 1024,
+              "16 one-wave workgroups per CU");
+/* the global image: B operands [part * 4 + which][lane], k_mx422's scale / limit table */
+struct alignas(16) MxsImg422 {
+    mx_u4 B[JX_MX_PARTS * 4][64];
+    MxTab tab;
+};
+__device__ MxsImg422 g_mxs422_img[2][JX_MAXQ + 1];
+__device__ MxsImg1 g_mxs422_img1[2][JX_MAXQ + 1];
+
+__global__ __launch_bounds__(64, JX_MX422_WPE) void k_mxs422(const jx_xform_args a)
+{
+    __shared__ __attribute__((aligned(16))) Mxs422Lds L;
+    __shared__ __attribute__((aligned(16))) MxsImg1 s_img;
+    MxG g;
+    g.rgb = a.g.rgb;
+    g.out = a.g.out;
+    g.pitch = a.g.in_pitch;
+    g.fstride = a.g.in_fstride;
+    g.ofstride = a.g.out_fstride;
+    g.bpr = (unsigned)a.g.bpr;
+    g.nb = (unsigned)a.g.nb;
+    g.total = (unsigned)a.g.nb * (unsigned)a.g.nframes;
+    g.row0 = a.g.row0;
+    g.quality = a.quality;
+    g.force = a.force_exact;
+    g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
+#pragma unroll
+    for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+
+    const unsigned lane = threadIdx.x & 63u;
+    const MxsImg422 &gimg = g_mxs422_img[g.force ? 1 : 0][g.quality];
+    {
+        constexpr unsigned kP1 = sizeof(MxsImg1) / 16;
+        const uint8_t *img = (const uint8_t *)&g_mxs422_img1[g.force ? 1 : 0][g.quality];
+        mxs_dma<16>(img + 16u * lane, &s_img);
+        if (lane < kP1 - 64u) mxs_dma<16>(img + 16u * (64u + lane), (uint8_t *)&s_img + 1024u);
+    }
+    const unsigned wv = blockIdx.x;
+    const uint32_t off0 = (uint32_t)((lane / 12u) * (unsigned)g.pitch + 16u * (lane % 12u));
+    const uint32_t off1 = (uint32_t)(((64u + lane) / 12u) * (unsigned)g.pitch + 16u * ((64u + lane) % 12u));
+    MxsCur iss;
+    mxs_at(iss, g, 8u * kMxs422C * wv);
+    MxsCur cmp = iss;
+#pragma unroll
+    for (unsigned k = 0; k < kMxs422C; k++) {
+        mxs_issue(iss, g, L.ring[k], off0, off1, lane);
+        mxs_next(iss, g);
+    }
+
+    /* lane constants (k_mx422's) */
+    const unsigned m = lane & 15u, q = lane >> 4;
+    const uint32_t aoff = 192u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 0u);
+    const uint32_t s0 = q < 3 ? kSelLo : kSelOne;
+    const uint32_t s1 = q < 3 ? kSelHi : kSelZero;
+    const uint32_t s2 = q < 3 ? kSelLo : kSelZero;
+    const uint32_t coff0 = 192u * (m & 3u) + 48u * (m >> 2) + 8u * q;
+    const uint32_t coff1 = 192u * (m & 3u) + 48u * (m >> 2) + 32u + 8u * (q < 2 ? q : 0u);
+    const uint32_t t0 = q < 2 ? kSelLo : (q == 2 ? kSelOne : kSelZero);
+    const uint32_t t1 = q < 2 ? kSelHi : kSelZero;
+    const uint32_t t2 = q < 2 ? kSelLo : kSelZero;
+    const uint32_t soy = lane * 16u, soc = (lane & 31u) * 16u + (lane >> 5) * (g.nb / 2u) * 128u;
+    const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
+    const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
+    const jx_mxtab &T = g_mx422tab[g.force ? 1 : 0][g.quality];
+
+    if (cmp.b >= g.total) return;
+    mx_wait_vm<2u * kMxs422C>();                    /* the image (older than the pixel DMA) */
+    mx_wave_sync();
+    uint32_t za[8];
+    {
+        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * ((j >> 3) * 4u + gq);
+        const mx_u2 sc = *(const mx_u2 *)&s_img.scan_t[u][0];
+#pragma unroll
+        for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
+    }
+    mx_u4 B[kParts][4];
+#pragma unroll
+    for (int p = 0; p < kParts; p++)
+#pragma unroll
+        for (int w = 0; w < 4; w++) B[p][w] = gimg.B[4 * p + w][lane];
+    const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
+    const MxsTabRef tb{s_img.sc, gimg.tab};
+
+    const auto body = [&](const MxsCur &S, uint8_t *sp) __attribute__((always_inline)) {
+        if (!S.simple) {
+            MxCur P;
+            mx_seek(P, g, S.b);
+            mx_issue(g, P, S.b, false, off0, off1, sp);      /* register path; waits vmcnt(0) */
+        }
+        const uint32_t qmask = S.simple ? 0u : mx422_true_rows(L, g, S.b);
+        mx_wave_sync();
+        const mx_f4 z = {};
+        uint32_t fl = 0;
+        mx_f4 acc[2][4];                               /* [Y, chroma][hl, ll, hh, lh] */
+        const auto mma2 = [&](mx_f4(&o)[4], const mx_h8 &Al0, const mx_h8 &Ah0, const mx_h8 &Al1,
+                              const mx_h8 &Ah1, int w0) __attribute__((always_inline)) {
+            o[0] = mx_mma(Al0, B[0][w0], z);
+            o[2] = mx_mma(Ah0, B[0][w0], z);
+            o[1] = mx_mma(Al0, B[1][w0], z);
+            o[3] = mx_mma(Ah0, B[1][w0], z);
+            o[0] = mx_mma(Al1, B[0][w0 + 1], o[0]);
+            o[2] = mx_mma(Ah1, B[0][w0 + 1], o[2]);
+            o[1] = mx_mma(Al1, B[1][w0 + 1], o[1]);
+            o[3] = mx_mma(Ah1, B[1][w0 + 1], o[3]);
+            if (kParts == 3) {
+                o[1] = mx_mma(Al0, B[kParts - 1][w0], o[1]);
+                o[3] = mx_mma(Ah0, B[kParts - 1][w0], o[3]);
+                o[1] = mx_mma(Al1, B[kParts - 1][w0 + 1], o[1]);
+                o[3] = mx_mma(Ah1, B[kParts - 1][w0 + 1], o[3]);
+            }
+        };
+        /* every LDS read of the step's A operands before its first MFMA; each column reads its
+         * scales after its tiles (the Y column after a fence on the chroma products) */
+        const mx_u2 y00 = *(const mx_u2 *)(sp + aoff);
+        const mx_u2 y01 = *(const mx_u2 *)(sp + aoff + 768u);
+        const mx_u2 y10 = *(const mx_u2 *)(sp + aoff + 96u);
+        const mx_u2 y11 = *(const mx_u2 *)(sp + aoff + 864u);
+        mx_u2 c00, c01, c10, c11;
+        if (__builtin_expect(qmask == 0, 1)) {
+            c00 = *(const mx_u2 *)(sp + coff0);
+            c01 = *(const mx_u2 *)(sp + coff0 + 768u);
+            c10 = *(const mx_u2 *)(sp + coff1);
+            c11 = *(const mx_u2 *)(sp + coff1 + 768u);
+        } else {
+            const unsigned l = mx_lane(), mm = l & 15u, qq = l >> 4, cb = mm >> 2;
+            const bool qb = (qmask >> cb) & 1u;
+            const uint8_t *qt = L.qtrue[cb] + 24u * (mm & 3u);
+            const uint8_t *p0 = qb && qq == 3 ? qt : sp + coff0;
+            const uint8_t *p1 = qb && qq < 2 ? qt + 8u + 8u * qq : sp + coff1;
+            const unsigned h0 = qb && qq == 3 ? 96u : 768u, h1 = qb && qq < 2 ? 96u : 768u;
+            c00 = *(const mx_u2 *)p0;
+            c01 = *(const mx_u2 *)(p0 + h0);
+            c10 = *(const mx_u2 *)p1;
+            c11 = *(const mx_u2 *)(p1 + h1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma2(acc[0], mx_aop(y00, s0, s1, s2), mx_aop(y01, s0, s1, s2), mx_aop(y10, s0, s1, s2),
+             mx_aop(y11, s0, s1, s2), 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma2(acc[1], mx_aop(c00, kSelLo, kSelHi, kSelLo), mx_aop(c01, kSelLo, kSelHi, kSelLo),
+             mx_aop(c10, t0, t1, t2), mx_aop(c11, t0, t1, t2), 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mx_column_t<0, true>(acc[0], MxW{}, limc0, tb, 0, j, za, fl, 0, &acc[1][3]);
+        __builtin_amdgcn_sched_barrier(0);
+        mx_column_t<kSt422C, true>(acc[1], MxW{}, limc2, tb, 2, j, za, fl, 1);
+        mx_wave_sync();
+        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
+            if (S.b + 8u > g.total) {                  /* clamped copies past the end */
+                const unsigned nvalid = g.total - S.b;
+                if (mx422_yblock(lane) >= nvalid) fl &= ~0xffu;
+                if (2u * (lane >> 4) >= nvalid) fl &= ~0xff00u;
+            }
+            mx422_exact_inline(L, sp, qmask, fl, T);
+        }
+        /* always two store instructions (the vmcnt accounting counts on it) */
+        if (S.simple) {
+            const mx_u4 vy = *(const mx_u4 *)(L.stage + ro);
+            const mx_u4 vc = *(const mx_u4 *)(L.stage + kSt422C + ro);
+            __builtin_nontemporal_store(vy, (mx_u4 *)((const uint8_t *)S.dst + soy));
+            __builtin_nontemporal_store(vc, (mx_u4 *)((const uint8_t *)S.cdst + soc));
+        } else {
+            const unsigned l = mx_lane();
+            const unsigned by = S.b + (l >> 3), bc = S.b + 2u * ((l >> 3) & 3u);
+            const unsigned yb = by < g.total ? by : g.total - 1u, cbk = bc < g.total ? bc : g.total - 1u;
+            const unsigned fy = yb / g.nb, biy = yb - fy * g.nb;
+            const unsigned fc = cbk / g.nb, bic = cbk - fc * g.nb;
+            const uint32_t rl = (l >> 3) * kBS + (l & 7u) * 16u;
+            const mx_u4 vy = *(const mx_u4 *)(L.stage + rl);
+            const mx_u4 vc = *(const mx_u4 *)(L.stage + kSt422C + rl);
+            if (by < g.total)
+                __builtin_nontemporal_store(
+                    vy, (mx_u4 *)(g.out + (long long)fy * g.ofstride + (long long)biy * 64 + (l & 7u) * 8));
+            if (bc < g.total)
+                __builtin_nontemporal_store(
+                    vc, (mx_u4 *)(g.out + (long long)fc * g.ofstride +
+                                  ((long long)g.nb + (l >> 5) * (g.nb / 2u) + bic / 2u) * 64 + (l & 7u) * 8));
+        }
+        mx_wave_sync();
+    };
+    const auto step = [&](auto kc) __attribute__((always_inline)) {
+        constexpr unsigned k = decltype(kc)::value;
+        if (cmp.b >= g.total) return;
+        mx_wait_vm<2 * (kMxs422C - 1 - k) + 2 * k>();
+        body(cmp, L.ring[k]);
+        mxs_next(cmp, g);
+    };
+    step(std::integral_constant<unsigned, 0>{});
+    step(std::integral_constant<unsigned, 1>{});
+    step(std::integral_constant<unsigned, 2>{});
+}
+
 /* ==== k_mx420: true 4:2:0 (extension, JPGX_FLAG_SUBSAMPLE, sample_ratio 2) ==================
  *
  * A step is two consecutive MCUs (MCU-linear launch-global index, frames concatenated): their
@@ -2044,7 +2260,8 @@ __device__ __forceinline__ void mx420_issue_general(const MxG &g, const Mx420G &
 
 /* a general step's MCUs whose right block column is a row's last: its true pixel rows (16 x 24 B)
  * into L.qtrue[MCU of the step]; returns the mask of those MCUs */
-__device__ __forceinline__ uint32_t mx420_true_rows(Mx420Lds &L, const MxG &g, const Mx420G &h, unsigned m0)
+template <class Lds>
+__device__ __forceinline__ uint32_t mx420_true_rows(Lds &L, const MxG &g, const Mx420G &h, unsigned m0)
 {
     const unsigned l = mx_lane(), y = l & 15u, ms = (l >> 4) & 1u;
     const unsigned m = m0 + ms;
@@ -2109,7 +2326,8 @@ __device__ __forceinline__ const uint8_t *mx420_mcu_src(const MxG &g, const Mx42
 __device__ __forceinline__ unsigned mx420_pm(unsigned gq) { return (gq & 1u) * 2u + (gq >> 1); }
 
 /* Inline exact pass: Y bits (col 0) of this step and chroma bits (col 1, pair base mp) */
-__device__ __forceinline__ void mx420_exact_inline(Mx420Lds &L, const uint8_t *sp, uint32_t bits, unsigned mp,
+template <class Lds>
+__device__ __forceinline__ void mx420_exact_inline(Lds &L, const uint8_t *sp, uint32_t bits, unsigned mp,
                                                    const MxG &g, const Mx420G &h, const jx_mxtab &T)
 {
     const unsigned lane = mx_lane();
@@ -2524,6 +2742,261 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
     if (nq) mx420_flush(L, nq, ns, g, h, T);
 }
 
+/* ==== k_mxs420: k_mx420's transform in short-lived one-wave workgroups (round 4) =============
+ *
+ * One wave = one step pair (two steps of two MCUs each: 16 Y blocks, 4 Cb + 4 Cr blocks), both
+ * steps' DMA up front (slots 0 and 1), the 1.2-KiB per-wave image by LDS-DMA, B operands and band
+ * limits from the global image, the exact pass inline on the stage (chroma tasks read their
+ * MCU's pixels from global memory, as k_mx420's flush).  Step 0 stores its Y (one operation), step
+ * 1 its Y and the pair's chroma: step 0 waits vmcnt(2), step 1 vmcnt(1).
+ */
+struct alignas(16) Mxs420Lds {
+    uint8_t ring[2][kSlot];             /* [y 0..15][4 blocks x 24 B] */
+    uint8_t stage[16 * kBS];
+    uint8_t qtrue[2][384];              /* general step: MCU's right column, true rows [16][24] */
+    mx_f4 rA[64];                       /* step 0's chroma R (not held across step 0's exact pass) */
+    uint16_t task[8];
+};
+static_assert(sizeof(Mxs420Lds) % 16 == 0 &&
+                  (sizeof(Mxs420Lds) + sizeof(MxsImg1) + 511) / 512 * 512 * 16 <= 160 * 1024,
+              "16 one-wave workgroups per CU");
+struct alignas(16) MxsImg420 {
+    mx_u4 B[JX_MX_PARTS * 5][64];
+    MxTab tab;
+};
+__device__ MxsImg420 g_mxs420_img[2][JX_MAXQ + 1];
+__device__ MxsImg1 g_mxs420_img1[2][JX_MAXQ + 1];
+
+__global__ __launch_bounds__(64, JX_MX420_WPE) void k_mxs420(const jx_xform_args a)
+{
+    __shared__ __attribute__((aligned(16))) Mxs420Lds L;
+    __shared__ __attribute__((aligned(16))) MxsImg1 s_img;
+    MxG g;
+    g.rgb = a.g.rgb;
+    g.out = a.g.out;
+    g.pitch = a.g.in_pitch;
+    g.fstride = a.g.in_fstride;
+    g.ofstride = a.g.out_fstride;
+    g.bpr = (unsigned)a.g.bpr;
+    g.nb = (unsigned)a.g.nb;
+    g.total = (unsigned)a.g.nb * (unsigned)a.g.nframes;
+    g.row0 = a.g.row0;
+    g.quality = a.quality;
+    g.force = a.force_exact;
+    g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
+#pragma unroll
+    for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+    Mx420G h;
+    h.mpr = g.bpr / 2u;
+    h.rows = g.nb / g.bpr / 2u;
+    h.nmcu = h.rows * h.mpr;
+    h.tm = h.nmcu * (unsigned)a.g.nframes;
+
+    const unsigned lane = threadIdx.x & 63u;
+    const MxsImg420 &gimg = g_mxs420_img[g.force ? 1 : 0][g.quality];
+    {
+        constexpr unsigned kP1 = sizeof(MxsImg1) / 16;
+        const uint8_t *img = (const uint8_t *)&g_mxs420_img1[g.force ? 1 : 0][g.quality];
+        mxs_dma<16>(img + 16u * lane, &s_img);
+        if (lane < kP1 - 64u) mxs_dma<16>(img + 16u * (64u + lane), (uint8_t *)&s_img + 1024u);
+    }
+    /* the pair: MCUs m0 .. m0 + 3; simple = one MCU row of one frame, no row-last MCU, in range */
+    const unsigned m0 = 4u * blockIdx.x;
+    const uint32_t off0 = (uint32_t)((lane / 6u) * (unsigned)g.pitch + 16u * (lane % 6u));
+    const uint32_t off1 = (uint32_t)(((64u + lane) / 6u) * (unsigned)g.pitch + 16u * ((64u + lane) % 6u));
+    Mx420Chunk cc;
+    bool simple = false;
+    if (m0 < h.tm) {
+        mx420_at(cc, g, h, m0);
+        simple = m0 + 4u <= h.tm && cc.mx + 4u < h.mpr && g.lin_store;
+    }
+#pragma unroll
+    for (unsigned k = 0; k < 2; k++) {
+        if (simple) {
+            mxs_dma<16>(cc.src + 96u * k + off0, L.ring[k]);
+            if (lane < 32) mxs_dma<16>(cc.src + 96u * k + off1, L.ring[k] + 1024u);
+        } else {
+            mxs_dma<4>(g.rgb, L.ring[k]);                   /* padding: filled at compute time */
+            mxs_dma<4>(g.rgb, L.ring[k]);
+        }
+    }
+
+    /* lane constants (k_mx420's) */
+    const unsigned m = lane & 15u, q = lane >> 4;
+    const uint32_t aoff = 96u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 0u);
+    const uint32_t s0 = q < 3 ? kSelLo : kSelOne;
+    const uint32_t s1 = q < 3 ? kSelHi : kSelZero;
+    const uint32_t s2 = q < 3 ? kSelLo : kSelZero;
+    const uint32_t cof0 = 192u * (m & 7u) + 48u * (m >> 3) + 8u * q;
+    const uint32_t cof1 = cof0 + (q < 2 ? 32u : 80u);
+    const uint32_t soy = (lane & 31u) * 16u + (lane >> 5) * g.bpr * 128u;
+    const uint32_t soc = (lane & 31u) * 16u + (lane >> 5) * h.nmcu * 128u;
+    const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
+    const uint32_t rc = kSt420C + kBS * (4u * (lane >> 5) + mx420_pm((lane >> 3) & 3u)) + (lane & 7u) * 16u;
+    const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
+    const jx_mxtab &T = g_mx420tab[g.force ? 1 : 0][g.quality];
+
+    if (m0 >= h.tm) return;
+    mx_wait_vm<4>();                                    /* the image (older than the pixel DMA) */
+    mx_wave_sync();
+    uint32_t za[8];
+    {
+        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * (4u * (j >> 3) + gq);
+        const mx_u2 sc = *(const mx_u2 *)&s_img.scan_t[u][0];
+#pragma unroll
+        for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
+    }
+    mx_u4 B[kParts][5];
+#pragma unroll
+    for (int p = 0; p < kParts; p++)
+#pragma unroll
+        for (int w = 0; w < 5; w++) B[p][w] = gimg.B[5 * p + w][lane];
+    const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
+    const MxsTabRef tb{s_img.sc, gimg.tab};
+
+    const auto step = [&](auto kc) __attribute__((always_inline)) {
+        constexpr unsigned k = decltype(kc)::value;
+        constexpr bool second = k == 1;
+        const unsigned ms = m0 + 2u * k;                /* the step's first MCU */
+        if (k == 0)
+            mx_wait_vm<2>();                            /* younger: step 1's DMA */
+        else
+            mx_wait_vm<1>();                            /* younger: step 0's Y store */
+        uint8_t *const sp = L.ring[k];
+        if (!simple) mx420_issue_general(g, h, ms, sp);     /* register path; waits vmcnt(0) */
+        const uint32_t qmask = simple ? 0u : mx420_true_rows(L, g, h, ms);
+        mx_wave_sync();
+        const mx_f4 z = {};
+        uint32_t fl = 0;
+        mx_f4 accY[4], accC[2];
+        const mx_u2 y00 = *(const mx_u2 *)(sp + aoff);
+        const mx_u2 y01 = *(const mx_u2 *)(sp + aoff + 384u);
+        const mx_u2 y10 = *(const mx_u2 *)(sp + aoff + 768u);
+        const mx_u2 y11 = *(const mx_u2 *)(sp + aoff + 1152u);
+        mx_u2 c0, c1, c2;
+        if (__builtin_expect(qmask == 0, 1)) {
+            c0 = *(const mx_u2 *)(sp + cof0);
+            c1 = *(const mx_u2 *)(sp + cof1);
+            c2 = *(const mx_u2 *)(sp + cof0 + 112u);
+        } else {
+            const unsigned l = mx_lane(), mm = l & 15u, qq = l >> 4, cb = mm >> 3, yr = 2u * (mm & 7u);
+            const bool qb = (qmask >> cb) & 1u;
+            const uint8_t *qt = L.qtrue[cb];
+            const uint8_t *p0 = qb && qq == 3 ? qt + 24u * yr : sp + cof0;
+            const uint8_t *p1 = qb && qq < 2 ? qt + 24u * yr + 8u + 8u * qq : sp + cof1;
+            const uint8_t *p2 = qb && qq >= 1 ? qt + 24u * (yr + 1u) + 8u * (qq - 1u) : sp + cof0 + 112u;
+            c0 = *(const mx_u2 *)p0;
+            c1 = *(const mx_u2 *)p1;
+            c2 = *(const mx_u2 *)p2;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        {
+            const mx_h8 Al0 = mx_aop(y00, s0, s1, s2), Ah0 = mx_aop(y01, s0, s1, s2);
+            const mx_h8 Al1 = mx_aop(y10, s0, s1, s2), Ah1 = mx_aop(y11, s0, s1, s2);
+            accY[0] = mx_mma(Al0, B[0][0], z);
+            accY[2] = mx_mma(Ah0, B[0][0], z);
+            accY[1] = mx_mma(Al0, B[1][0], z);
+            accY[3] = mx_mma(Ah0, B[1][0], z);
+            accY[0] = mx_mma(Al1, B[0][1], accY[0]);
+            accY[2] = mx_mma(Ah1, B[0][1], accY[2]);
+            accY[1] = mx_mma(Al1, B[1][1], accY[1]);
+            accY[3] = mx_mma(Ah1, B[1][1], accY[3]);
+            if (kParts == 3) {
+                accY[1] = mx_mma(Al0, B[kParts - 1][0], accY[1]);
+                accY[3] = mx_mma(Ah0, B[kParts - 1][0], accY[3]);
+                accY[1] = mx_mma(Al1, B[kParts - 1][1], accY[1]);
+                accY[3] = mx_mma(Ah1, B[kParts - 1][1], accY[3]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        {
+            const mx_h8 C0 = mx_aop(c0, kSelLo, kSelHi, kSelLo), C1 = mx_aop(c1, kSelLo, kSelHi, kSelLo);
+            const mx_h8 C2 = mx_aop(c2, kSelLo, kSelHi, kSelLo);
+            accC[0] = mx_mma(C0, B[0][2], z);
+            accC[1] = mx_mma(C0, B[1][2], z);
+            accC[0] = mx_mma(C1, B[0][3], accC[0]);
+            accC[1] = mx_mma(C1, B[1][3], accC[1]);
+            accC[0] = mx_mma(C2, B[0][4], accC[0]);
+            accC[1] = mx_mma(C2, B[1][4], accC[1]);
+            if (kParts == 3) {
+                accC[1] = mx_mma(C0, B[kParts - 1][2], accC[1]);
+                accC[1] = mx_mma(C1, B[kParts - 1][3], accC[1]);
+                accC[1] = mx_mma(C2, B[kParts - 1][4], accC[1]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mx_column_t<0, true>(accY, MxW{}, limc0, tb, 0, j, za, fl, 0, &accC[1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const float sl = JX_MX_LOEXP == 0 ? 1.0f : 0x1p-12f;
+        const mx_f4 s12 = {sl, sl, sl, sl};
+        const mx_f4 rc4 = JX_MX_LOEXP == 0 ? accC[1] + accC[0] : __builtin_elementwise_fma(accC[1], s12, accC[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (second) {
+            const mx_f4 rA0 = L.rA[lane];
+            mx_f2 R[4];
+            float lo4[4], hi4[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(rA0[i]), __float_as_uint(rc4[i]),
+                                                                false, false);
+                lo4[i] = __uint_as_float(r[0]);
+                hi4[i] = __uint_as_float(r[1]);
+            }
+            R[0] = mx_f2{lo4[0], lo4[1]};
+            R[1] = mx_f2{lo4[2], lo4[3]};
+            R[2] = mx_f2{hi4[0], hi4[1]};
+            R[3] = mx_f2{hi4[2], hi4[3]};
+            mx_column_r<kSt420C>(R, mx_w(tb, 2, j), limc2, tb, 2, j, za, fl, 1);
+        } else {
+            L.rA[lane] = rc4;
+        }
+        mx_wave_sync();
+        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
+            {   /* clamped MCUs past the launch's end: no tasks */
+                if (ms + (gq >> 1) >= h.tm) fl &= ~0xffu;
+                if (m0 + mx420_pm(gq) >= h.tm) fl &= ~0xff00u;
+            }
+            mx420_exact_inline(L, sp, fl, m0, g, h, T);
+        }
+        /* stores: the Y store; on the second step also the pair's chroma */
+        if (simple) {
+            const mx_u4 vy = *(const mx_u4 *)(L.stage + ro);
+            __builtin_nontemporal_store(vy, (mx_u4 *)((const uint8_t *)(cc.ydst + 256u * k) + soy));
+            if (second) {
+                const mx_u4 vc = *(const mx_u4 *)(L.stage + rc);
+                __builtin_nontemporal_store(vc, (mx_u4 *)((const uint8_t *)cc.cdst + soc));
+            }
+        } else {
+            const unsigned l = mx_lane();
+            {
+                const unsigned jb = (l >> 3) & 3u, mm = ms + (jb >> 1);
+                const unsigned mc = mm < h.tm ? mm : h.tm - 1u;
+                const unsigned yb = mx420_yblock(g, h, mc - (jb >> 1), l >> 5, jb);
+                const unsigned f = yb / g.nb, bi = yb - f * g.nb;
+                const mx_u4 vy = *(const mx_u4 *)(L.stage + (l >> 3) * kBS + (l & 7u) * 16u);
+                if (mm < h.tm)
+                    __builtin_nontemporal_store(
+                        vy, (mx_u4 *)(g.out + (long long)f * g.ofstride + (long long)bi * 64 + (l & 7u) * 8));
+            }
+            if (second) {
+                const unsigned pm = (l >> 3) & 3u, mm = m0 + pm;
+                const unsigned mc = mm < h.tm ? mm : h.tm - 1u;
+                unsigned f, mi, my, mx;
+                mx420_mcu(h, mc, f, mi, my, mx);
+                const mx_u4 vc = *(const mx_u4 *)(L.stage + kSt420C + kBS * (4u * (l >> 5) + mx420_pm(pm)) +
+                                                   (l & 7u) * 16u);
+                if (mm < h.tm)
+                    __builtin_nontemporal_store(
+                        vc, (mx_u4 *)(g.out + (long long)f * g.ofstride +
+                                      ((long long)g.nb + (l >> 5) * h.nmcu + mi) * 64 + (l & 7u) * 8));
+            }
+        }
+        mx_wave_sync();
+    };
+    step(std::integral_constant<unsigned, 0>{});
+    step(std::integral_constant<unsigned, 1>{});
+}
+
 int mx_rc(hipError_t e) { return e == hipSuccess ? JPGX_OK : JPGX_EHIP; }
 
 constexpr int kMaxDev = 64;
@@ -2659,6 +3132,45 @@ int mx422_tables_for_current_device(int *waves)
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx422tab), tab.data(),
                                               tab.size() * sizeof(jx_mxtab)));
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx422B), ops, sizeof(uint16_t) * JX_MX_PARTS * 4 * 64 * 8));
+        if (!rc) {
+            /* k_mxs422's images: the B operands and k_mx422's LDS table (wave 0's layout: Y scales
+             * / limits at plan column j % 8, chroma at 8 + j), the per-wave scales, limits, scan */
+            std::vector<MxsImg422> img(2 * (JX_MAXQ + 1));
+            std::vector<MxsImg1> img1(img.size());
+            memset(img.data(), 0, img.size() * sizeof(MxsImg422));
+            memset(img1.data(), 0, img1.size() * sizeof(MxsImg1));
+            static const int scan[8][8] = JX_SCAN_ORDER_INIT;
+            for (size_t i = 0; i < img.size(); i++) {
+                const jx_mxtab &t = tab[i];
+                memcpy(img[i].B, ops, sizeof img[i].B);
+                for (unsigned tt = 0; tt < 4; tt++)
+                    for (unsigned jp = 0; jp < 16; jp++) {
+                        const unsigned n = tt < 2 ? (jp & 7u) : 8u + jp;
+                        float x[8];
+                        for (int pp = 0; pp < 4; pp++)
+                            for (int h = 0; h < 2; h++) {
+                                const int v = jx_pk_k(pp, h);
+                                x[2 * pp + h] = (tt & 1u) ? t.lsq[n][v] : t.w[n][v];
+                            }
+                        img[i].tab.wl[tt][0][jp] = mx_f4{x[0], x[1], x[2], x[3]};
+                        img[i].tab.wl[tt][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
+                    }
+                for (int h = 0; h < 2; h++)
+                    for (int jp = 0; jp < 16; jp++) {
+                        img1[i].sc.w[0][h][jp] = img[i].tab.wl[0][h][jp];
+                        img1[i].sc.w[1][h][jp] = img[i].tab.wl[2][h][jp];
+                    }
+                for (unsigned jp = 0; jp < 16; jp++) {
+                    img1[i].limc[0][jp] = mx_limc(img[i].tab, 1, jp);
+                    img1[i].limc[1][jp] = mx_limc(img[i].tab, 3, jp);
+                }
+                for (int uu = 0; uu < 8; uu++)
+                    for (int v = 0; v < 8; v++) img1[i].scan_t[uu][v] = (uint8_t)scan[v][uu];
+            }
+            rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs422_img), img.data(), img.size() * sizeof(MxsImg422)));
+            if (!rc)
+                rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs422_img1), img1.data(), img1.size() * sizeof(MxsImg1)));
+        }
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
@@ -2704,6 +3216,44 @@ int mx420_tables_for_current_device(int *waves)
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx420tab), tab.data(),
                                               tab.size() * sizeof(jx_mxtab)));
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx420B), ops, sizeof(uint16_t) * JX_MX_PARTS * 5 * 64 * 8));
+        if (!rc) {
+            /* k_mxs420's images (k_mx420's table layout, as k_mxs422's) */
+            std::vector<MxsImg420> img(2 * (JX_MAXQ + 1));
+            std::vector<MxsImg1> img1(img.size());
+            memset(img.data(), 0, img.size() * sizeof(MxsImg420));
+            memset(img1.data(), 0, img1.size() * sizeof(MxsImg1));
+            static const int scan[8][8] = JX_SCAN_ORDER_INIT;
+            for (size_t i = 0; i < img.size(); i++) {
+                const jx_mxtab &t = tab[i];
+                memcpy(img[i].B, ops, sizeof img[i].B);
+                for (unsigned tt = 0; tt < 4; tt++)
+                    for (unsigned jp = 0; jp < 16; jp++) {
+                        const unsigned n = tt < 2 ? (jp & 7u) : 8u + jp;
+                        float x[8];
+                        for (int pp = 0; pp < 4; pp++)
+                            for (int hh = 0; hh < 2; hh++) {
+                                const int v = jx_pk_k(pp, hh);
+                                x[2 * pp + hh] = (tt & 1u) ? t.lsq[n][v] : t.w[n][v];
+                            }
+                        img[i].tab.wl[tt][0][jp] = mx_f4{x[0], x[1], x[2], x[3]};
+                        img[i].tab.wl[tt][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
+                    }
+                for (int hh = 0; hh < 2; hh++)
+                    for (int jp = 0; jp < 16; jp++) {
+                        img1[i].sc.w[0][hh][jp] = img[i].tab.wl[0][hh][jp];
+                        img1[i].sc.w[1][hh][jp] = img[i].tab.wl[2][hh][jp];
+                    }
+                for (unsigned jp = 0; jp < 16; jp++) {
+                    img1[i].limc[0][jp] = mx_limc(img[i].tab, 1, jp);
+                    img1[i].limc[1][jp] = mx_limc(img[i].tab, 3, jp);
+                }
+                for (int uu = 0; uu < 8; uu++)
+                    for (int v = 0; v < 8; v++) img1[i].scan_t[uu][v] = (uint8_t)scan[v][uu];
+            }
+            rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs420_img), img.data(), img.size() * sizeof(MxsImg420)));
+            if (!rc)
+                rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs420_img1), img1.data(), img1.size() * sizeof(MxsImg1)));
+        }
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
@@ -2728,6 +3278,13 @@ extern "C" int jx_launch_mx420(const jx_xform_args *xa, void *stream)
     const int rc = mx420_tables_for_current_device(&waves);
     if (rc) return rc;
     const size_t mcus = (size_t)xa->g.nb / 4 * (size_t)xa->g.nframes;
+#ifndef JX_MX420_SHORT
+#define JX_MX420_SHORT 1                /* 1: k_mxs420 (a step pair per one-wave workgroup), 0: k_mx420 */
+#endif
+    if (JX_MX420_SHORT) {
+        hipLaunchKernelGGL(k_mxs420, dim3((unsigned)((mcus + 3) / 4)), dim3(64), 0, (hipStream_t)stream, *xa);
+        return mx_rc(hipGetLastError());
+    }
     const size_t chunks = (mcus + kCM420 - 1) / kCM420;
     const size_t w = std::min<size_t>(chunks, (size_t)std::max(waves, 4));
     const unsigned grid = (unsigned)((w + 3) / 4);
@@ -2745,6 +3302,14 @@ extern "C" int jx_launch_mx422(const jx_xform_args *xa, void *stream)
     if (rc) return rc;
     const size_t total = (size_t)xa->g.nb * (size_t)xa->g.nframes;
     const size_t nsteps = (total + 7) / 8;
+#ifndef JX_MX422_SHORT
+#define JX_MX422_SHORT 1                /* 1: k_mxs422 (short one-wave workgroups), 0: k_mx422 */
+#endif
+    if (JX_MX422_SHORT) {
+        hipLaunchKernelGGL(k_mxs422, dim3((unsigned)((nsteps + kMxs422C - 1) / kMxs422C)), dim3(64), 0,
+                           (hipStream_t)stream, *xa);
+        return mx_rc(hipGetLastError());
+    }
     const size_t w = std::min<size_t>(nsteps, (size_t)std::max(waves, 4));
     const unsigned grid = (unsigned)((w + 3) / 4);
     hipLaunchKernelGGL(k_mx422, dim3(grid), dim3(256), JX_MX_DYNLDS, (hipStream_t)stream, *xa);

@@ -5,6 +5,7 @@ that an issued MFMA may still read.  A chained product whose SrcC registers the 
 for an LDS read gave nondeterministic wrong C rows 12..15 (profiles/r03_mfma_war.txt), which
 parity tests only catch by luck -- so the property is checked on the ISA of every build."""
 import os
+import re
 import subprocess
 import sys
 
@@ -18,10 +19,21 @@ def test_mfma_operand_rule(tmp_path):
                     "-fno-slp-vectorize", "-I" + os.path.join(REPO, "include"), "--cuda-device-only", "-S",
                     os.path.join(PKG, "csrc", "jpgx_mx.hip"), "-o", str(asm)],
                    check=True, capture_output=True)
-    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), str(asm),
-                        "k_mx", "k_mxs", "k_mx422", "k_mx420"], capture_output=True, text=True)
+    names = ["k_mx", "k_mxs", "k_mx422", "k_mxs422", "k_mx420", "k_mxs420"]
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), str(asm)] + names,
+                       capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
-    assert r.stdout.count(" 0 load(s) into live MFMA operands") == 4, r.stdout
+    assert r.stdout.count(" 0 load(s) into live MFMA operands") == len(names), r.stdout
+    # the launched (short-wave) kernels: no scratch, no VGPR / SGPR spills
+    text = asm.read_text()
+    for n in ("k_mxs", "k_mxs422", "k_mxs420"):
+        m = re.search(r"\.name:\s+_ZN12_GLOBAL__N_1\d+%sE13jx_xform_args\s*\n(.*?)\.vgpr_spill_count:\s+(\d+)" % n,
+                      text, re.S)
+        assert m, n
+        meta = m.group(1)
+        assert int(re.search(r"\.private_segment_fixed_size:\s+(\d+)", meta).group(1)) == 0, n
+        assert int(re.search(r"\.sgpr_spill_count:\s+(\d+)", meta).group(1)) == 0, n
+        assert int(m.group(2)) == 0, n
 
 
 def test_mfma_operand_rule_catches_a_violation(tmp_path):
