@@ -241,7 +241,6 @@ def launch_ranks(n):
     here, one process per GPU, as a child torch.distributed.run (never an exec), before this
     process makes any GPU call; its exit code is ours.  Refused when the node has fewer GPUs than
     N, unless JPGX_BENCH_BACKEND=gloo asks for the rehearsal with ranks sharing the GPUs."""
-    import socket
     import subprocess
 
     import torch
@@ -250,13 +249,11 @@ def launch_ranks(n):
     if n > ndev and not rehearsal:
         log(f"bench: --gpus {n} but this node has {ndev} GPU(s)")
         return 2
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    # --standalone: the launcher binds its own free port on 127.0.0.1 and keeps it (no window
+    # between picking a port here and binding it there for another process to take it)
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.abspath(__file__)] + sys.argv[1:]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes=1", f"--nproc-per-node={n}", os.path.abspath(__file__)] + sys.argv[1:]
     log(f"bench: starting {n} ranks: {' '.join(cmd[2:])}")
     return subprocess.run(cmd, env=env).returncode
 

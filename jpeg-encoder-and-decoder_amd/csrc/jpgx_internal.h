@@ -13,6 +13,24 @@
 
 #define JX_WG 256           /* threads per workgroup for the transform (4 waves)           */
 
+/* unsigned 32-bit division by a launch constant d >= 1 as a multiply-high (Granlund and
+ * Montgomery's round-up method): q = (t + ((n - t) >> s1)) >> s2, t = mulhi(m, n); exact for
+ * every 32-bit n.  Lets a wave find its position with a few scalar operations instead of the
+ * ~35-instruction software division. */
+struct jx_udiv {
+    uint32_t m, s1, s2;
+};
+static inline struct jx_udiv jx_udiv_make(uint32_t d)
+{
+    unsigned l = 0;
+    while (l < 32 && (1ull << l) < (unsigned long long)d) l++;
+    struct jx_udiv r;
+    r.m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+    r.s1 = l ? 1u : 0u;
+    r.s2 = l ? l - 1u : 0u;
+    return r;
+}
+
 struct jx_geom {
     const uint8_t *rgb;     /* pixel (0, 8*row_begin) of frame 0                          */
     int16_t *out;           /* frame 0 output [3][nb][64]                                 */
@@ -24,6 +42,7 @@ struct jx_geom {
     int nframes;
     int row0;               /* frame block-row of stripe row 0 (underflow only at row 0)  */
     uint32_t under[6];      /* the underflow pixel row, interleaved (u0 u0 u0 u1 u1 u1..)  */
+    struct jx_udiv dnb, dbpr;   /* division by nb and by bpr                              */
 };
 
 /* Per-quality tables, device resident (one copy per quality 1..97, built once per device).

@@ -877,6 +877,8 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     g.nb = (int)nb;
     g.nframes = fr->nframes;
     g.row0 = fr->row_begin;
+    g.dnb = jx_udiv_make((uint32_t)nb);
+    g.dbpr = jx_udiv_make((uint32_t)bpr);
     jx_under_dwords(p->underflow, g.under);
     rc = tables_for_current_device();
     if (rc) return rc;

@@ -9,17 +9,22 @@
  * JpgData.zig_zag_* arrays, [frame][Y|Cb|Cr][nb][64] int16.
  *
  * Work unit: a "step" of 8 consecutive blocks (launch-global block index, frames
- * concatenated); persistent waves take chunks of 4 steps grid-stride (mx_span_init).
+ * concatenated).  The launched kernel (round 4) is k_mxs: short-lived waves, JX_MXS_C = 3
+ * steps per wave, one workgroup of JX_MXS_WPG = 4 waves sharing an LDS image of the B operands
+ * and tables; a wave issues the DMA of all its steps up front and exits after its third store.
+ * k_mx (JX_MX_SHORT=0) is the round-3 persistent form: chunks of kChunk steps grid-stride
+ * (mx_span_init), DMA two steps ahead in a 3-slot ring.
  *   Input   the step's 8 pixel rows x 8 blocks x 24 B land in a 1.5-KiB LDS slot ([y][24 jb + k])
- *           by LDS-DMA (16-byte pieces), issued two steps ahead (3-slot ring).
+ *           by LDS-DMA (16-byte pieces).
  *   Rows    set s (blocks 4s..4s+3), half h (pixel rows 4h..4h+3): a 16 x 32 f16 A operand,
  *           row m = 4 jb + y, k = byte k of the pixel row (zero-extended: the f16 b 2^-24,
  *           exact, one v_perm per two bytes; k = 24 the bias 1.0).  One product with B = colour x cosine gives, in C row m, column j, the
  *           row transform of channel j/8 (Y, Cb), frequency u = j%8.  Cr: the two sets
  *           concatenated along K (B zero outside its set's columns), so column j of the Cr tile
- *           is set j/8's Cr at u = j%8.  B = Bh + 2^-12 Bl (JX_MX_PARTS = 2 f16 parts; 3 adds a
+ *           is set j/8's Cr at u = j%8.  B = Bh + Bl (JX_MX_PARTS = 2 f16 parts; 3 adds a
  *           second lo part for a 1.28x narrower band at 50% more MFMAs, measured slower); acc_h =
- *           A Bh is EXACT in any summation order (jpgx_plan.cpp); R = acc_h + 2^-12 acc_l.
+ *           A Bh is EXACT in any summation order (jpgx_plan.cpp); R = acc_h + acc_l (JX_MX_LOEXP
+ *           = 0: Bl encoded at Bh's scale, so the combine is one packed add).
  *   Columns every lane then holds three whole columns (8 rows, registers 0..3 of the two
  *           halves): (set 0, c = j/8, u), (set 1, same), (Cr, set j/8, u).  Each runs jx_fdct8_pk
  *           (lane by lane the FOps code the band is derived for), the quantiser tm = F w +
@@ -27,11 +32,11 @@
  *           stage at its zig-zag position, and the band test d^2 - lsq >= 0 (d = F w - rint,
  *           exact) folded into a running max.
  *   Exact   (rare) a column whose max says "some coefficient in the band" records its flagged
- *           v's; the step's flagged blocks' pixel rows are copied to a per-wave LDS side buffer
- *           with their tasks (mx_defer); eight tasks at a time, eight lanes each (mx_flush):
- *           lane x forms (X(x,y) c_u[x]) c_v[y] in fp64, the sum runs x-outer / y-inner
- *           (dct.c:46-50) lane to lane over DPP, F = ((1/4 a(u)) a(v)) s, round(F / Q) goes to
- *           HBM after the wave's own stores of those blocks have landed.
+ *           v's; k_mxs recomputes them in the step, from the pixels still in its LDS slot, into
+ *           the stage before the store (mx_exact_inline); k_mx defers them to a per-wave side
+ *           buffer (mx_defer / mx_flush).  Eight tasks at a time, eight lanes each: lane x forms
+ *           (X(x,y) c_u[x]) c_v[y] in fp64, the sum runs x-outer / y-inner (dct.c:46-50) lane
+ *           to lane over DPP, F = ((1/4 a(u)) a(v)) s, round(F / Q).
  *   Output  channel c's 8 blocks x 128 B leave as one 1-KiB nontemporal store.
  */
 #include <hip/hip_runtime.h>
@@ -194,7 +199,14 @@ struct MxG {
     int row0, quality, force;
     bool lin_store;                     /* plane offsets fit the stores' 32-bit lane offsets */
     uint32_t u[6];                      /* the underflow pixel row (jx_geom.under) */
+    jx_udiv dnb, dbpr;                  /* division by nb, by bpr (jx_geom) */
 };
+
+__device__ __forceinline__ unsigned mx_udiv(unsigned n, const jx_udiv &d)
+{
+    const unsigned t = __umulhi(d.m, n);
+    return (t + ((n - t) >> d.s1)) >> d.s2;
+}
 
 /* A step's position: frame f, block bi in the frame, block-row r, column c, and running
  * pointers to its pixel (8c, 8r) and to its first block's channel-0 output. */
@@ -213,9 +225,9 @@ __device__ __forceinline__ void mx_ptrs(MxCur &P, const MxG &g)
 
 __device__ __forceinline__ void mx_seek(MxCur &P, const MxG &g, unsigned b0)
 {
-    P.f = b0 / g.nb;
+    P.f = mx_udiv(b0, g.dnb);
     P.bi = b0 - P.f * g.nb;
-    P.r = P.bi / g.bpr;
+    P.r = mx_udiv(P.bi, g.dbpr);
     P.c = P.bi - P.r * g.bpr;
     mx_ptrs(P, g);
 }
@@ -721,6 +733,8 @@ __global__ __launch_bounds__(256, JX_MX_WPE) void k_mx(const jx_xform_args a)
     g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
 #pragma unroll
     for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+    g.dnb = a.g.dnb;
+    g.dbpr = a.g.dbpr;
 
     const unsigned lane = threadIdx.x & 63u;
     MxLds &L = s_lds[threadIdx.x >> 6];
@@ -1018,9 +1032,9 @@ using MxsShared = std::conditional<kMxsWPG == 1, MxsImg1, MxsImg>::type;
 /* where the B operands and the column tables come from (four-wave image / one-wave image) */
 typedef mx_u4 MxsBOps[3 * JX_MX_PARTS][64];
 __device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg &l, const MxsImg &) { return l.B; }
-__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg1 &, const MxsImg &g) { return g.B; }
+[[maybe_unused]] __device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg1 &, const MxsImg &g) { return g.B; }
 __device__ __forceinline__ const MxTab &mxs_tb(const MxsImg &l, const MxsImg &) { return l.tab; }
-__device__ __forceinline__ MxsTabRef mxs_tb(const MxsImg1 &l, const MxsImg &g) { return MxsTabRef{l.sc, g.tab}; }
+[[maybe_unused]] __device__ __forceinline__ MxsTabRef mxs_tb(const MxsImg1 &l, const MxsImg &g) { return MxsTabRef{l.sc, g.tab}; }
 #ifdef JX_MXS_STAMP                    /* timing probe builds only: per-wave timestamps */
 __device__ unsigned long long g_mxs_ts[1u << 20];
 #define JX_MXS_TS(i, v) do { if (lane == 0 && 8u * wv + 8u <= (1u << 20)) g_mxs_ts[8u * wv + (i)] = (v); } while (0)
@@ -1141,6 +1155,8 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
     g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
 #pragma unroll
     for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+    g.dnb = a.g.dnb;
+    g.dbpr = a.g.dbpr;
 
 #ifdef JX_MXS_STAMP
     const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime(), cs0 = __builtin_amdgcn_s_memtime();
@@ -1704,6 +1720,8 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
     g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
 #pragma unroll
     for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+    g.dnb = a.g.dnb;
+    g.dbpr = a.g.dbpr;
 
     const unsigned lane = threadIdx.x & 63u;
     Mx422Lds &L = s_lds[threadIdx.x >> 6];
@@ -1955,6 +1973,8 @@ __global__ __launch_bounds__(64, JX_MX422_WPE) void k_mxs422(const jx_xform_args
     g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
 #pragma unroll
     for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+    g.dnb = a.g.dnb;
+    g.dbpr = a.g.dbpr;
 
     const unsigned lane = threadIdx.x & 63u;
     const MxsImg422 &gimg = g_mxs422_img[g.force ? 1 : 0][g.quality];
@@ -2490,6 +2510,8 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
     g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
 #pragma unroll
     for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+    g.dnb = a.g.dnb;
+    g.dbpr = a.g.dbpr;
     Mx420G h;
     h.mpr = g.bpr / 2u;
     h.rows = g.nb / g.bpr / 2u;
@@ -2786,6 +2808,8 @@ __global__ __launch_bounds__(64, JX_MX420_WPE) void k_mxs420(const jx_xform_args
     g.lin_store = (unsigned long long)g.nb * 256ull + 1024ull < (1ull << 31);
 #pragma unroll
     for (int k = 0; k < 6; k++) g.u[k] = a.g.under[k];
+    g.dnb = a.g.dnb;
+    g.dbpr = a.g.dbpr;
     Mx420G h;
     h.mpr = g.bpr / 2u;
     h.rows = g.nb / g.bpr / 2u;

@@ -482,6 +482,22 @@ int main(int argc, char **argv)
         skel<128, 16, 24, 4, 2, 1, 0>(3, 0);
         skel<128, 16, 24, 4, 2, 1, 0>(2, 0);
     }
+    if (!strcmp(which, "r4c")) {
+        /* occupancy (waves per SIMD, pinned by LDS) and MFMA count at k_mxs-like compute, non-persistent */
+        skel<0, 0, 0, 3, 2, 1, 0>(4, 0);
+        skel<128, 16, 24, 3, 2, 1, 0>(3, 0);
+        skel<128, 16, 24, 3, 2, 1, 0>(4, 0);
+        skel<128, 16, 24, 3, 2, 1, 0>(5, 0);
+        skel<128, 16, 24, 3, 2, 1, 0>(6, 0);
+        skel<128, 16, 24, 2, 1, 1, 0>(5, 0);
+        skel<128, 16, 24, 2, 1, 1, 0>(6, 0);
+        skel<128, 0, 24, 3, 2, 1, 0>(4, 0);
+        skel<128, 8, 24, 3, 2, 1, 0>(4, 0);
+        skel<96, 16, 24, 3, 2, 1, 0>(4, 0);
+        skel<96, 16, 24, 3, 2, 1, 0>(5, 0);
+        skel<128, 16, 24, 3, 1, 1, 0>(4, 0);       /* 3 steps through 2 slots */
+        skel<128, 16, 24, 3, 1, 1, 0>(5, 0);
+    }
     if (!strcmp(which, "r4")) {
         /* round 4: non-persistent grids (one chunk per wave) with random-operand compute, and the
          * VALU -> MFMA trade (same memory pattern, 4 waves per SIMD) */
