@@ -233,7 +233,19 @@ def sub_kernel_name(sr):
     """The kernels a true-subsampling launch runs (jpgx_blocks_gpu's dispatch)."""
     if alt_selected():
         return f"k_xform(Y)+k_chroma<{sr}>"
-    return "k_mx422" if sr == 1 else "k_mx420"
+    return mx_kernel_name(sr)
+
+
+def mx_kernel_name(sr):
+    """The MFMA kernel this library's launch runs for sample ratio sr (0 = 4:4:4): k_mxs /
+    k_mxs422 / k_mxs420 (short-lived waves), or the persistent k_mx* of a variant build."""
+    import ctypes
+
+    import jpgx
+    f = jpgx.lib.jx_mx_kernel_name
+    f.restype = ctypes.c_char_p
+    f.argtypes = [ctypes.c_int]
+    return f(sr).decode()
 
 
 def launch_ranks(n):
@@ -293,7 +305,7 @@ def main():
         os.environ["JPGX_LIB"] = ALT_LIB
     elif args.kernel == "mx" and alt_selected():
         os.environ.pop("JPGX_LIB")                # --kernel mx: the product library, whatever the env said
-    kname = "k_xform" if alt_selected() else "k_mx"
+    kname = "k_xform" if alt_selected() else mx_kernel_name(0)
 
     import torch
     import torch.distributed as dist

@@ -3374,3 +3374,12 @@ extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)
     hipLaunchKernelGGL(k_mx, dim3(grid), dim3(256), JX_MX_DYNLDS, (hipStream_t)stream, *xa);
     return mx_rc(hipGetLastError());
 }
+
+/* the kernel a launch of this build runs for sample ratio 0 (4:4:4), 1 (true 4:2:2), 2 (4:2:0):
+ * bench.py and the profiles name the kernel they time with it */
+extern "C" const char *jx_mx_kernel_name(int sr)
+{
+    if (sr == 1) return JX_MX422_SHORT ? "k_mxs422" : "k_mx422";
+    if (sr == 2) return JX_MX420_SHORT ? "k_mxs420" : "k_mx420";
+    return JX_MX_SHORT ? "k_mxs" : "k_mx";
+}

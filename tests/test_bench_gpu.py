@@ -29,7 +29,7 @@ def test_bench_single_gpu_line():
     assert KEYS <= d.keys() and d["n_gpus"] == 1
     assert d["output_check"]["ok"] and d["output_check"]["frames_checked"] == 8
     rf = d["roofline"]
-    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel"] == "k_mx"
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel"] == "k_mxs"
 
 
 def test_bench_two_ranks_rehearsal():

@@ -11,12 +11,14 @@ import csv
 import hashlib
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "csrc")
 KSRCS = {"k_mx": ("jpgx_mx.hip", "jpgx_internal.h", "xform_math.h", "jx_consts.h"),
+         "k_mxs": ("jpgx_mx.hip", "jpgx_internal.h", "xform_math.h", "jx_consts.h"),
          "k_xform": ("jpgx_kernels.hip", "jpgx_internal.h", "xform_math.h", "jx_consts.h")}
 BYTES_PER_LAUNCH = 8 * 3840 * 2160 * 9          # bench.py workload, 9 B/px algorithmic
 
@@ -30,12 +32,18 @@ def kernel_source_sha(kernel="k_mx"):
     return h.hexdigest()
 
 
+def is_kernel(name, kernel):
+    """name (mangled `..15k_mxsE..` or demangled `..::k_mxs(..`) is exactly `kernel`, not a
+    longer name that starts with it (k_mx vs k_mxs / k_mx422)"""
+    return re.search(r"(?<![A-Za-z_])%s(?=[(E<]|$)" % re.escape(kernel), name) is not None
+
+
 def counters(path, kernel="k_xform"):
     """{counter: [per-dispatch values]} for dispatches of `kernel` (summed over dimensions)."""
     per = defaultdict(lambda: defaultdict(float))
     with open(path) as f:
         for row in csv.DictReader(f):
-            if kernel not in row["Kernel_Name"]:
+            if not is_kernel(row["Kernel_Name"], kernel):
                 continue
             per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
     return {k: [v[d] for d in sorted(v, key=int)] for k, v in per.items()}
@@ -45,7 +53,7 @@ def trace_ms(path, kernel="k_xform"):
     out = []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if kernel in row["Kernel_Name"]:
+            if is_kernel(row["Kernel_Name"], kernel):
                 out.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
     return out
 
@@ -76,7 +84,7 @@ def main(src, dst, kernel="k_xform"):
         if os.path.exists(f):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if kernel in row["Name"]:
+                    if is_kernel(row["Name"], kernel):
                         res["rocprof_stats"] = {k: row[k] for k in row}
     tr = os.path.join(src, "prof", "run_kernel_trace.csv")
     if os.path.exists(tr):
