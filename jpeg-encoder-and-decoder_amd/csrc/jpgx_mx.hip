@@ -1136,6 +1136,9 @@ __device__ __forceinline__ void mxs_issue(const MxsCur &P, const MxG &g, uint8_t
     }
 }
 
+#ifdef JX_MXS_NUMVGPR
+__attribute__((amdgpu_waves_per_eu(JX_MXS_NUMVGPR, JX_MXS_NUMVGPR)))
+#endif
 __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_args a)
 {
     __shared__ __attribute__((aligned(16))) MxsLds s_lds[kMxsWPG];
@@ -1223,11 +1226,16 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
 #pragma unroll
         for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
     }
+#ifndef JX_MXS_BLDS
+#define JX_MXS_BLDS 0                   /* 1: B operands read from the LDS image every step (fewer VGPRs) */
+#endif
+#if !JX_MXS_BLDS
     mx_u4 B[kParts][3];
 #pragma unroll
     for (int p = 0; p < kParts; p++)
 #pragma unroll
         for (int w = 0; w < 3; w++) B[p][w] = mxs_B(s_img, gimg)[3 * p + w][lane];
+#endif
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
     const auto &tb = mxs_tb(s_img, gimg);
 #ifdef JX_MXS_STAMP
@@ -1264,6 +1272,13 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         const mx_u2 d10 = *(const mx_u2 *)(sp + aoff + 96u);
         const mx_u2 d11 = *(const mx_u2 *)(sp + aoff + 864u);
         const MxW w0 = mx_w(tb, 0, j);
+#if JX_MXS_BLDS
+        mx_u4 B[kParts][3];
+#pragma unroll
+        for (int p = 0; p < kParts; p++)
+#pragma unroll
+            for (int w = 0; w < 3; w++) B[p][w] = mxs_B(s_img, gimg)[3 * p + w][lane];
+#endif
         const mx_h8 A00 = mx_aop(d00, s0, s1, s2), A01 = mx_aop(d01, s0, s1, s2);
         const mx_h8 A10 = mx_aop(d10, s0, s1, s2), A11 = mx_aop(d11, s0, s1, s2);
         __builtin_amdgcn_sched_barrier(0);
