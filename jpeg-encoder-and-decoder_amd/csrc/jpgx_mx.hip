@@ -1968,11 +1968,37 @@ struct alignas(16) MxsImg422 {
 };
 __device__ MxsImg422 g_mxs422_img[2][JX_MAXQ + 1];
 __device__ MxsImg1 g_mxs422_img1[2][JX_MAXQ + 1];
-
-__global__ __launch_bounds__(64, JX_MX422_WPE) void k_mxs422(const jx_xform_args a)
+/* waves per workgroup: 1 (B operands from the global image) or 4 (B, scales, limc and the zig-zag
+ * table in LDS, shared through one s_barrier; band limits from the global image, rare path) */
+#ifndef JX_MXS422_WPG
+#define JX_MXS422_WPG 1
+#endif
+constexpr unsigned kMxs422WPG = JX_MXS422_WPG;
+static_assert(kMxs422WPG == 1 || kMxs422WPG == 4, "1 or 4 waves per workgroup");
+struct alignas(16) MxsImg422w {
+    mx_u4 B[JX_MX_PARTS * 4][64];
+    MxsImg1 s;
+};
+constexpr unsigned kMxs422Pieces = sizeof(MxsImg422w) / 16;
+static_assert(kMxs422Pieces <= 768 && (kMxs422WPG == 1 || sizeof(Mxs422Lds) * 4 + sizeof(MxsImg422w) <= 40 * 1024),
+              "4 workgroups of 4 waves per CU");
+__device__ MxsImg422w g_mxs422_imgw[2][JX_MAXQ + 1];
+typedef std::conditional<kMxs422WPG == 4, MxsImg422w, MxsImg1>::type Mxs422Shared;
+[[maybe_unused]] __device__ __forceinline__ const MxsImg1 &mxs422_s(const MxsImg422w &l) { return l.s; }
+[[maybe_unused]] __device__ __forceinline__ const MxsImg1 &mxs422_s(const MxsImg1 &l) { return l; }
+[[maybe_unused]] __device__ __forceinline__ const mx_u4 (&mxs422_B(const MxsImg422w &l, const MxsImg422 &))[JX_MX_PARTS * 4][64]
 {
-    __shared__ __attribute__((aligned(16))) Mxs422Lds L;
-    __shared__ __attribute__((aligned(16))) MxsImg1 s_img;
+    return l.B;
+}
+[[maybe_unused]] __device__ __forceinline__ const mx_u4 (&mxs422_B(const MxsImg1 &, const MxsImg422 &g))[JX_MX_PARTS * 4][64]
+{
+    return g.B;
+}
+
+__global__ __launch_bounds__(64 * kMxs422WPG, JX_MX422_WPE) void k_mxs422(const jx_xform_args a)
+{
+    __shared__ __attribute__((aligned(16))) Mxs422Lds s_lds[kMxs422WPG];
+    __shared__ __attribute__((aligned(16))) Mxs422Shared s_img;
     MxG g;
     g.rgb = a.g.rgb;
     g.out = a.g.out;
@@ -1992,14 +2018,24 @@ __global__ __launch_bounds__(64, JX_MX422_WPE) void k_mxs422(const jx_xform_args
     g.dbpr = a.g.dbpr;
 
     const unsigned lane = threadIdx.x & 63u;
+    const unsigned wave = kMxs422WPG == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    Mxs422Lds &L = s_lds[wave];
     const MxsImg422 &gimg = g_mxs422_img[g.force ? 1 : 0][g.quality];
-    {
+    if constexpr (kMxs422WPG == 4) {
+        const uint8_t *img = (const uint8_t *)&g_mxs422_imgw[g.force ? 1 : 0][g.quality];
+#pragma unroll
+        for (unsigned i = 0; i < 3; i++) {
+            const unsigned piece = 256u * i + threadIdx.x;
+            if (256u * i + 64u * wave < kMxs422Pieces && piece < kMxs422Pieces)
+                mxs_dma<16>(img + 16u * piece, (uint8_t *)&s_img + 16u * (256u * i + 64u * wave));
+        }
+    } else {
         constexpr unsigned kP1 = sizeof(MxsImg1) / 16;
         const uint8_t *img = (const uint8_t *)&g_mxs422_img1[g.force ? 1 : 0][g.quality];
         mxs_dma<16>(img + 16u * lane, &s_img);
         if (lane < kP1 - 64u) mxs_dma<16>(img + 16u * (64u + lane), (uint8_t *)&s_img + 1024u);
     }
-    const unsigned wv = blockIdx.x;
+    const unsigned wv = blockIdx.x * kMxs422WPG + wave;
     const uint32_t off0 = (uint32_t)((lane / 12u) * (unsigned)g.pitch + 16u * (lane % 12u));
     const uint32_t off1 = (uint32_t)(((64u + lane) / 12u) * (unsigned)g.pitch + 16u * ((64u + lane) % 12u));
     MxsCur iss;
@@ -2027,13 +2063,18 @@ __global__ __launch_bounds__(64, JX_MX422_WPE) void k_mxs422(const jx_xform_args
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
     const jx_mxtab &T = g_mx422tab[g.force ? 1 : 0][g.quality];
 
-    if (cmp.b >= g.total) return;
+    if constexpr (kMxs422WPG == 1) {
+        if (cmp.b >= g.total) return;
+    }
     mx_wait_vm<2u * kMxs422C>();                    /* the image (older than the pixel DMA) */
+    if constexpr (kMxs422WPG == 4) __builtin_amdgcn_s_barrier();
     mx_wave_sync();
+    if (cmp.b >= g.total) return;
+    const MxsImg1 &si = mxs422_s(s_img);
     uint32_t za[8];
     {
         const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * ((j >> 3) * 4u + gq);
-        const mx_u2 sc = *(const mx_u2 *)&s_img.scan_t[u][0];
+        const mx_u2 sc = *(const mx_u2 *)&si.scan_t[u][0];
 #pragma unroll
         for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
     }
@@ -2041,9 +2082,9 @@ __global__ __launch_bounds__(64, JX_MX422_WPE) void k_mxs422(const jx_xform_args
 #pragma unroll
     for (int p = 0; p < kParts; p++)
 #pragma unroll
-        for (int w = 0; w < 4; w++) B[p][w] = gimg.B[4 * p + w][lane];
-    const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
-    const MxsTabRef tb{s_img.sc, gimg.tab};
+        for (int w = 0; w < 4; w++) B[p][w] = mxs422_B(s_img, gimg)[4 * p + w][lane];
+    const float limc0 = si.limc[0][j], limc2 = si.limc[1][j];
+    const MxsTabRef tb{si.sc, gimg.tab};
 
     const auto body = [&](const MxsCur &S, uint8_t *sp) __attribute__((always_inline)) {
         if (!S.simple) {
@@ -2789,25 +2830,58 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
  */
 struct alignas(16) Mxs420Lds {
     uint8_t ring[2][kSlot];             /* [y 0..15][4 blocks x 24 B] */
-    uint8_t stage[16 * kBS];
-    uint8_t qtrue[2][384];              /* general step: MCU's right column, true rows [16][24] */
+    union {
+        uint8_t stage[16 * kBS];
+        struct {                        /* general step: MCU's right column, true rows [16][24]; read
+                                           for the A operands before the chroma column writes here */
+            uint8_t y_[kSt420C];
+            uint8_t qtrue[2][384];
+        };
+    };
     mx_f4 rA[64];                       /* step 0's chroma R (not held across step 0's exact pass) */
     uint16_t task[8];
 };
-static_assert(sizeof(Mxs420Lds) % 16 == 0 &&
-                  (sizeof(Mxs420Lds) + sizeof(MxsImg1) + 511) / 512 * 512 * 16 <= 160 * 1024,
-              "16 one-wave workgroups per CU");
+static_assert(2 * 384 <= 16 * kBS - kSt420C, "qtrue inside the chroma stage");
+/* waves per workgroup: 1 (B operands from the global image, the scales in the wave's LDS) or 4
+ * (the whole image in LDS, shared through one s_barrier) */
+#ifndef JX_MXS420_WPG
+#define JX_MXS420_WPG 1
+#endif
+constexpr unsigned kMxs420WPG = JX_MXS420_WPG;
+static_assert(kMxs420WPG == 1 || kMxs420WPG == 4, "1 or 4 waves per workgroup");
 struct alignas(16) MxsImg420 {
     mx_u4 B[JX_MX_PARTS * 5][64];
     MxTab tab;
+    float limc[2][16];
+    uint8_t scan_t[8][8];
 };
+constexpr unsigned kMxs420Pieces = sizeof(MxsImg420) / 16;
+static_assert(sizeof(MxsImg420) % 16 == 0 && kMxs420Pieces <= 1024, "four 16-byte pieces per thread");
+static_assert(sizeof(Mxs420Lds) % 16 == 0 &&
+                  (kMxs420WPG == 4 ? sizeof(Mxs420Lds) * 4 + sizeof(MxsImg420) <= 40 * 1024
+                                   : sizeof(Mxs420Lds) + sizeof(MxsImg1) <= 10 * 1024),
+              "16 waves per CU");
 __device__ MxsImg420 g_mxs420_img[2][JX_MAXQ + 1];
 __device__ MxsImg1 g_mxs420_img1[2][JX_MAXQ + 1];
-
-__global__ __launch_bounds__(64, JX_MX420_WPE) void k_mxs420(const jx_xform_args a)
+typedef std::conditional<kMxs420WPG == 4, MxsImg420, MxsImg1>::type Mxs420Shared;
+[[maybe_unused]] __device__ __forceinline__ const mx_u4 (&mxs420_B(const MxsImg420 &l, const MxsImg420 &))[JX_MX_PARTS * 5][64]
 {
-    __shared__ __attribute__((aligned(16))) Mxs420Lds L;
-    __shared__ __attribute__((aligned(16))) MxsImg1 s_img;
+    return l.B;
+}
+[[maybe_unused]] __device__ __forceinline__ const mx_u4 (&mxs420_B(const MxsImg1 &, const MxsImg420 &g))[JX_MX_PARTS * 5][64]
+{
+    return g.B;
+}
+[[maybe_unused]] __device__ __forceinline__ const MxTab &mxs420_tb(const MxsImg420 &l, const MxsImg420 &) { return l.tab; }
+[[maybe_unused]] __device__ __forceinline__ MxsTabRef mxs420_tb(const MxsImg1 &l, const MxsImg420 &g)
+{
+    return MxsTabRef{l.sc, g.tab};
+}
+
+__global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const jx_xform_args a)
+{
+    __shared__ __attribute__((aligned(16))) Mxs420Lds s_lds[kMxs420WPG];
+    __shared__ __attribute__((aligned(16))) Mxs420Shared s_img;
     MxG g;
     g.rgb = a.g.rgb;
     g.out = a.g.out;
@@ -2832,15 +2906,25 @@ __global__ __launch_bounds__(64, JX_MX420_WPE) void k_mxs420(const jx_xform_args
     h.tm = h.nmcu * (unsigned)a.g.nframes;
 
     const unsigned lane = threadIdx.x & 63u;
+    const unsigned wave = kMxs420WPG == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    Mxs420Lds &L = s_lds[wave];
     const MxsImg420 &gimg = g_mxs420_img[g.force ? 1 : 0][g.quality];
-    {
+    if constexpr (kMxs420WPG == 4) {
+        const uint8_t *img = (const uint8_t *)&gimg;
+#pragma unroll
+        for (unsigned i = 0; i < 4; i++) {
+            const unsigned piece = 256u * i + threadIdx.x;
+            if (256u * i + 64u * wave < kMxs420Pieces && piece < kMxs420Pieces)
+                mxs_dma<16>(img + 16u * piece, (uint8_t *)&s_img + 16u * (256u * i + 64u * wave));
+        }
+    } else {
         constexpr unsigned kP1 = sizeof(MxsImg1) / 16;
         const uint8_t *img = (const uint8_t *)&g_mxs420_img1[g.force ? 1 : 0][g.quality];
         mxs_dma<16>(img + 16u * lane, &s_img);
         if (lane < kP1 - 64u) mxs_dma<16>(img + 16u * (64u + lane), (uint8_t *)&s_img + 1024u);
     }
     /* the pair: MCUs m0 .. m0 + 3; simple = one MCU row of one frame, no row-last MCU, in range */
-    const unsigned m0 = 4u * blockIdx.x;
+    const unsigned m0 = 4u * (blockIdx.x * kMxs420WPG + wave);
     const uint32_t off0 = (uint32_t)((lane / 6u) * (unsigned)g.pitch + 16u * (lane % 6u));
     const uint32_t off1 = (uint32_t)(((64u + lane) / 6u) * (unsigned)g.pitch + 16u * ((64u + lane) % 6u));
     Mx420Chunk cc;
@@ -2875,9 +2959,13 @@ __global__ __launch_bounds__(64, JX_MX420_WPE) void k_mxs420(const jx_xform_args
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
     const jx_mxtab &T = g_mx420tab[g.force ? 1 : 0][g.quality];
 
-    if (m0 >= h.tm) return;
+    if constexpr (kMxs420WPG == 1) {
+        if (m0 >= h.tm) return;
+    }
     mx_wait_vm<4>();                                    /* the image (older than the pixel DMA) */
+    if constexpr (kMxs420WPG == 4) __builtin_amdgcn_s_barrier();
     mx_wave_sync();
+    if (m0 >= h.tm) return;
     uint32_t za[8];
     {
         const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * (4u * (j >> 3) + gq);
@@ -2889,9 +2977,9 @@ __global__ __launch_bounds__(64, JX_MX420_WPE) void k_mxs420(const jx_xform_args
 #pragma unroll
     for (int p = 0; p < kParts; p++)
 #pragma unroll
-        for (int w = 0; w < 5; w++) B[p][w] = gimg.B[5 * p + w][lane];
+        for (int w = 0; w < 5; w++) B[p][w] = mxs420_B(s_img, gimg)[5 * p + w][lane];
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
-    const MxsTabRef tb{s_img.sc, gimg.tab};
+    const auto &tb = mxs420_tb(s_img, gimg);
 
     const auto step = [&](auto kc) __attribute__((always_inline)) {
         constexpr unsigned k = decltype(kc)::value;
@@ -3209,6 +3297,14 @@ int mx422_tables_for_current_device(int *waves)
             rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs422_img), img.data(), img.size() * sizeof(MxsImg422)));
             if (!rc)
                 rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs422_img1), img1.data(), img1.size() * sizeof(MxsImg1)));
+            if (!rc) {
+                std::vector<MxsImg422w> imgw(img.size());
+                for (size_t i = 0; i < img.size(); i++) {
+                    memcpy(imgw[i].B, img[i].B, sizeof imgw[i].B);
+                    imgw[i].s = img1[i];
+                }
+                rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs422_imgw), imgw.data(), imgw.size() * sizeof(MxsImg422w)));
+            }
         }
         int cus = 0, per_cu = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -3288,6 +3384,8 @@ int mx420_tables_for_current_device(int *waves)
                 }
                 for (int uu = 0; uu < 8; uu++)
                     for (int v = 0; v < 8; v++) img1[i].scan_t[uu][v] = (uint8_t)scan[v][uu];
+                memcpy(img[i].limc, img1[i].limc, sizeof img[i].limc);
+                memcpy(img[i].scan_t, img1[i].scan_t, sizeof img[i].scan_t);
             }
             rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs420_img), img.data(), img.size() * sizeof(MxsImg420)));
             if (!rc)
@@ -3321,7 +3419,9 @@ extern "C" int jx_launch_mx420(const jx_xform_args *xa, void *stream)
 #define JX_MX420_SHORT 1                /* 1: k_mxs420 (a step pair per one-wave workgroup), 0: k_mx420 */
 #endif
     if (JX_MX420_SHORT) {
-        hipLaunchKernelGGL(k_mxs420, dim3((unsigned)((mcus + 3) / 4)), dim3(64), 0, (hipStream_t)stream, *xa);
+        const size_t waves = (mcus + 3) / 4;
+        hipLaunchKernelGGL(k_mxs420, dim3((unsigned)((waves + kMxs420WPG - 1) / kMxs420WPG)), dim3(64 * kMxs420WPG), 0,
+                           (hipStream_t)stream, *xa);
         return mx_rc(hipGetLastError());
     }
     const size_t chunks = (mcus + kCM420 - 1) / kCM420;
@@ -3345,7 +3445,8 @@ extern "C" int jx_launch_mx422(const jx_xform_args *xa, void *stream)
 #define JX_MX422_SHORT 1                /* 1: k_mxs422 (short one-wave workgroups), 0: k_mx422 */
 #endif
     if (JX_MX422_SHORT) {
-        hipLaunchKernelGGL(k_mxs422, dim3((unsigned)((nsteps + kMxs422C - 1) / kMxs422C)), dim3(64), 0,
+        const size_t waves = (nsteps + kMxs422C - 1) / kMxs422C;
+        hipLaunchKernelGGL(k_mxs422, dim3((unsigned)((waves + kMxs422WPG - 1) / kMxs422WPG)), dim3(64 * kMxs422WPG), 0,
                            (hipStream_t)stream, *xa);
         return mx_rc(hipGetLastError());
     }
