@@ -362,3 +362,44 @@ def test_product_entry_points_fail_loudly_without_a_gpu():
         jpgx.HostContext(2)
     assert e.value.rc == jpgx.ENODEV
     assert jpgx.device_count() == 0
+
+
+def test_launch_constant_division_is_exact(tmp_path):
+    """jx_udiv_make (jpgx_internal.h): the multiply-high division a wave uses to find its frame,
+    block-row and column (mx_seek) equals n / d for every divisor shape the launches use (frame
+    and row block counts, powers of two, 1, the extremes) and random 32-bit numerators."""
+    src = tmp_path / "udiv.cpp"
+    src.write_text(r'''
+#include <stdio.h>
+#include "jpgx_internal.h"
+static unsigned dv(unsigned n, jx_udiv d) {
+    const unsigned t = (unsigned)(((unsigned long long)d.m * n) >> 32);
+    return (t + ((n - t) >> d.s1)) >> d.s2;
+}
+int main() {
+    unsigned long long x = 88172645463325252ull;
+    const unsigned ds[] = {1, 2, 3, 7, 8, 9, 60, 240, 480, 2048, 4096, 129600, 259200, 8294400,
+                           33554432, 0x7fffffffu, 0x80000000u, 0x80000001u, 0xffffffffu};
+    int bad = 0;
+    for (int k = 0; k < 20000; k++) {
+        unsigned d;
+        if (k < 19) d = ds[k];
+        else { x ^= x << 13; x ^= x >> 7; x ^= x << 17; d = (unsigned)(x >> (x & 31)); if (!d) d = 1; }
+        const jx_udiv D = jx_udiv_make(d);
+        for (int i = 0; i < 200; i++) {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            unsigned n = (unsigned)x;
+            if (i == 0) n = 0; else if (i == 1) n = 0xffffffffu; else if (i == 2) n = d - 1; else if (i == 3) n = d;
+            if (dv(n, D) != n / d) bad++;
+        }
+    }
+    printf("%d\n", bad);
+    return bad != 0;
+}
+''')
+    exe = tmp_path / "udiv"
+    import subprocess
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I" + os.path.join(PKG, "csrc"), "-I" + os.path.join(REPO, "include"),
+                    str(src), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout
