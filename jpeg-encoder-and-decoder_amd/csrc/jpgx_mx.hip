@@ -96,6 +96,12 @@ __host__ __device__ constexpr unsigned mx_pos(unsigned c, unsigned jb)
     return c == 0 ? jb : (c == 1 ? 12u + jb : (jb < 4 ? 8u + jb : 16u + jb));
 }
 constexpr unsigned kStageBytes = 24 * kBS;
+/* k_mxs's lean stage (JX_MXS_LEAN): Y 0..7, Cb 8..15; the Cr column is computed after the Y and
+ * Cb stores and takes the set-0 slots of its lane (Cr 0..3 at 0..3, Cr 4..7 at 8..11) */
+__host__ __device__ constexpr unsigned mx_pos_lean(unsigned c, unsigned jb)
+{
+    return c == 0 ? jb : (c == 1 ? 8u + jb : (jb < 4 ? jb : 4u + jb));
+}
 
 constexpr int kSide = 8;                /* deferred exact tasks per flush (8-lane groups)    */
 constexpr int kSidePix = 6;             /* k_mx: deferred blocks' pixel slots per wave       */
@@ -432,7 +438,7 @@ __device__ __forceinline__ unsigned mx_col_block(unsigned k, unsigned sl)
 /* Inline exact pass of one step (a step with more tasks than the deferred queue holds, e.g.
  * FLAG_FORCE_EXACT): every flagged coefficient (bit 8 col + v of a lane's `bits`), eight at a
  * time, patching the stage. */
-template <class Lds>
+template <bool LEAN = false, class Lds>
 __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uint32_t bits,
                                                 const jx_mxtab &T)
 {
@@ -457,7 +463,8 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
         const unsigned jb = mx_col_block(k, sl);
         const int val = mx_exact_coef(mx_lds((void *)slot) + 24u * jb, 192u, ch, u, v, x, T);
         if (live && x == 7)
-            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + kBS * mx_pos(ch, jb) +
+            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) +
+                                                           kBS * (LEAN ? mx_pos_lean(ch, jb) : mx_pos(ch, jb)) +
                                                            2u * (unsigned)kMxScan[v][u]) = (int16_t)val;
         mx_wave_sync();
     }
@@ -661,6 +668,19 @@ __device__ __forceinline__ void mx_fence(const mx_f4 &r)
     asm volatile("" ::"s"(v) : "memory");
 }
 
+/* Keep the C inputs of chained products live (so that no VALU instruction or load reuses their
+ * registers) until the chain's results have been read (mx_fence).  Round 4: a VALU write into the
+ * C input of a chained product 3 wait states after its issue -- what hipcc's hazard recognizer
+ * pads for this form on gfx950 -- gave nondeterministic wrong C rows 12..15 (blocks 3 / 7 of a
+ * step; profiles/r04_mfma_valu_war.txt).  tools/mfma_war_check.py --valu-srcc checks the rule. */
+#ifndef JX_MX_KEEPC
+#define JX_MX_KEEPC 1
+#endif
+__device__ __forceinline__ void mx_keep(const mx_f4 (&x)[4])
+{
+    if (JX_MX_KEEPC) asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
+}
+
 /* Column pass of one column (R pairs), quantiser, stage writes at za[v] + OFF, band flags (rare
  * path: the exact per-coefficient test with the limits of table t0 + 1, after mx_fence(*fence)
  * when an MFMA may be in flight) into fl */
@@ -700,15 +720,17 @@ __device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, f
 template <unsigned OFF, bool LAZY = false, class TB>
 __device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t, float limc, const TB &tb,
                                              unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc,
-                                             const mx_f4 *fence = nullptr)
+                                             const mx_f4 *fence = nullptr, const mx_f4 (*keep)[4] = nullptr)
 {
     mx_f2 R[4];
     mx_combine(acc[0], acc[1], acc[2], acc[3], R);
     if (LAZY) {
         __builtin_amdgcn_sched_barrier(0);
         if (fence) mx_fence(*fence);              /* a later MFMA may still be in flight */
+        if (keep) mx_keep(*keep);                 /* every chain up to `fence` is done */
         mx_column_r<OFF>(R, mx_w(tb, t0, j), limc, tb, t0, j, za, fl, kc, nullptr);
     } else {
+        if (keep) mx_keep(*keep);                 /* the tiles are read: their chains are done */
         mx_column_r<OFF>(R, t, limc, tb, t0, j, za, fl, kc, fence);
     }
 }
@@ -993,9 +1015,13 @@ static_assert(kMxsC >= 1, "k_mxs: at least one step per wave");
 constexpr unsigned kMxsR = kMxsC < 3 ? kMxsC : 3;
 constexpr bool kMxsRing = kMxsC > 3;
 
+#ifndef JX_MXS_LEAN
+#define JX_MXS_LEAN 0                   /* 1: 16-block stage (mx_pos_lean), Y / Cb stored before the Cr column */
+#endif
+constexpr bool kMxsLean = JX_MXS_LEAN != 0;
 struct alignas(16) MxsLds {
     uint8_t ring[kMxsR][kSlot];         /* pixels, [y][24 jb + k]                       */
-    uint8_t stage[kStageBytes];         /* zig-zag stage (k_mx's layout, mx_pos)        */
+    uint8_t stage[(kMxsLean ? 16 : 24) * kBS];  /* zig-zag stage (mx_pos / mx_pos_lean)  */
     uint16_t task[8];                   /* inline exact batch                           */
 };
 static_assert(sizeof(MxsLds) % 16 == 0, "16-byte aligned LDS regions");
@@ -1205,7 +1231,8 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
     const uint32_t s2 = q < 3 ? kSelLo : kSelZero;
     const uint32_t so0 = lane * 16u, so1 = so0 + g.nb * 128u, so2 = so1 + g.nb * 128u;
     const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
-    const uint32_t rr = ro + ((lane >> 3) < 4 ? 8u : 16u) * kBS;
+    const uint32_t rr = ro + (kMxsLean ? ((lane >> 3) < 4 ? 0u : 4u) : ((lane >> 3) < 4 ? 8u : 16u)) * kBS;
+    const uint32_t rcb = (kMxsLean ? 8u : 12u) * kBS + ro;
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
     const jx_mxtab &T = g_mxtab[g.force ? 1 : 0][g.quality];
 
@@ -1221,7 +1248,8 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
      * global load: its wait would drain the pixel DMA too) */
     uint32_t za[8];
     {
-        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * mx_pos(j >> 3, gq);
+        const uint32_t base =
+            (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * (kMxsLean ? mx_pos_lean(j >> 3, gq) : mx_pos(j >> 3, gq));
         const mx_u2 sc = *(const mx_u2 *)&s_img.scan_t[u][0];
 #pragma unroll
         for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
@@ -1301,14 +1329,22 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         __builtin_amdgcn_sched_barrier(0);
         mx_column_t<0>(acc[0], w0, limc0, tb, 0, j, za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
-        acc[2][0] = mx_mma(A00, B[0][1], z);
-        acc[2][2] = mx_mma(A01, B[0][1], z);
-        acc[2][1] = mx_mma(A00, B[1][1], z);
-        acc[2][3] = mx_mma(A01, B[1][1], z);
-        acc[2][0] = mx_mma(A10, B[0][2], acc[2][0]);
-        acc[2][2] = mx_mma(A11, B[0][2], acc[2][2]);
-        acc[2][1] = mx_mma(A10, B[1][2], acc[2][1]);
-        acc[2][3] = mx_mma(A11, B[1][2], acc[2][3]);
+        const mx_f4 c0 = mx_mma(A00, B[0][1], z);
+        const mx_f4 c2 = mx_mma(A01, B[0][1], z);
+        const mx_f4 c1 = mx_mma(A00, B[1][1], z);
+        const mx_f4 c3 = mx_mma(A01, B[1][1], z);
+        acc[2][0] = mx_mma(A10, B[0][2], c0);
+        acc[2][2] = mx_mma(A11, B[0][2], c2);
+        acc[2][1] = mx_mma(A10, B[1][2], c1);
+        acc[2][3] = mx_mma(A11, B[1][2], c3);
+#ifndef JX_MX_KEEPA
+#define JX_MX_KEEPA 0                   /* 1: the A operands too */
+#endif
+        const auto keepc = [&]() __attribute__((always_inline)) {
+            const mx_f4 cc[4] = {c0, c1, c2, c3};
+            mx_keep(cc);
+            if (JX_MX_KEEPA) asm volatile("" ::"v"(A00), "v"(A01), "v"(A10), "v"(A11));
+        };
         if (kParts == 3) {
             acc[2][1] = mx_mma(A00, B[kParts - 1][1], acc[2][1]);
             acc[2][3] = mx_mma(A01, B[kParts - 1][1], acc[2][3]);
@@ -1319,26 +1355,77 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         mx_column_t<4 * kBS>(acc[1], w0, limc0, tb, 0, j, za, fl, 1, &acc[2][3]);
         __builtin_amdgcn_sched_barrier(0);
         const uint8_t *const ob = (const uint8_t *)S.dst;
+        /* the launch's last step: flags of its clamped copies are dropped (never stored) */
+        const auto clamp = [&](uint32_t &f) __attribute__((always_inline)) {
+            if (S.b + 8u > g.total) {
+                const unsigned nvalid = g.total - S.b;
+#pragma unroll
+                for (int kk = 0; kk < 3; kk++)
+                    if (mx_col_block((unsigned)kk, lane) >= nvalid) f &= ~(0xffu << (8 * kk));
+            }
+        };
+        const auto store = [&](int c) __attribute__((always_inline)) {    /* the general path's store c */
+            const unsigned l = mx_lane();
+            const unsigned bl = S.b + (l >> 3), b = bl < g.total ? bl : g.total - 1u;
+            const unsigned f = b / g.nb, bi = b - f * g.nb;
+            const unsigned pos = kMxsLean ? mx_pos_lean((unsigned)c, l >> 3) : mx_pos((unsigned)c, l >> 3);
+            const mx_u4 val = *(const mx_u4 *)(L.stage + kBS * pos + (l & 7u) * 16u);
+            if (bl < g.total)
+                __builtin_nontemporal_store(
+                    val, (mx_u4 *)(g.out + (long long)f * g.ofstride + ((long long)c * g.nb + bi) * 64 + (l & 7u) * 8));
+        };
+        if constexpr (kMxsLean) {
+            /* Y and Cb leave before the Cr column, which then takes their set-0 slots */
+            mx_fence(acc[2][3]);                       /* the Cr products are done (operand rule) */
+            keepc();
+            mx_wave_sync();
+            if (__builtin_expect(__ballot((fl & 0xffffu) != 0) != 0, 0)) {
+                uint32_t f2 = fl & 0xffffu;
+                clamp(f2);
+                mx_exact_inline<true>(L, sp, f2, T);
+            }
+            if (S.simple) {
+                const mx_u4 v0 = *(const mx_u4 *)(L.stage + ro);
+                const mx_u4 v1 = *(const mx_u4 *)(L.stage + rcb);
+                __builtin_nontemporal_store(v0, (mx_u4 *)(ob + so0));
+                __builtin_nontemporal_store(v1, (mx_u4 *)(ob + so1));
+            } else {
+                store(0);
+                store(1);
+            }
+            mx_wave_sync();
+            mx_column_t<0, true>(acc[2], w0, limc2, tb, 2, j, za, fl, 2);
+            mx_wave_sync();
+            if (__builtin_expect(__ballot((fl >> 16) != 0) != 0, 0)) {
+                uint32_t f2 = fl & 0xff0000u;
+                clamp(f2);
+                mx_exact_inline<true>(L, sp, f2, T);
+            }
+            if (S.simple) {
+                const mx_u4 v2 = *(const mx_u4 *)(L.stage + rr);
+                __builtin_nontemporal_store(v2, (mx_u4 *)(ob + so2));
+            } else {
+                store(2);
+            }
+            mx_wave_sync();
+            return;
+        }
         const bool early = S.simple && __ballot((fl & 0xffffu) != 0) == 0;
         if (early) {
             mx_fence(acc[2][3]);                       /* the Cr products are done (operand rule) */
+            keepc();
             mx_wave_sync();
             const mx_u4 v0 = *(const mx_u4 *)(L.stage + ro);
-            const mx_u4 v1 = *(const mx_u4 *)(L.stage + 12u * kBS + ro);
+            const mx_u4 v1 = *(const mx_u4 *)(L.stage + rcb);
             __builtin_nontemporal_store(v0, (mx_u4 *)(ob + so0));
             __builtin_nontemporal_store(v1, (mx_u4 *)(ob + so1));
         }
         __builtin_amdgcn_sched_barrier(0);
         mx_column_t<8 * kBS, true>(acc[2], w0, limc2, tb, 2, j, za, fl, 2);
+        keepc();
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
-            /* the launch's last step: flags of its clamped copies are dropped (never stored) */
-            if (S.b + 8u > g.total) {
-                const unsigned nvalid = g.total - S.b;
-#pragma unroll
-                for (int kk = 0; kk < 3; kk++)
-                    if (mx_col_block((unsigned)kk, lane) >= nvalid) fl &= ~(0xffu << (8 * kk));
-            }
+            clamp(fl);
             mx_exact_inline(L, sp, fl, T);
         }
 #endif
@@ -1348,23 +1435,14 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
             __builtin_nontemporal_store(v2, (mx_u4 *)(ob + so2));
         } else if (S.simple) {
             const mx_u4 v0 = *(const mx_u4 *)(L.stage + ro);
-            const mx_u4 v1 = *(const mx_u4 *)(L.stage + 12u * kBS + ro);
+            const mx_u4 v1 = *(const mx_u4 *)(L.stage + rcb);
             const mx_u4 v2 = *(const mx_u4 *)(L.stage + rr);
             __builtin_nontemporal_store(v0, (mx_u4 *)(ob + so0));
             __builtin_nontemporal_store(v1, (mx_u4 *)(ob + so1));
             __builtin_nontemporal_store(v2, (mx_u4 *)(ob + so2));
         } else {
-            const unsigned l = mx_lane();
-            const unsigned bl = S.b + (l >> 3), b = bl < g.total ? bl : g.total - 1u;
-            const unsigned f = b / g.nb, bi = b - f * g.nb;
 #pragma unroll
-            for (int c = 0; c < 3; c++) {
-                const mx_u4 val = *(const mx_u4 *)(L.stage + kBS * mx_pos((unsigned)c, l >> 3) + (l & 7u) * 16u);
-                if (bl < g.total)
-                    __builtin_nontemporal_store(
-                        val, (mx_u4 *)(g.out + (long long)f * g.ofstride +
-                                       ((long long)c * g.nb + bi) * 64 + (l & 7u) * 8));
-            }
+            for (int c = 0; c < 3; c++) store(c);
         }
         mx_wave_sync();
     };
@@ -2097,16 +2175,17 @@ __global__ __launch_bounds__(64 * kMxs422WPG, JX_MX422_WPE) void k_mxs422(const 
         const mx_f4 z = {};
         uint32_t fl = 0;
         mx_f4 acc[2][4];                               /* [Y, chroma][hl, ll, hh, lh] */
-        const auto mma2 = [&](mx_f4(&o)[4], const mx_h8 &Al0, const mx_h8 &Ah0, const mx_h8 &Al1,
+        mx_f4 mid[2][4];                               /* the chains' first products (mx_keep) */
+        const auto mma2 = [&](mx_f4(&o)[4], mx_f4(&m)[4], const mx_h8 &Al0, const mx_h8 &Ah0, const mx_h8 &Al1,
                               const mx_h8 &Ah1, int w0) __attribute__((always_inline)) {
-            o[0] = mx_mma(Al0, B[0][w0], z);
-            o[2] = mx_mma(Ah0, B[0][w0], z);
-            o[1] = mx_mma(Al0, B[1][w0], z);
-            o[3] = mx_mma(Ah0, B[1][w0], z);
-            o[0] = mx_mma(Al1, B[0][w0 + 1], o[0]);
-            o[2] = mx_mma(Ah1, B[0][w0 + 1], o[2]);
-            o[1] = mx_mma(Al1, B[1][w0 + 1], o[1]);
-            o[3] = mx_mma(Ah1, B[1][w0 + 1], o[3]);
+            m[0] = mx_mma(Al0, B[0][w0], z);
+            m[2] = mx_mma(Ah0, B[0][w0], z);
+            m[1] = mx_mma(Al0, B[1][w0], z);
+            m[3] = mx_mma(Ah0, B[1][w0], z);
+            o[0] = mx_mma(Al1, B[0][w0 + 1], m[0]);
+            o[2] = mx_mma(Ah1, B[0][w0 + 1], m[2]);
+            o[1] = mx_mma(Al1, B[1][w0 + 1], m[1]);
+            o[3] = mx_mma(Ah1, B[1][w0 + 1], m[3]);
             if (kParts == 3) {
                 o[1] = mx_mma(Al0, B[kParts - 1][w0], o[1]);
                 o[3] = mx_mma(Ah0, B[kParts - 1][w0], o[3]);
@@ -2138,14 +2217,19 @@ __global__ __launch_bounds__(64 * kMxs422WPG, JX_MX422_WPE) void k_mxs422(const 
             c10 = *(const mx_u2 *)p1;
             c11 = *(const mx_u2 *)(p1 + h1);
         }
+        /* every A operand is built before the first product, so no VALU write falls between a
+         * chain's products and the read of its results (the C inputs need no keeping, mx_keep) */
+        const mx_h8 Ay0 = mx_aop(y00, s0, s1, s2), Ay1 = mx_aop(y01, s0, s1, s2);
+        const mx_h8 Ay2 = mx_aop(y10, s0, s1, s2), Ay3 = mx_aop(y11, s0, s1, s2);
+        const mx_h8 Ac0 = mx_aop(c00, kSelLo, kSelHi, kSelLo), Ac1 = mx_aop(c01, kSelLo, kSelHi, kSelLo);
+        const mx_h8 Ac2 = mx_aop(c10, t0, t1, t2), Ac3 = mx_aop(c11, t0, t1, t2);
         __builtin_amdgcn_sched_barrier(0);
-        mma2(acc[0], mx_aop(y00, s0, s1, s2), mx_aop(y01, s0, s1, s2), mx_aop(y10, s0, s1, s2),
-             mx_aop(y11, s0, s1, s2), 0);
+        mma2(acc[0], mid[0], Ay0, Ay1, Ay2, Ay3, 0);
         __builtin_amdgcn_sched_barrier(0);
-        mma2(acc[1], mx_aop(c00, kSelLo, kSelHi, kSelLo), mx_aop(c01, kSelLo, kSelHi, kSelLo),
-             mx_aop(c10, t0, t1, t2), mx_aop(c11, t0, t1, t2), 2);
+        mma2(acc[1], mid[1], Ac0, Ac1, Ac2, Ac3, 2);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0, true>(acc[0], MxW{}, limc0, tb, 0, j, za, fl, 0, &acc[1][3]);
+        /* the Y column fences on the chroma products: after it, every chain of the step is done */
+        mx_column_t<0, true>(acc[0], MxW{}, limc0, tb, 0, j, za, fl, 0, &acc[1][3], &mid[1]);
         __builtin_amdgcn_sched_barrier(0);
         mx_column_t<kSt422C, true>(acc[1], MxW{}, limc2, tb, 2, j, za, fl, 1);
         mx_wave_sync();
@@ -2995,7 +3079,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
         mx_wave_sync();
         const mx_f4 z = {};
         uint32_t fl = 0;
-        mx_f4 accY[4], accC[2];
+        mx_f4 accY[4], accC[2], midY[4], midC[4];     /* mid: the chains' earlier products (mx_keep) */
         const mx_u2 y00 = *(const mx_u2 *)(sp + aoff);
         const mx_u2 y01 = *(const mx_u2 *)(sp + aoff + 384u);
         const mx_u2 y10 = *(const mx_u2 *)(sp + aoff + 768u);
@@ -3020,14 +3104,14 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
         {
             const mx_h8 Al0 = mx_aop(y00, s0, s1, s2), Ah0 = mx_aop(y01, s0, s1, s2);
             const mx_h8 Al1 = mx_aop(y10, s0, s1, s2), Ah1 = mx_aop(y11, s0, s1, s2);
-            accY[0] = mx_mma(Al0, B[0][0], z);
-            accY[2] = mx_mma(Ah0, B[0][0], z);
-            accY[1] = mx_mma(Al0, B[1][0], z);
-            accY[3] = mx_mma(Ah0, B[1][0], z);
-            accY[0] = mx_mma(Al1, B[0][1], accY[0]);
-            accY[2] = mx_mma(Ah1, B[0][1], accY[2]);
-            accY[1] = mx_mma(Al1, B[1][1], accY[1]);
-            accY[3] = mx_mma(Ah1, B[1][1], accY[3]);
+            midY[0] = mx_mma(Al0, B[0][0], z);
+            midY[2] = mx_mma(Ah0, B[0][0], z);
+            midY[1] = mx_mma(Al0, B[1][0], z);
+            midY[3] = mx_mma(Ah0, B[1][0], z);
+            accY[0] = mx_mma(Al1, B[0][1], midY[0]);
+            accY[2] = mx_mma(Ah1, B[0][1], midY[2]);
+            accY[1] = mx_mma(Al1, B[1][1], midY[1]);
+            accY[3] = mx_mma(Ah1, B[1][1], midY[3]);
             if (kParts == 3) {
                 accY[1] = mx_mma(Al0, B[kParts - 1][0], accY[1]);
                 accY[3] = mx_mma(Ah0, B[kParts - 1][0], accY[3]);
@@ -3039,12 +3123,12 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
         {
             const mx_h8 C0 = mx_aop(c0, kSelLo, kSelHi, kSelLo), C1 = mx_aop(c1, kSelLo, kSelHi, kSelLo);
             const mx_h8 C2 = mx_aop(c2, kSelLo, kSelHi, kSelLo);
-            accC[0] = mx_mma(C0, B[0][2], z);
-            accC[1] = mx_mma(C0, B[1][2], z);
-            accC[0] = mx_mma(C1, B[0][3], accC[0]);
-            accC[1] = mx_mma(C1, B[1][3], accC[1]);
-            accC[0] = mx_mma(C2, B[0][4], accC[0]);
-            accC[1] = mx_mma(C2, B[1][4], accC[1]);
+            midC[0] = mx_mma(C0, B[0][2], z);
+            midC[1] = mx_mma(C0, B[1][2], z);
+            midC[2] = mx_mma(C1, B[0][3], midC[0]);
+            midC[3] = mx_mma(C1, B[1][3], midC[1]);
+            accC[0] = mx_mma(C2, B[0][4], midC[2]);
+            accC[1] = mx_mma(C2, B[1][4], midC[3]);
             if (kParts == 3) {
                 accC[1] = mx_mma(C0, B[kParts - 1][2], accC[1]);
                 accC[1] = mx_mma(C1, B[kParts - 1][3], accC[1]);
@@ -3052,11 +3136,12 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0, true>(accY, MxW{}, limc0, tb, 0, j, za, fl, 0, &accC[1]);
+        mx_column_t<0, true>(accY, MxW{}, limc0, tb, 0, j, za, fl, 0, &accC[1], &midY);
         __builtin_amdgcn_sched_barrier(0);
         const float sl = JX_MX_LOEXP == 0 ? 1.0f : 0x1p-12f;
         const mx_f4 s12 = {sl, sl, sl, sl};
         const mx_f4 rc4 = JX_MX_LOEXP == 0 ? accC[1] + accC[0] : __builtin_elementwise_fma(accC[1], s12, accC[0]);
+        mx_keep(midC);
         __builtin_amdgcn_sched_barrier(0);
         if (second) {
             const mx_f4 rA0 = L.rA[lane];

@@ -24,7 +24,13 @@ def test_mfma_operand_rule(tmp_path):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
     assert r.stdout.count(" 0 load(s) into live MFMA operands") == len(names), r.stdout
-    # the launched (short-wave) kernels: no scratch, no VGPR / SGPR spills
+    # the launched (short-wave) kernels: no VALU write into the C input of a product in flight either
+    short = ["k_mxs", "k_mxs422", "k_mxs420"]
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), "--valu-srcc", str(asm)]
+                       + short, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert r.stdout.count(" 0 load(s) or VALU write(s) of C inputs into live MFMA operands") == len(short), r.stdout
+    # and no scratch, no VGPR / SGPR spills
     text = asm.read_text()
     for n in ("k_mxs", "k_mxs422", "k_mxs420"):
         m = re.search(r"\.name:\s+_ZN12_GLOBAL__N_1\d+%sE13jx_xform_args\s*\n(.*?)\.vgpr_spill_count:\s+(\d+)" % n,
@@ -99,3 +105,27 @@ def test_mfma_operand_rule_covers_agprs_and_returning_atomics(tmp_path):
         "\tglobal_atomic_add_f32 a8, v[20:21], v22, off sc0",
         "\tv_accvgpr_read_b32 v30, a8"])
     assert r.returncode == 1 and "1 load(s)" in r.stdout, r.stdout
+
+
+def test_mfma_valu_srcc_rule(tmp_path):
+    """--valu-srcc: a VALU write into the C input of a chained product before its result (or a
+    later product's) is read is a violation (the round-4 rows-12..15 fault,
+    profiles/r04_mfma_valu_war.txt); the same write after the read is not; without the flag the
+    load-only rule ignores it"""
+    lines = [
+        "\tv_mfma_f32_16x16x32_f16 v[8:11], v[0:3], v[4:7], 0",
+        "\tv_mfma_f32_16x16x32_f16 v[12:15], v[0:3], v[4:7], v[8:11]",
+        "\ts_nop 0",
+        "\tv_pk_add_f32 v[8:9], v[20:21], v[22:23]",
+        "\tv_add_f32_e32 v30, v12, v13"]
+    s = tmp_path / "fake.s"
+    s.write_text("\n".join(["_ZN12_GLOBAL__N_14k_mxE13jx_xform_args:"] + lines + [".Lfunc_end0:", ""]))
+    tool = os.path.join(REPO, "tools", "mfma_war_check.py")
+    bad = subprocess.run([sys.executable, tool, "--valu-srcc", str(s), "k_mx"], capture_output=True, text=True)
+    assert bad.returncode == 1 and " 1 load(s) or VALU write(s)" in bad.stdout, bad.stdout
+    plain = subprocess.run([sys.executable, tool, str(s), "k_mx"], capture_output=True, text=True)
+    assert plain.returncode == 0, plain.stdout
+    lines[2:4] = ["\tv_add_f32_e32 v30, v12, v13", "\tv_pk_add_f32 v[8:9], v[20:21], v[22:23]"]
+    s.write_text("\n".join(["_ZN12_GLOBAL__N_14k_mxE13jx_xform_args:"] + lines + [".Lfunc_end0:", ""]))
+    ok = subprocess.run([sys.executable, tool, "--valu-srcc", str(s), "k_mx"], capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stdout

@@ -14,8 +14,11 @@ result or the result of a later MFMA (which waits for it; a wave's MFMAs complet
 so then this one has read every operand), no instruction that writes VGPRs
 from memory -- LDS reads, permutes / swizzles, LDS or global atomics with return, global /
 buffer / flat / scratch / image loads -- may write any of its SrcA / SrcB / SrcC registers (VGPRs
-or AGPRs).  A path is followed for at most LIMIT instructions.
-Usage: python tools/mfma_war_check.py FILE.s [kernel ...]   (exit status 1 on a violation)
+or AGPRs).  With --valu-srcc, no VALU instruction may write its SrcC registers either (round 4:
+a VALU write into the C input of a chained product 3 wait states after its issue -- the count
+hipcc's hazard recognizer pads for this gfx950 form -- gave nondeterministic wrong C rows 12..15;
+profiles/r04_mfma_valu_war.txt).  A path is followed for at most LIMIT instructions.
+Usage: python tools/mfma_war_check.py [--valu-srcc] FILE.s [kernel ...]   (exit 1 on a violation)
 """
 import re
 import sys
@@ -85,13 +88,14 @@ def successors(ins, labels, j):
     return out
 
 
-def check(ins, labels):
+def check(ins, labels, valu_srcc=False):
     bad = []
     for i, t in enumerate(ins):
         op, ops = operands(t)
         if not op.startswith("v_mfma"):
             continue
         src = regs(",".join(ops[1:]))
+        srcc = regs(ops[3]) if len(ops) > 3 else set()
         # paths: (next index, registers whose read implies completion, steps taken)
         stack = [(k, frozenset(regs(ops[0])), 1) for k in successors(ins, labels, i)]
         seen = set()
@@ -116,6 +120,10 @@ def check(ins, labels):
                                  "scratch_store")) and uops:
                 reads = regs(",".join(uops[1:])) if uop.startswith("v_") else regs(",".join(uops))
                 done = bool(reads & dst)          # the result is read: the MFMA has completed
+                if not done and valu_srcc and uop.startswith("v_") and not uop.startswith("v_readfirstlane"):
+                    hit = regs(uops[0]) & srcc
+                    if hit and j not in found:
+                        found[j] = (i, j, t, u, sorted(hit))
             if not done:
                 stack.extend((k, dst, n + 1) for k in successors(ins, labels, j))
         bad.extend(found[j] for j in sorted(found))
@@ -123,8 +131,11 @@ def check(ins, labels):
 
 
 def main():
-    path = sys.argv[1]
-    names = sys.argv[2:] or ["k_mx", "k_mx422", "k_mx420"]
+    args = sys.argv[1:]
+    valu_srcc = "--valu-srcc" in args
+    args = [a for a in args if a != "--valu-srcc"]
+    path = args[0]
+    names = args[1:] or ["k_mx", "k_mx422", "k_mx420"]
     text = open(path).read()
     rc = 0
     for n in names:
@@ -133,8 +144,9 @@ def main():
             print(f"{n}: not found")
             rc = 1
             continue
-        bad = check(ins, labels)
-        print(f"{n}: {sum(1 for x in ins if x.startswith('v_mfma'))} MFMAs, {len(bad)} load(s) into live MFMA operands")
+        bad = check(ins, labels, valu_srcc)
+        what = "load(s) or VALU write(s) of C inputs" if valu_srcc else "load(s)"
+        print(f"{n}: {sum(1 for x in ins if x.startswith('v_mfma'))} MFMAs, {len(bad)} {what} into live MFMA operands")
         for i, j, t, u, hit in bad[:12]:
             print(f"   at {j} after the MFMA at {i}: {t[:64]}\n         {u[:64]}  -> {hit}")
         rc |= 1 if bad else 0
