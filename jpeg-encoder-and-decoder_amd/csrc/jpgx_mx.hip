@@ -1926,16 +1926,17 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
         const mx_f4 z = {};
         uint32_t fl = 0;
         mx_f4 acc[2][4];                               /* [Y, chroma][hl, ll, hh, lh] */
-        const auto mma2 = [&](mx_f4(&o)[4], const mx_h8 &Al0, const mx_h8 &Ah0, const mx_h8 &Al1,
+        mx_f4 mid[2][4];                               /* the chains' first products (mx_keep) */
+        const auto mma2 = [&](mx_f4(&o)[4], mx_f4(&m)[4], const mx_h8 &Al0, const mx_h8 &Ah0, const mx_h8 &Al1,
                               const mx_h8 &Ah1, int w0) {
-            o[0] = mx_mma(Al0, B[0][w0], z);
-            o[2] = mx_mma(Ah0, B[0][w0], z);
-            o[1] = mx_mma(Al0, B[1][w0], z);
-            o[3] = mx_mma(Ah0, B[1][w0], z);
-            o[0] = mx_mma(Al1, B[0][w0 + 1], o[0]);
-            o[2] = mx_mma(Ah1, B[0][w0 + 1], o[2]);
-            o[1] = mx_mma(Al1, B[1][w0 + 1], o[1]);
-            o[3] = mx_mma(Ah1, B[1][w0 + 1], o[3]);
+            m[0] = mx_mma(Al0, B[0][w0], z);
+            m[2] = mx_mma(Ah0, B[0][w0], z);
+            m[1] = mx_mma(Al0, B[1][w0], z);
+            m[3] = mx_mma(Ah0, B[1][w0], z);
+            o[0] = mx_mma(Al1, B[0][w0 + 1], m[0]);
+            o[2] = mx_mma(Ah1, B[0][w0 + 1], m[2]);
+            o[1] = mx_mma(Al1, B[1][w0 + 1], m[1]);
+            o[3] = mx_mma(Ah1, B[1][w0 + 1], m[3]);
             if (kParts == 3) {
                 o[1] = mx_mma(Al0, B[kParts - 1][w0], o[1]);
                 o[3] = mx_mma(Ah0, B[kParts - 1][w0], o[3]);
@@ -1972,14 +1973,17 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
                 c11 = *(const mx_u2 *)(p1 + h1);
             }
         }
+        /* all A operands before the first product (k_mxs422's order, mx_keep) */
+        const mx_h8 Ay0 = mx_aop(y00, s0, s1, s2), Ay1 = mx_aop(y01, s0, s1, s2);
+        const mx_h8 Ay2 = mx_aop(y10, s0, s1, s2), Ay3 = mx_aop(y11, s0, s1, s2);
+        const mx_h8 Ac0 = mx_aop(c00, kSelLo, kSelHi, kSelLo), Ac1 = mx_aop(c01, kSelLo, kSelHi, kSelLo);
+        const mx_h8 Ac2 = mx_aop(c10, t0, t1, t2), Ac3 = mx_aop(c11, t0, t1, t2);
         __builtin_amdgcn_sched_barrier(0);
-        mma2(acc[0], mx_aop(y00, s0, s1, s2), mx_aop(y01, s0, s1, s2), mx_aop(y10, s0, s1, s2),
-             mx_aop(y11, s0, s1, s2), 0);
+        mma2(acc[0], mid[0], Ay0, Ay1, Ay2, Ay3, 0);
         __builtin_amdgcn_sched_barrier(0);
-        mma2(acc[1], mx_aop(c00, kSelLo, kSelHi, kSelLo), mx_aop(c01, kSelLo, kSelHi, kSelLo),
-             mx_aop(c10, t0, t1, t2), mx_aop(c11, t0, t1, t2), 2);
+        mma2(acc[1], mid[1], Ac0, Ac1, Ac2, Ac3, 2);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0, true>(acc[0], MxW{}, limc0, s_tab, 0, j, za, fl, 0, &acc[1][3]);
+        mx_column_t<0, true>(acc[0], MxW{}, limc0, s_tab, 0, j, za, fl, 0, &acc[1][3], &mid[1]);
         __builtin_amdgcn_sched_barrier(0);
         mx_column_t<kSt422C, true>(acc[1], MxW{}, limc2, s_tab, 2, j, za, fl, 1);
         mx_wave_sync();
