@@ -15,9 +15,11 @@ for v in lx12 lx12kc; do
   JPGX_LIB=$PWD/$V/libjpgx_$v.so timeout -k 10 240 python tools/diag_golden.py 4 > gpurun_out/r4d/c_$v.txt 2>&1 || exit $?
   echo "== $v"; grep "rep" gpurun_out/r4d/c_$v.txt | cut -c1-60
 done
-KB_SUB=0 timeout -k 10 300 python tools/kbench.py 2 nokc w1c3 legacy > "$OUT/kb444.txt" 2>&1 || exit $?
+KB_SUB=0 timeout -k 10 400 python tools/kbench.py 2 nokc w1c3 legacy l2w5 l3 c2 > "$OUT/kb444.txt" 2>&1 || exit $?
 KB_SUB=1 timeout -k 10 300 python tools/kbench.py 2 l422 s422w4 > "$OUT/kb422.txt" 2>&1 || exit $?
 KB_SUB=2 timeout -k 10 300 python tools/kbench.py 2 l420 s420w4 > "$OUT/kb420.txt" 2>&1 || exit $?
 cat "$OUT/kb444.txt" "$OUT/kb422.txt" "$OUT/kb420.txt"
-timeout -k 10 300 ./tools/membench3 r4c > "$OUT/skel_r4c.txt" 2>&1 || exit $?
-cut -c1-150 "$OUT/skel_r4c.txt"
+if [ "${SKEL:-0}" = "1" ]; then
+  timeout -k 10 300 ./tools/membench3 r4c > "$OUT/skel_r4c.txt" 2>&1 || exit $?
+  cut -c1-150 "$OUT/skel_r4c.txt"
+fi
