@@ -676,6 +676,17 @@ __device__ __forceinline__ void mx_fence(const mx_f4 &r)
 #ifndef JX_MX_KEEPC
 #define JX_MX_KEEPC 1
 #endif
+/* diagnostics (JX_MX_GAP = N): N + 1 wait states after each group of products, before the VALU
+ * work that follows it */
+#ifndef JX_MX_GAP
+#define JX_MX_GAP -1
+#endif
+__device__ __forceinline__ void mx_gap()
+{
+#if JX_MX_GAP >= 0
+    asm volatile("s_nop %0" ::"n"(JX_MX_GAP));
+#endif
+}
 __device__ __forceinline__ void mx_keep(const mx_f4 (&x)[4])
 {
     if (JX_MX_KEEPC) asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
@@ -1326,6 +1337,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         mma_set(acc[0], A00, A01);
         __builtin_amdgcn_sched_barrier(0);
         mma_set(acc[1], A10, A11);
+        mx_gap();
         __builtin_amdgcn_sched_barrier(0);
         mx_column_t<0>(acc[0], w0, limc0, tb, 0, j, za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
@@ -1337,6 +1349,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         acc[2][2] = mx_mma(A11, B[0][2], c2);
         acc[2][1] = mx_mma(A10, B[1][2], c1);
         acc[2][3] = mx_mma(A11, B[1][2], c3);
+        mx_gap();
 #ifndef JX_MX_KEEPA
 #define JX_MX_KEEPA 0                   /* 1: the A operands too */
 #endif
@@ -2231,6 +2244,7 @@ __global__ __launch_bounds__(64 * kMxs422WPG, JX_MX422_WPE) void k_mxs422(const 
         mma2(acc[0], mid[0], Ay0, Ay1, Ay2, Ay3, 0);
         __builtin_amdgcn_sched_barrier(0);
         mma2(acc[1], mid[1], Ac0, Ac1, Ac2, Ac3, 2);
+        mx_gap();
         __builtin_amdgcn_sched_barrier(0);
         /* the Y column fences on the chroma products: after it, every chain of the step is done */
         mx_column_t<0, true>(acc[0], MxW{}, limc0, tb, 0, j, za, fl, 0, &acc[1][3], &mid[1]);
@@ -3133,6 +3147,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
             midC[3] = mx_mma(C1, B[1][3], midC[1]);
             accC[0] = mx_mma(C2, B[0][4], midC[2]);
             accC[1] = mx_mma(C2, B[1][4], midC[3]);
+            mx_gap();
             if (kParts == 3) {
                 accC[1] = mx_mma(C0, B[kParts - 1][2], accC[1]);
                 accC[1] = mx_mma(C1, B[kParts - 1][3], accC[1]);
@@ -3573,7 +3588,7 @@ extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)
                            (hipStream_t)stream, *xa);
         return mx_rc(hipGetLastError());
     }
-    const size_t w = JX_MX_NP ? (nsteps + JX_MX_NP - 1) / JX_MX_NP
+    const size_t w = JX_MX_NP ? (nsteps + JX_MX_NP - 1) / (JX_MX_NP ? JX_MX_NP : 1)
                               : std::min<size_t>(nsteps, (size_t)std::max(waves, 4));
     const unsigned grid = (unsigned)((w + 3) / 4);
     hipLaunchKernelGGL(k_mx, dim3(grid), dim3(256), JX_MX_DYNLDS, (hipStream_t)stream, *xa);
