@@ -681,6 +681,14 @@ __device__ __forceinline__ void mx_fence(const mx_f4 &r)
 #ifndef JX_MX_GAP
 #define JX_MX_GAP -1
 #endif
+/* diagnostics (JX_MX_DMABAR = 1): an s_barrier after a one-wave workgroup's step wait */
+#ifndef JX_MX_DMABAR
+#define JX_MX_DMABAR 0
+#endif
+__device__ __forceinline__ void mx_dmabar()
+{
+    if (JX_MX_DMABAR) __builtin_amdgcn_s_barrier();
+}
 __device__ __forceinline__ void mx_gap()
 {
 #if JX_MX_GAP >= 0
@@ -2288,6 +2296,7 @@ __global__ __launch_bounds__(64 * kMxs422WPG, JX_MX422_WPE) void k_mxs422(const 
         constexpr unsigned k = decltype(kc)::value;
         if (cmp.b >= g.total) return;
         mx_wait_vm<2 * (kMxs422C - 1 - k) + 2 * k>();
+        if (kMxs422WPG == 1) mx_dmabar();
         body(cmp, L.ring[k]);
         mxs_next(cmp, g);
     };
@@ -3091,6 +3100,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
             mx_wait_vm<2>();                            /* younger: step 1's DMA */
         else
             mx_wait_vm<1>();                            /* younger: step 0's Y store */
+        if (kMxs420WPG == 1) mx_dmabar();
         uint8_t *const sp = L.ring[k];
         if (!simple) mx420_issue_general(g, h, ms, sp);     /* register path; waits vmcnt(0) */
         const uint32_t qmask = simple ? 0u : mx420_true_rows(L, g, h, ms);
