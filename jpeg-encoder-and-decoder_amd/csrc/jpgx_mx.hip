@@ -699,6 +699,23 @@ __device__ __forceinline__ void mx_keep(const mx_f4 (&x)[4])
 {
     if (JX_MX_KEEPC) asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
 }
+/* the A / B operands of the products too (JX_MX_KEEPA): a product queued behind a chained one
+ * reads its operands late, pass by pass */
+#ifndef JX_MX_KEEPA
+#define JX_MX_KEEPA 1
+#endif
+template <class T>
+__device__ __forceinline__ int mx_keep1(const T &x)
+{
+    if (JX_MX_KEEPA) asm volatile("" ::"v"(x));
+    return 0;
+}
+template <class... T>
+__device__ __forceinline__ void mx_keep_ops(const T &...x)
+{
+    const int k[] = {mx_keep1(x)...};
+    (void)k;
+}
 
 /* Column pass of one column (R pairs), quantiser, stage writes at za[v] + OFF, band flags (rare
  * path: the exact per-coefficient test with the limits of table t0 + 1, after mx_fence(*fence)
@@ -736,20 +753,23 @@ __device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, f
 /* the same from the hi / lo accumulator tiles of rows 0..3 and 4..7; LAZY: the column's scales
  * are read here, after the tiles have been read (and after mx_fence(*fence) when a later MFMA may
  * still be in flight) -- no load meets an MFMA operand */
-template <unsigned OFF, bool LAZY = false, class TB>
+struct MxNoKeep {
+    __device__ void operator()() const {}
+};
+template <unsigned OFF, bool LAZY = false, class TB, class KF = MxNoKeep>
 __device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t, float limc, const TB &tb,
                                              unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc,
-                                             const mx_f4 *fence = nullptr, const mx_f4 (*keep)[4] = nullptr)
+                                             const mx_f4 *fence = nullptr, const KF &keep = KF{})
 {
     mx_f2 R[4];
     mx_combine(acc[0], acc[1], acc[2], acc[3], R);
     if (LAZY) {
         __builtin_amdgcn_sched_barrier(0);
         if (fence) mx_fence(*fence);              /* a later MFMA may still be in flight */
-        if (keep) mx_keep(*keep);                 /* every chain up to `fence` is done */
+        keep();                                   /* every product up to `fence` is done */
         mx_column_r<OFF>(R, mx_w(tb, t0, j), limc, tb, t0, j, za, fl, kc, nullptr);
     } else {
-        if (keep) mx_keep(*keep);                 /* the tiles are read: their chains are done */
+        keep();                                   /* the tiles are read: their chains are done */
         mx_column_r<OFF>(R, t, limc, tb, t0, j, za, fl, kc, fence);
     }
 }
@@ -1358,13 +1378,10 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         acc[2][1] = mx_mma(A10, B[1][2], c1);
         acc[2][3] = mx_mma(A11, B[1][2], c3);
         mx_gap();
-#ifndef JX_MX_KEEPA
-#define JX_MX_KEEPA 0                   /* 1: the A operands too */
-#endif
         const auto keepc = [&]() __attribute__((always_inline)) {
             const mx_f4 cc[4] = {c0, c1, c2, c3};
             mx_keep(cc);
-            if (JX_MX_KEEPA) asm volatile("" ::"v"(A00), "v"(A01), "v"(A10), "v"(A11));
+            mx_keep_ops(A00, A01, A10, A11, B[0][1], B[1][1], B[0][2], B[1][2]);
         };
         if (kParts == 3) {
             acc[2][1] = mx_mma(A00, B[kParts - 1][1], acc[2][1]);
@@ -2004,7 +2021,8 @@ __global__ __launch_bounds__(256, JX_MX422_WPE) void k_mx422(const jx_xform_args
         __builtin_amdgcn_sched_barrier(0);
         mma2(acc[1], mid[1], Ac0, Ac1, Ac2, Ac3, 2);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0, true>(acc[0], MxW{}, limc0, s_tab, 0, j, za, fl, 0, &acc[1][3], &mid[1]);
+        mx_column_t<0, true>(acc[0], MxW{}, limc0, s_tab, 0, j, za, fl, 0, &acc[1][3],
+                             [&]() __attribute__((always_inline)) { mx_keep(mid[1]); });
         __builtin_amdgcn_sched_barrier(0);
         mx_column_t<kSt422C, true>(acc[1], MxW{}, limc2, s_tab, 2, j, za, fl, 1);
         mx_wave_sync();
@@ -2255,7 +2273,11 @@ __global__ __launch_bounds__(64 * kMxs422WPG, JX_MX422_WPE) void k_mxs422(const 
         mx_gap();
         __builtin_amdgcn_sched_barrier(0);
         /* the Y column fences on the chroma products: after it, every chain of the step is done */
-        mx_column_t<0, true>(acc[0], MxW{}, limc0, tb, 0, j, za, fl, 0, &acc[1][3], &mid[1]);
+        const auto keep422 = [&]() __attribute__((always_inline)) {
+            mx_keep(mid[1]);
+            mx_keep_ops(Ay2, Ay3, Ac2, Ac3, B[0][1], B[1][1], B[0][3], B[1][3]);
+        };
+        mx_column_t<0, true>(acc[0], MxW{}, limc0, tb, 0, j, za, fl, 0, &acc[1][3], keep422);
         __builtin_amdgcn_sched_barrier(0);
         mx_column_t<kSt422C, true>(acc[1], MxW{}, limc2, tb, 2, j, za, fl, 1);
         mx_wave_sync();
@@ -3129,9 +3151,12 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
             c2 = *(const mx_u2 *)p2;
         }
         __builtin_amdgcn_sched_barrier(0);
+        /* every A operand before the first product; all operands stay live until the products are
+         * done (mx_keep_ops after the Y column's fence) */
+        const mx_h8 Al0 = mx_aop(y00, s0, s1, s2), Ah0 = mx_aop(y01, s0, s1, s2);
+        const mx_h8 Al1 = mx_aop(y10, s0, s1, s2), Ah1 = mx_aop(y11, s0, s1, s2);
+        __builtin_amdgcn_sched_barrier(0);
         {
-            const mx_h8 Al0 = mx_aop(y00, s0, s1, s2), Ah0 = mx_aop(y01, s0, s1, s2);
-            const mx_h8 Al1 = mx_aop(y10, s0, s1, s2), Ah1 = mx_aop(y11, s0, s1, s2);
             midY[0] = mx_mma(Al0, B[0][0], z);
             midY[2] = mx_mma(Ah0, B[0][0], z);
             midY[1] = mx_mma(Al0, B[1][0], z);
@@ -3148,9 +3173,16 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
             }
         }
         __builtin_amdgcn_sched_barrier(0);
+        /* the Y products are done before anything writes a register again: a chained product may
+         * wait in the matrix pipe and read its operands late (profiles/r04_mfma_valu_war.txt) */
+        mx_fence(accY[3]);
+        mx_keep(midY);
+        mx_keep_ops(Al1, Ah1);
+        __builtin_amdgcn_sched_barrier(0);
+        const mx_h8 C0 = mx_aop(c0, kSelLo, kSelHi, kSelLo), C1 = mx_aop(c1, kSelLo, kSelHi, kSelLo);
+        const mx_h8 C2 = mx_aop(c2, kSelLo, kSelHi, kSelLo);
+        __builtin_amdgcn_sched_barrier(0);
         {
-            const mx_h8 C0 = mx_aop(c0, kSelLo, kSelHi, kSelLo), C1 = mx_aop(c1, kSelLo, kSelHi, kSelLo);
-            const mx_h8 C2 = mx_aop(c2, kSelLo, kSelHi, kSelLo);
             midC[0] = mx_mma(C0, B[0][2], z);
             midC[1] = mx_mma(C0, B[1][2], z);
             midC[2] = mx_mma(C1, B[0][3], midC[0]);
@@ -3165,12 +3197,16 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<0, true>(accY, MxW{}, limc0, tb, 0, j, za, fl, 0, &accC[1], &midY);
+        /* the same for the chroma products */
+        mx_fence(accC[1]);
+        mx_keep(midC);
+        mx_keep_ops(C1, C2);
+        __builtin_amdgcn_sched_barrier(0);
+        mx_column_t<0, true>(accY, MxW{}, limc0, tb, 0, j, za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
         const float sl = JX_MX_LOEXP == 0 ? 1.0f : 0x1p-12f;
         const mx_f4 s12 = {sl, sl, sl, sl};
         const mx_f4 rc4 = JX_MX_LOEXP == 0 ? accC[1] + accC[0] : __builtin_elementwise_fma(accC[1], s12, accC[0]);
-        mx_keep(midC);
         __builtin_amdgcn_sched_barrier(0);
         if (second) {
             const mx_f4 rA0 = L.rA[lane];

@@ -18,7 +18,11 @@ or AGPRs).  With --valu-srcc, no VALU instruction may write its SrcC registers e
 a VALU write into the C input of a chained product 3 wait states after its issue -- the count
 hipcc's hazard recognizer pads for this gfx950 form -- gave nondeterministic wrong C rows 12..15;
 profiles/r04_mfma_valu_war.txt).  A path is followed for at most LIMIT instructions.
-Usage: python tools/mfma_war_check.py [--valu-srcc] FILE.s [kernel ...]   (exit 1 on a violation)
+With --valu-all, for a product that may start late -- a chained one (C input from a register: it
+waits for its producer in the matrix pipe) or one issued behind it in the same burst -- no VALU
+instruction may write ANY of its operands (A, B or C) either: such a product reads them late, after
+hipcc's hazard padding, which counts from issue (profiles/r04_mfma_valu_war.txt).
+Usage: python tools/mfma_war_check.py [--valu-srcc | --valu-all] FILE.s [kernel ...]   (exit 1 on a violation)
 """
 import re
 import sys
@@ -88,7 +92,34 @@ def successors(ins, labels, j):
     return out
 
 
-def check(ins, labels, valu_srcc=False):
+def delayed(ins, i):
+    """MFMA i may start late: it takes its C input from a register (a chained product, which waits
+    for its producer in the matrix pipe), or follows one in the same burst of products (no VALU read
+    of a product result in between; a wave's products execute in order)"""
+    def chained(t):
+        _, o = operands(t)
+        return len(o) > 3 and bool(regs(o[3]))
+    if chained(ins[i]):
+        return True
+    for j in range(i - 1, max(i - 64, -1), -1):
+        t = ins[j]
+        op, o = operands(t)
+        if op.startswith("v_mfma"):
+            if chained(t):
+                return True
+            continue
+        if t.startswith(".LBB") or op.startswith(("s_cbranch", "s_branch", "s_endpgm")):
+            return False
+        if op.startswith("v_") and o:
+            # a VALU read of an earlier product's result ends the burst
+            for k in range(j - 1, max(j - 64, -1), -1):
+                pk, ok = operands(ins[k])
+                if pk.startswith("v_mfma") and regs(ok[0]) & regs(",".join(o[1:])):
+                    return False
+    return False
+
+
+def check(ins, labels, valu_srcc=False, valu_all=False):
     bad = []
     for i, t in enumerate(ins):
         op, ops = operands(t)
@@ -96,6 +127,8 @@ def check(ins, labels, valu_srcc=False):
             continue
         src = regs(",".join(ops[1:]))
         srcc = regs(ops[3]) if len(ops) > 3 else set()
+        if valu_all and delayed(ins, i):
+            srcc = src                     # every operand of a product that may start late
         # paths: (next index, registers whose read implies completion, steps taken)
         stack = [(k, frozenset(regs(ops[0])), 1) for k in successors(ins, labels, i)]
         seen = set()
@@ -132,8 +165,9 @@ def check(ins, labels, valu_srcc=False):
 
 def main():
     args = sys.argv[1:]
-    valu_srcc = "--valu-srcc" in args
-    args = [a for a in args if a != "--valu-srcc"]
+    valu_all = "--valu-all" in args
+    valu_srcc = "--valu-srcc" in args or valu_all
+    args = [a for a in args if a not in ("--valu-srcc", "--valu-all")]
     path = args[0]
     names = args[1:] or ["k_mx", "k_mx422", "k_mx420"]
     text = open(path).read()
@@ -144,8 +178,9 @@ def main():
             print(f"{n}: not found")
             rc = 1
             continue
-        bad = check(ins, labels, valu_srcc)
-        what = "load(s) or VALU write(s) of C inputs" if valu_srcc else "load(s)"
+        bad = check(ins, labels, valu_srcc, valu_all)
+        what = ("load(s) or VALU write(s)" if valu_all else
+                "load(s) or VALU write(s) of C inputs" if valu_srcc else "load(s)")
         print(f"{n}: {sum(1 for x in ins if x.startswith('v_mfma'))} MFMAs, {len(bad)} {what} into live MFMA operands")
         for i, j, t, u, hit in bad[:12]:
             print(f"   at {j} after the MFMA at {i}: {t[:64]}\n         {u[:64]}  -> {hit}")
