@@ -26,10 +26,10 @@ def test_mfma_operand_rule(tmp_path):
     assert r.stdout.count(" 0 load(s) into live MFMA operands") == len(names), r.stdout
     # the launched (short-wave) kernels: no VALU write into the C input of a product in flight either
     short = ["k_mxs", "k_mxs422", "k_mxs420"]
-    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), "--valu-srcc", str(asm)]
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), "--valu-all", str(asm)]
                        + short, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
-    assert r.stdout.count(" 0 load(s) or VALU write(s) of C inputs into live MFMA operands") == len(short), r.stdout
+    assert r.stdout.count(" 0 load(s) or VALU write(s) into live MFMA operands") == len(short), r.stdout
     # and no scratch, no VGPR / SGPR spills
     text = asm.read_text()
     for n in ("k_mxs", "k_mxs422", "k_mxs420"):
@@ -129,3 +129,29 @@ def test_mfma_valu_srcc_rule(tmp_path):
     s.write_text("\n".join(["_ZN12_GLOBAL__N_14k_mxE13jx_xform_args:"] + lines + [".Lfunc_end0:", ""]))
     ok = subprocess.run([sys.executable, tool, "--valu-srcc", str(s), "k_mx"], capture_output=True, text=True)
     assert ok.returncode == 0, ok.stdout
+
+
+def test_mfma_chained_operand_rule(tmp_path):
+    """--valu-all: a chained product (C input from a register) may start late, so a VALU write into
+    its A operand before a result is read is a violation; the same write after an independent
+    product (C = 0) is not (hipcc's padding holds for it)"""
+    tool = os.path.join(REPO, "tools", "mfma_war_check.py")
+    s = tmp_path / "fake.s"
+
+    def run(lines):
+        s.write_text("\n".join(["_ZN12_GLOBAL__N_14k_mxE13jx_xform_args:"] + lines + [".Lfunc_end0:", ""]))
+        return subprocess.run([sys.executable, tool, "--valu-all", str(s), "k_mx"], capture_output=True, text=True)
+
+    chained = run([
+        "\tv_mfma_f32_16x16x32_f16 v[8:11], v[0:3], v[4:7], 0",
+        "\tv_mfma_f32_16x16x32_f16 v[12:15], v[16:19], v[4:7], v[8:11]",
+        "\ts_nop 2",
+        "\tv_perm_b32 v16, s0, v20, v21",
+        "\tv_add_f32_e32 v30, v12, v13"])
+    assert chained.returncode == 1 and " 1 load(s) or VALU write(s)" in chained.stdout, chained.stdout
+    independent = run([
+        "\tv_mfma_f32_16x16x32_f16 v[8:11], v[0:3], v[4:7], 0",
+        "\ts_nop 2",
+        "\tv_perm_b32 v0, s0, v20, v21",
+        "\tv_add_f32_e32 v30, v8, v9"])
+    assert independent.returncode == 0, independent.stdout
