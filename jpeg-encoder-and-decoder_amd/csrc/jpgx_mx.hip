@@ -2092,7 +2092,7 @@ __device__ MxsImg1 g_mxs422_img1[2][JX_MAXQ + 1];
 /* waves per workgroup: 1 (B operands from the global image) or 4 (B, scales, limc and the zig-zag
  * table in LDS, shared through one s_barrier; band limits from the global image, rare path) */
 #ifndef JX_MXS422_WPG
-#define JX_MXS422_WPG 1
+#define JX_MXS422_WPG 4
 #endif
 constexpr unsigned kMxs422WPG = JX_MXS422_WPG;
 static_assert(kMxs422WPG == 1 || kMxs422WPG == 4, "1 or 4 waves per workgroup");
@@ -2978,7 +2978,7 @@ static_assert(2 * 384 <= 16 * kBS - kSt420C, "qtrue inside the chroma stage");
 /* waves per workgroup: 1 (B operands from the global image, the scales in the wave's LDS) or 4
  * (the whole image in LDS, shared through one s_barrier) */
 #ifndef JX_MXS420_WPG
-#define JX_MXS420_WPG 1
+#define JX_MXS420_WPG 4
 #endif
 constexpr unsigned kMxs420WPG = JX_MXS420_WPG;
 static_assert(kMxs420WPG == 1 || kMxs420WPG == 4, "1 or 4 waves per workgroup");
