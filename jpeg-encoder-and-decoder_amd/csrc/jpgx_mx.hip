@@ -1074,7 +1074,6 @@ struct alignas(16) MxsImg {
 };
 constexpr unsigned kMxsPieces = sizeof(MxsImg) / 16;
 static_assert(sizeof(MxsImg) % 16 == 0 && kMxsPieces <= 768, "three 16-byte pieces per thread");
-static_assert(sizeof(MxsLds) * 4 + sizeof(MxsImg) <= 40 * 1024, "4 workgroups of 4 waves per CU");
 __device__ MxsImg g_mxs_img[2][JX_MAXQ + 1];     /* [force][quality] */
 /* waves per workgroup: 4 (the image above shared through one s_barrier) or 1 (each wave its own
  * small image -- the scales, hot-path limits and zig-zag positions -- and its B operands and band
@@ -1083,14 +1082,16 @@ __device__ MxsImg g_mxs_img[2][JX_MAXQ + 1];     /* [force][quality] */
 #define JX_MXS_WPG 4
 #endif
 constexpr unsigned kMxsWPG = JX_MXS_WPG;
-static_assert(kMxsWPG == 1 || kMxsWPG == 4, "k_mxs: 1 or 4 waves per workgroup");
+static_assert(kMxsWPG == 1 || kMxsWPG == 4 || kMxsWPG == 8, "k_mxs: 1, 4 or 8 waves per workgroup");
+static_assert(kMxsWPG == 1 || sizeof(MxsLds) * kMxsWPG + sizeof(MxsImg) <= 160 * 1024 / (16 / kMxsWPG),
+              "16 waves per CU");
 struct alignas(16) MxsImg1 {
     MxsScales sc;
     float limc[2][16];
     uint8_t scan_t[8][8];
 };
 static_assert(sizeof(MxsImg1) % 16 == 0 && sizeof(MxsImg1) / 16 <= 128, "two 16-byte pieces per lane");
-static_assert(kMxsWPG == 4 || (sizeof(MxsLds) + sizeof(MxsImg1) + 511) / 512 * 512 * 16 <= 160 * 1024,
+static_assert(kMxsWPG != 1 || (sizeof(MxsLds) + sizeof(MxsImg1) + 511) / 512 * 512 * 16 <= 160 * 1024,
               "16 one-wave workgroups per CU");
 __device__ MxsImg1 g_mxs_img1[2][JX_MAXQ + 1];
 using MxsShared = std::conditional<kMxsWPG == 1, MxsImg1, MxsImg>::type;
@@ -1234,13 +1235,13 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
     MxsLds &L = s_lds[wave];
     const MxsImg &gimg = g_mxs_img[g.force ? 1 : 0][g.quality];
     /* the image into LDS (LDS-DMA: piece p of thread t lands at 16 p) */
-    if constexpr (kMxsWPG == 4) {
+    if constexpr (kMxsWPG >= 2) {
         const uint8_t *img = (const uint8_t *)&gimg;
 #pragma unroll
-        for (unsigned i = 0; i < 3; i++) {
-            const unsigned piece = 256u * i + threadIdx.x;
-            if (256u * i + 64u * wave < kMxsPieces && piece < kMxsPieces)
-                mxs_dma<16>(img + 16u * piece, (uint8_t *)&s_img + 16u * (256u * i + 64u * wave));
+        for (unsigned i = 0; i < (kMxsPieces + 64u * kMxsWPG - 1u) / (64u * kMxsWPG); i++) {
+            const unsigned piece = 64u * kMxsWPG * i + threadIdx.x;
+            if (64u * kMxsWPG * i + 64u * wave < kMxsPieces && piece < kMxsPieces)
+                mxs_dma<16>(img + 16u * piece, (uint8_t *)&s_img + 16u * (64u * kMxsWPG * i + 64u * wave));
         }
     } else {
         constexpr unsigned kP1 = sizeof(MxsImg1) / 16;
@@ -1280,7 +1281,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         if (cmp.b >= g.total) return;
     }
     mx_wait_vm<2u * kPro>();
-    if constexpr (kMxsWPG == 4) __builtin_amdgcn_s_barrier();
+    if constexpr (kMxsWPG >= 2) __builtin_amdgcn_s_barrier();
     mx_wave_sync();
     if (cmp.b >= g.total) return;
     /* stage addresses of this lane's column at v = 0..7: the zig-zag positions from the image (no
@@ -2095,16 +2096,16 @@ __device__ MxsImg1 g_mxs422_img1[2][JX_MAXQ + 1];
 #define JX_MXS422_WPG 4
 #endif
 constexpr unsigned kMxs422WPG = JX_MXS422_WPG;
-static_assert(kMxs422WPG == 1 || kMxs422WPG == 4, "1 or 4 waves per workgroup");
+static_assert(kMxs422WPG == 1 || kMxs422WPG == 4 || kMxs422WPG == 8, "1, 4 or 8 waves per workgroup");
 struct alignas(16) MxsImg422w {
     mx_u4 B[JX_MX_PARTS * 4][64];
     MxsImg1 s;
 };
 constexpr unsigned kMxs422Pieces = sizeof(MxsImg422w) / 16;
-static_assert(kMxs422Pieces <= 768 && (kMxs422WPG == 1 || sizeof(Mxs422Lds) * 4 + sizeof(MxsImg422w) <= 40 * 1024),
+static_assert(kMxs422WPG == 1 || sizeof(Mxs422Lds) * kMxs422WPG + sizeof(MxsImg422w) <= 160 * 1024 / (16 / kMxs422WPG),
               "4 workgroups of 4 waves per CU");
 __device__ MxsImg422w g_mxs422_imgw[2][JX_MAXQ + 1];
-typedef std::conditional<kMxs422WPG == 4, MxsImg422w, MxsImg1>::type Mxs422Shared;
+typedef std::conditional<kMxs422WPG >= 2, MxsImg422w, MxsImg1>::type Mxs422Shared;
 [[maybe_unused]] __device__ __forceinline__ const MxsImg1 &mxs422_s(const MxsImg422w &l) { return l.s; }
 [[maybe_unused]] __device__ __forceinline__ const MxsImg1 &mxs422_s(const MxsImg1 &l) { return l; }
 [[maybe_unused]] __device__ __forceinline__ const mx_u4 (&mxs422_B(const MxsImg422w &l, const MxsImg422 &))[JX_MX_PARTS * 4][64]
@@ -2142,13 +2143,13 @@ __global__ __launch_bounds__(64 * kMxs422WPG, JX_MX422_WPE) void k_mxs422(const 
     const unsigned wave = kMxs422WPG == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     Mxs422Lds &L = s_lds[wave];
     const MxsImg422 &gimg = g_mxs422_img[g.force ? 1 : 0][g.quality];
-    if constexpr (kMxs422WPG == 4) {
+    if constexpr (kMxs422WPG >= 2) {
         const uint8_t *img = (const uint8_t *)&g_mxs422_imgw[g.force ? 1 : 0][g.quality];
 #pragma unroll
-        for (unsigned i = 0; i < 3; i++) {
-            const unsigned piece = 256u * i + threadIdx.x;
-            if (256u * i + 64u * wave < kMxs422Pieces && piece < kMxs422Pieces)
-                mxs_dma<16>(img + 16u * piece, (uint8_t *)&s_img + 16u * (256u * i + 64u * wave));
+        for (unsigned i = 0; i < (kMxs422Pieces + 64u * kMxs422WPG - 1u) / (64u * kMxs422WPG); i++) {
+            const unsigned piece = 64u * kMxs422WPG * i + threadIdx.x;
+            if (64u * kMxs422WPG * i + 64u * wave < kMxs422Pieces && piece < kMxs422Pieces)
+                mxs_dma<16>(img + 16u * piece, (uint8_t *)&s_img + 16u * (64u * kMxs422WPG * i + 64u * wave));
         }
     } else {
         constexpr unsigned kP1 = sizeof(MxsImg1) / 16;
@@ -2188,7 +2189,7 @@ __global__ __launch_bounds__(64 * kMxs422WPG, JX_MX422_WPE) void k_mxs422(const 
         if (cmp.b >= g.total) return;
     }
     mx_wait_vm<2u * kMxs422C>();                    /* the image (older than the pixel DMA) */
-    if constexpr (kMxs422WPG == 4) __builtin_amdgcn_s_barrier();
+    if constexpr (kMxs422WPG >= 2) __builtin_amdgcn_s_barrier();
     mx_wave_sync();
     if (cmp.b >= g.total) return;
     const MxsImg1 &si = mxs422_s(s_img);
@@ -2981,7 +2982,7 @@ static_assert(2 * 384 <= 16 * kBS - kSt420C, "qtrue inside the chroma stage");
 #define JX_MXS420_WPG 4
 #endif
 constexpr unsigned kMxs420WPG = JX_MXS420_WPG;
-static_assert(kMxs420WPG == 1 || kMxs420WPG == 4, "1 or 4 waves per workgroup");
+static_assert(kMxs420WPG == 1 || kMxs420WPG == 4 || kMxs420WPG == 8, "1, 4 or 8 waves per workgroup");
 struct alignas(16) MxsImg420 {
     mx_u4 B[JX_MX_PARTS * 5][64];
     MxTab tab;
@@ -2991,12 +2992,12 @@ struct alignas(16) MxsImg420 {
 constexpr unsigned kMxs420Pieces = sizeof(MxsImg420) / 16;
 static_assert(sizeof(MxsImg420) % 16 == 0 && kMxs420Pieces <= 1024, "four 16-byte pieces per thread");
 static_assert(sizeof(Mxs420Lds) % 16 == 0 &&
-                  (kMxs420WPG == 4 ? sizeof(Mxs420Lds) * 4 + sizeof(MxsImg420) <= 40 * 1024
+                  (kMxs420WPG >= 2 ? sizeof(Mxs420Lds) * kMxs420WPG + sizeof(MxsImg420) <= 160 * 1024 / (16 / kMxs420WPG)
                                    : sizeof(Mxs420Lds) + sizeof(MxsImg1) <= 10 * 1024),
               "16 waves per CU");
 __device__ MxsImg420 g_mxs420_img[2][JX_MAXQ + 1];
 __device__ MxsImg1 g_mxs420_img1[2][JX_MAXQ + 1];
-typedef std::conditional<kMxs420WPG == 4, MxsImg420, MxsImg1>::type Mxs420Shared;
+typedef std::conditional<kMxs420WPG >= 2, MxsImg420, MxsImg1>::type Mxs420Shared;
 [[maybe_unused]] __device__ __forceinline__ const mx_u4 (&mxs420_B(const MxsImg420 &l, const MxsImg420 &))[JX_MX_PARTS * 5][64]
 {
     return l.B;
@@ -3042,13 +3043,13 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
     const unsigned wave = kMxs420WPG == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     Mxs420Lds &L = s_lds[wave];
     const MxsImg420 &gimg = g_mxs420_img[g.force ? 1 : 0][g.quality];
-    if constexpr (kMxs420WPG == 4) {
+    if constexpr (kMxs420WPG >= 2) {
         const uint8_t *img = (const uint8_t *)&gimg;
 #pragma unroll
-        for (unsigned i = 0; i < 4; i++) {
-            const unsigned piece = 256u * i + threadIdx.x;
-            if (256u * i + 64u * wave < kMxs420Pieces && piece < kMxs420Pieces)
-                mxs_dma<16>(img + 16u * piece, (uint8_t *)&s_img + 16u * (256u * i + 64u * wave));
+        for (unsigned i = 0; i < (kMxs420Pieces + 64u * kMxs420WPG - 1u) / (64u * kMxs420WPG); i++) {
+            const unsigned piece = 64u * kMxs420WPG * i + threadIdx.x;
+            if (64u * kMxs420WPG * i + 64u * wave < kMxs420Pieces && piece < kMxs420Pieces)
+                mxs_dma<16>(img + 16u * piece, (uint8_t *)&s_img + 16u * (64u * kMxs420WPG * i + 64u * wave));
         }
     } else {
         constexpr unsigned kP1 = sizeof(MxsImg1) / 16;
@@ -3096,7 +3097,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
         if (m0 >= h.tm) return;
     }
     mx_wait_vm<4>();                                    /* the image (older than the pixel DMA) */
-    if constexpr (kMxs420WPG == 4) __builtin_amdgcn_s_barrier();
+    if constexpr (kMxs420WPG >= 2) __builtin_amdgcn_s_barrier();
     mx_wave_sync();
     if (m0 >= h.tm) return;
     uint32_t za[8];
