@@ -43,6 +43,8 @@ struct jx_geom {
     int row0;               /* frame block-row of stripe row 0 (underflow only at row 0)  */
     uint32_t under[6];      /* the underflow pixel row, interleaved (u0 u0 u0 u1 u1 u1..)  */
     struct jx_udiv dnb, dbpr;   /* division by nb and by bpr                              */
+    uint32_t mpr, nmcu;         /* true 4:2:0: MCUs per MCU row, per frame (16x16 MCUs)       */
+    struct jx_udiv dmpr, dnmcu; /* division by them                                       */
 };
 
 /* Per-quality tables, device resident (one copy per quality 1..97, built once per device).

@@ -879,6 +879,10 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     g.row0 = fr->row_begin;
     g.dnb = jx_udiv_make((uint32_t)nb);
     g.dbpr = jx_udiv_make((uint32_t)bpr);
+    g.mpr = (uint32_t)bpr / 2u;
+    g.nmcu = (uint32_t)(nb / (size_t)bpr / 2u) * g.mpr;
+    g.dmpr = jx_udiv_make(g.mpr ? g.mpr : 1u);
+    g.dnmcu = jx_udiv_make(g.nmcu ? g.nmcu : 1u);
     jx_under_dwords(p->underflow, g.under);
     rc = tables_for_current_device();
     if (rc) return rc;

@@ -2382,6 +2382,7 @@ __device__ jx_mxtab g_mx420tab[2][JX_MAXQ + 1];
 /* MCU geometry of the launch */
 struct Mx420G {
     unsigned mpr, nmcu, tm, rows;       /* MCUs per row, per frame, in the launch; MCU rows per frame */
+    jx_udiv dmpr, dnmcu;                /* division by mpr, nmcu (jx_geom) */
 };
 
 struct Mx420Chunk {
@@ -2402,9 +2403,9 @@ __device__ __forceinline__ void mx420_ptrs(Mx420Chunk &C, const MxG &g, const Mx
 __device__ __forceinline__ void mx420_at(Mx420Chunk &C, const MxG &g, const Mx420G &h, unsigned m0)
 {
     C.m0 = m0;
-    C.f = m0 / h.nmcu;
+    C.f = mx_udiv(m0, h.dnmcu);
     C.mi = m0 - C.f * h.nmcu;
-    C.my = C.mi / h.mpr;
+    C.my = mx_udiv(C.mi, h.dmpr);
     C.mx = C.mi - C.my * h.mpr;
     mx420_ptrs(C, g, h);
 }
@@ -2432,9 +2433,9 @@ __device__ __forceinline__ void mx420_next(Mx420Chunk &C, const MxG &g, const Mx
 __device__ __forceinline__ void mx420_mcu(const Mx420G &h, unsigned m, unsigned &f, unsigned &mi,
                                           unsigned &my, unsigned &mx)
 {
-    f = m / h.nmcu;
+    f = mx_udiv(m, h.dnmcu);
     mi = m - f * h.nmcu;
-    my = mi / h.mpr;
+    my = mx_udiv(mi, h.dmpr);
     mx = mi - my * h.mpr;
 }
 
@@ -2703,10 +2704,12 @@ __global__ __launch_bounds__(256, JX_MX420_WPE) void k_mx420(const jx_xform_args
     g.dnb = a.g.dnb;
     g.dbpr = a.g.dbpr;
     Mx420G h;
-    h.mpr = g.bpr / 2u;
-    h.rows = g.nb / g.bpr / 2u;
-    h.nmcu = h.rows * h.mpr;
+    h.mpr = a.g.mpr;
+    h.nmcu = a.g.nmcu;
+    h.rows = mx_udiv(h.nmcu, a.g.dmpr);
     h.tm = h.nmcu * (unsigned)a.g.nframes;
+    h.dmpr = a.g.dmpr;
+    h.dnmcu = a.g.dnmcu;
 
     const unsigned lane = threadIdx.x & 63u;
     Mx420Lds &L = s_lds[threadIdx.x >> 6];
@@ -3034,10 +3037,12 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
     g.dnb = a.g.dnb;
     g.dbpr = a.g.dbpr;
     Mx420G h;
-    h.mpr = g.bpr / 2u;
-    h.rows = g.nb / g.bpr / 2u;
-    h.nmcu = h.rows * h.mpr;
+    h.mpr = a.g.mpr;
+    h.nmcu = a.g.nmcu;
+    h.rows = mx_udiv(h.nmcu, a.g.dmpr);
     h.tm = h.nmcu * (unsigned)a.g.nframes;
+    h.dmpr = a.g.dmpr;
+    h.dnmcu = a.g.dnmcu;
 
     const unsigned lane = threadIdx.x & 63u;
     const unsigned wave = kMxs420WPG == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
