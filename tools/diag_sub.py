@@ -37,8 +37,8 @@ for sr in srs:
         got = out.cpu().numpy()
         bad = np.argwhere((got != want).any(axis=2))
         desc = []
-        for f, b in bad[:10]:
+        for f, b in bad[:int(os.environ.get("DIAG_SHOW", "10"))]:
             plane = 0 if b < nb else (1 if b < nb + nbc else 2)
             bb = b if plane == 0 else (b - nb if plane == 1 else b - nb - nbc)
-            desc.append((int(f), plane, int(bb), int(bb) % 8))
+            desc.append((int(f), plane, int(bb) // (W // 8), int(bb) % (W // 8)) if plane == 0 else (int(f), plane, int(bb)))
         print(f"sr{sr} rep {r}: {len(bad)} wrong block(s) {desc}", flush=True)

@@ -11,7 +11,7 @@ if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/gpu_tests.txt" 2>&1
   rc=$?; tail -3 "$OUT/gpu_tests.txt"; [ $rc -eq 0 ] || exit $rc
 fi
-KB_SUB=0 timeout -k 10 300 python tools/kbench.py 2 w1c3 legacy > "$OUT/kb444.txt" 2>&1 || exit $?
+KB_SUB=0 timeout -k 10 300 python tools/kbench.py 2 nokc w1c3 legacy > "$OUT/kb444.txt" 2>&1 || exit $?
 KB_SUB=1 timeout -k 10 300 python tools/kbench.py 2 l422 s422w4 > "$OUT/kb422.txt" 2>&1 || exit $?
 KB_SUB=2 timeout -k 10 300 python tools/kbench.py 2 l420 s420w4 > "$OUT/kb420.txt" 2>&1 || exit $?
 cat "$OUT/kb444.txt" "$OUT/kb422.txt" "$OUT/kb420.txt"
