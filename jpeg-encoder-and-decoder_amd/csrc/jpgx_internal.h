@@ -82,6 +82,7 @@ struct jx_mxtab {
     float lsq[24][8];       /* a float <= lim^2 of the rigorous band (flag: d*d - lsq >= 0);
                                -1 with FORCE_EXACT                                            */
     int16_t q[2][64];       /* scaled tables, q[t][u*8+v] = Qs[u][v] (src/quantise.c:58)       */
+    double r[2][64];        /* fl(fl(1/4 a(u) a(v)) / q[t][u*8+v]): the exact pass's fast decision */
 };
 
 struct jx_xform_args {

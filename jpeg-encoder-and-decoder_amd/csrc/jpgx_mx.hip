@@ -134,9 +134,9 @@ __constant__ double kMxAlpha[8] = {JX_ALPHA0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0}
 /* per channel the reference's colour constants as the exact pass uses them: t = (k0 r + k1 g)
  * + k2 b (the signs of its subtractions folded into k1, k2: a - b*k == a + b*(-k) exactly),
  * then (A + S t) - 128 with (A, S) = (0, 1) Y, (128, -1) Cb, (128, 1) Cr */
-__constant__ double kMxColour[3][5] = {{0.299, 0.587, 0.114, 0.0, 1.0},
-                                       {0.168736, -0.331264, 0.5, 128.0, -1.0},
-                                       {0.5, -0.418688, -0.081312, 128.0, 1.0}};
+#define JX_MX_COLOUR_INIT                                                                          \
+    {{0.299, 0.587, 0.114, 0.0, 1.0}, {0.168736, -0.331264, 0.5, 128.0, -1.0}, {0.5, -0.418688, -0.081312, 128.0, 1.0}}
+__constant__ double kMxColour[3][5] = JX_MX_COLOUR_INIT;
 
 /* Keep the compiler from moving this wave's LDS accesses across this point (a wave's LDS
  * instructions execute in program order; no fence: that would drain the memory counters). */
@@ -389,11 +389,52 @@ __device__ __forceinline__ void mx_pad(const MxG &g, Lds &L, int n)
  * transposed divisor (quantise.c:58).  px = the block's pixel row 0, rows rs bytes apart.  The
  * result is valid in lane x == 7.
  */
-/* the x-outer / y-inner sum of the products (lane x holds the 8 of its x), F and round(F / Q):
- * valid in lane x == 7 */
-__device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch, unsigned u, unsigned v,
-                                            unsigned x, const jx_mxtab &T)
+/* s of lane (x ^ 1), (x ^ 2) or (7 - x) of an 8-lane group (DPP quad_perm / row_half_mirror) */
+template <int CTRL>
+__device__ __forceinline__ double mx_dpp64(double s)
 {
+    const uint64_t b = __builtin_bit_cast(uint64_t, s);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+}
+
+/*
+ * The x-outer / y-inner sum of the products (lane x holds the 8 of its x), F and round(F / Q).
+ *
+ * Fast decision (round 5, JX_MX_FASTEXACT): the reference's 64-term sum runs sequentially
+ * (dct.c:46-50), but only round(F / Q) is kept.  Each lane sums its 8 products in order, the 8
+ * partial sums meet in a 3-level butterfly (every lane ends with the same total, a + b == b + a):
+ * every term passes at most 10 additions.  Terms: |X| <= 171 (the Cb quirk, preprocess.c:161:
+ * 128 - (0.168736 r - 0.331264 g + 0.5 b) spans [-170.6, 84.5]; Y, Cr and the 4:2:x averages stay
+ * inside), |c| <= 1, so sum |t| <= 64 * 171 (1 + u)^2 <= 10944.01 (u = 2^-53).  Recursive
+ * summation (Higham, Thm 4.4): |s_seq - s| <= g63 sum|t|, |s_par - s| <= g10 sum|t| (g_n = n u /
+ * (1 - n u)), so |s_seq - s_par| <= 73.01 u 10944.01 < 8.9e-11.  The reference's t = fl(fl(K s) /
+ * Q) (K = (1/4 a(u)) a(v) in (0, 0.25], Q >= 1, |t| <= 2736) and the fast t' = fl(s_par R), R =
+ * fl(K / Q) from the table (jx_mxtab.r, R), differ by at most 0.25 * 8.9e-11 + 4.01 u 2736 < 2.4e-11.
+ * So when t' is more than 2^-33 (1.16e-10) away from every half-integer (|t' - rint(t')| < 1/2 -
+ * 2^-33; the difference is exact), no half-integer lies between t' and the reference's t, and
+ * round(t) == rint(t').  Otherwise (near-ties: flat blocks, exact DC halves) the whole batch takes
+ * the sequential sum -- wave-uniform, rare.
+ * Valid in lane x == 7 (fast path: every lane).
+ */
+#ifndef JX_MX_FASTEXACT
+#define JX_MX_FASTEXACT 1
+#endif
+template <bool FAST = (JX_MX_FASTEXACT != 0)>
+__device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch, unsigned u, unsigned v,
+                                            unsigned x, const jx_mxtab &T, double R)
+{
+    if constexpr (FAST) {
+        double p = prod[0];
+#pragma unroll
+        for (int y = 1; y < 8; y++) p += prod[y];
+        p += mx_dpp64<0xB1>(p);                  /* quad_perm [1,0,3,2]: lane x ^ 1 */
+        p += mx_dpp64<0x4E>(p);                  /* quad_perm [2,3,0,1]: lane x ^ 2 */
+        p += mx_dpp64<0x141>(p);                 /* row_half_mirror: lane 7 - x      */
+        const double t = p * R, r = __builtin_rint(t);
+        if (__ballot(0.5 - __builtin_fabs(t - r) <= 0x1p-33) == 0) return (int)r;   /* t - r: exact */
+    }
     double sum = 0.0;
 #pragma unroll
     for (int xx = 0; xx < 8; xx++) {
@@ -408,12 +449,38 @@ __device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch
     return (int)round(F / (double)q);
 }
 
+/* where the exact pass's constants come from: the __constant__ tables (MxExConst; k_mx, the
+ * 4:2:x kernels) or a copy in the workgroup's LDS image (MxExTab; k_mxs: under full HBM load a
+ * global read of a table costs the wave microseconds, round 5) */
+struct MxExConst {
+    const jx_mxtab &T;
+    __device__ double cosx(unsigned k, unsigned i) const { return kMxCos[k][i]; }
+    __device__ double colour(unsigned ch, unsigned i) const { return kMxColour[ch][i]; }
+    __device__ double recip(unsigned c, unsigned i) const { return T.r[c][i]; }
+    __device__ unsigned scan(unsigned u, unsigned v) const { return (unsigned)kMxScan[v][u]; }
+};
+struct alignas(16) MxExTab {
+    double cosx_[8][8];                 /* kMxCos                                    */
+    double colour_[3][5];               /* kMxColour                                 */
+    double pad_;
+    double r_[2][64];                   /* jx_mxtab.r of the workgroup's quality     */
+};
+struct MxExLds {
+    const MxExTab &X;
+    const uint8_t (&scan_t)[8][8];
+    __device__ double cosx(unsigned k, unsigned i) const { return X.cosx_[k][i]; }
+    __device__ double colour(unsigned ch, unsigned i) const { return X.colour_[ch][i]; }
+    __device__ double recip(unsigned c, unsigned i) const { return X.r_[c][i]; }
+    __device__ unsigned scan(unsigned u, unsigned v) const { return scan_t[u][v]; }
+};
+
+template <class XT>
 __device__ __forceinline__ int mx_exact_coef(const lds_u8 *px, unsigned rs, unsigned ch, unsigned u,
-                                             unsigned v, unsigned x, const jx_mxtab &T)
+                                             unsigned v, unsigned x, const jx_mxtab &T, const XT &xt)
 {
-    const double cu = kMxCos[u][x];
-    const double k0c = kMxColour[ch][0], k1c = kMxColour[ch][1], k2c = kMxColour[ch][2];
-    const double Ac = kMxColour[ch][3], Sc = kMxColour[ch][4];
+    const double cu = xt.cosx(u, x);
+    const double k0c = xt.colour(ch, 0), k1c = xt.colour(ch, 1), k2c = xt.colour(ch, 2);
+    const double Ac = xt.colour(ch, 3), Sc = xt.colour(ch, 4);
     double prod[8];
 #pragma unroll
     for (int y = 0; y < 8; y++) {
@@ -421,9 +488,9 @@ __device__ __forceinline__ int mx_exact_coef(const lds_u8 *px, unsigned rs, unsi
         const double rr = (double)p[0], gv = (double)p[1], bv = (double)p[2];
         const double tt = (k0c * rr + k1c * gv) + k2c * bv;
         const double X = (Ac + Sc * tt) - 128.0;
-        prod[y] = X * cu * kMxCos[v][y];
+        prod[y] = X * cu * xt.cosx(v, y);
     }
-    return mx_exact_sum(prod, ch, u, v, x, T);
+    return mx_exact_sum(prod, ch, u, v, x, T, xt.recip(ch == 0 ? 0 : 1, u * 8 + v));
 }
 
 __device__ __forceinline__ lds_u8 *mx_lds(void *p) { return (lds_u8 *)p; }
@@ -438,9 +505,9 @@ __device__ __forceinline__ unsigned mx_col_block(unsigned k, unsigned sl)
 /* Inline exact pass of one step (a step with more tasks than the deferred queue holds, e.g.
  * FLAG_FORCE_EXACT): every flagged coefficient (bit 8 col + v of a lane's `bits`), eight at a
  * time, patching the stage. */
-template <bool LEAN = false, class Lds>
+template <bool LEAN = false, class Lds, class XT>
 __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uint32_t bits,
-                                                const jx_mxtab &T)
+                                                const jx_mxtab &T, const XT &xt)
 {
     const unsigned lane = mx_lane();
     mx_wave_sync();
@@ -461,11 +528,11 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
         const unsigned sl = code >> 8, k = (code >> 3) & 3u, v = code & 7u;
         const unsigned jj = sl & 15u, u = jj & 7u, ch = k < 2 ? (jj >> 3) : 2u;
         const unsigned jb = mx_col_block(k, sl);
-        const int val = mx_exact_coef(mx_lds((void *)slot) + 24u * jb, 192u, ch, u, v, x, T);
+        const int val = mx_exact_coef(mx_lds((void *)slot) + 24u * jb, 192u, ch, u, v, x, T, xt);
         if (live && x == 7)
             *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) +
                                                            kBS * (LEAN ? mx_pos_lean(ch, jb) : mx_pos(ch, jb)) +
-                                                           2u * (unsigned)kMxScan[v][u]) = (int16_t)val;
+                                                           2u * xt.scan(u, v)) = (int16_t)val;
         mx_wave_sync();
     }
 }
@@ -488,7 +555,7 @@ __device__ __forceinline__ void mx_flush(MxLds &L, int &nq, int &ns, const MxG &
         const bool act = vb != 0;
         const unsigned v = act ? (unsigned)__builtin_ctz(vb) : 0u;
         vb &= vb - 1u;
-        const int val = mx_exact_coef(mx_lds(L.pix[slot]), 24u, ch, u, v, x, T);
+        const int val = mx_exact_coef(mx_lds(L.pix[slot]), 24u, ch, u, v, x, T, MxExConst{T});
         if (act && x == 7) dst[kMxScan[v][u]] = (int16_t)val;
     }
     mx_wave_sync();
@@ -529,7 +596,7 @@ __device__ __forceinline__ void mx_defer(MxLds &L, const uint8_t *sp, uint32_t b
     if (nq + ncol > kSide || ns + nblk > kSidePix) {
         if (nq) mx_flush(L, nq, ns, g, T);
         if (ncol > kSide || nblk > kSidePix) {
-            mx_exact_inline(L, sp, bits, T);
+            mx_exact_inline(L, sp, bits, T, MxExConst{T});
             return;
         }
     }
@@ -666,6 +733,17 @@ __device__ __forceinline__ void mx_fence(const mx_f4 &r)
 {
     const uint32_t v = __builtin_amdgcn_readfirstlane(__float_as_uint(r.w));
     asm volatile("" ::"s"(v) : "memory");
+}
+
+/* the same for a group of products the compiler may issue in any order: one VALU read of every
+ * result (v_add3 + v_add), so the fence waits for the group's last product whichever it is */
+template <int N>
+__device__ __forceinline__ void mx_fence_all(const mx_f4 (&r)[N])
+{
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) v += __float_as_uint(r[i].w);
+    asm volatile("" ::"v"(v) : "memory");
 }
 
 /* Keep the C inputs of chained products live (so that no VALU instruction or load reuses their
@@ -1066,8 +1144,33 @@ struct alignas(16) MxsLds {
 static_assert(sizeof(MxsLds) % 16 == 0, "16-byte aligned LDS regions");
 /* the workgroup image: B operands, scale / limit table, hot-path limits (mx_limc) per lane
  * profile and column kind */
-struct alignas(16) MxsImg {
-    mx_u4 B[3 * JX_MX_PARTS][64];
+#ifndef JX_MXS_BLDS
+#define JX_MXS_BLDS 0                   /* 1: B operands read from the LDS image every step (fewer VGPRs) */
+#endif
+/* Round-5 experiment (profiles/r05_exact_pass.txt): B operands from global memory (g_mxB) and the
+ * exact pass's tables in the image instead.  The tables in LDS save ~3 us per launch, but every
+ * build that loads B from global memory -- at the top of the wave, after the image barrier, with
+ * or without a full drain before step 0 -- gives wrong C rows 12..15 (blocks 3 / 7 of a step,
+ * mostly the chained Cr tile) in 10-100 % of launches, and tools/mfma_war_check.py finds no rule
+ * violation in their ISA: not root-caused, so the product keeps B in the LDS image.  Diagnostics
+ * only (NOT exact): JX_MXS_BGLOBAL=1, with JX_MXS_BLATE / JX_MXS_DRAIN0. */
+#ifndef JX_MXS_BLATE
+#define JX_MXS_BLATE 0
+#endif
+#ifndef JX_MXS_DRAIN0
+#define JX_MXS_DRAIN0 0
+#endif
+#ifndef JX_MXS_BGLOBAL
+#define JX_MXS_BGLOBAL 0
+#endif
+constexpr bool kMxsBGlobal = JX_MXS_BGLOBAL != 0;
+struct alignas(16) MxsImgB {
+    mx_u4 B[3 * JX_MX_PARTS][64];       /* B operands                                */
+};
+struct alignas(16) MxsImgX {
+    MxExTab ex;                         /* the exact pass's tables (B: g_mxB)        */
+};
+struct alignas(16) MxsImg : std::conditional<kMxsBGlobal, MxsImgX, MxsImgB>::type {
     MxTab tab;
     float limc[2][16];
     uint8_t scan_t[8][8];               /* zig-zag position of (v, u) at [u][v] */
@@ -1097,8 +1200,14 @@ __device__ MxsImg1 g_mxs_img1[2][JX_MAXQ + 1];
 using MxsShared = std::conditional<kMxsWPG == 1, MxsImg1, MxsImg>::type;
 /* where the B operands and the column tables come from (four-wave image / one-wave image) */
 typedef mx_u4 MxsBOps[3 * JX_MX_PARTS][64];
-__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg &l, const MxsImg &) { return l.B; }
-[[maybe_unused]] __device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg1 &, const MxsImg &g) { return g.B; }
+__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImgB &l) { return l.B; }
+__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImgX &) { return g_mxB; }
+__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg &l, const MxsImg &) { return mxs_B(l); }
+[[maybe_unused]] __device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg1 &, const MxsImg &g) { return mxs_B(g); }
+/* the exact pass's tables: the LDS image's copy, or the __constant__ tables */
+__device__ __forceinline__ MxExLds mxs_xt(const MxsImgX &l, const uint8_t (&scan)[8][8], const jx_mxtab &) { return MxExLds{l.ex, scan}; }
+__device__ __forceinline__ MxExConst mxs_xt(const MxsImgB &, const uint8_t (&)[8][8], const jx_mxtab &T) { return MxExConst{T}; }
+[[maybe_unused]] __device__ __forceinline__ MxExConst mxs_xt(const MxsImg1 &, const uint8_t (&)[8][8], const jx_mxtab &T) { return MxExConst{T}; }
 __device__ __forceinline__ const MxTab &mxs_tb(const MxsImg &l, const MxsImg &) { return l.tab; }
 [[maybe_unused]] __device__ __forceinline__ MxsTabRef mxs_tb(const MxsImg1 &l, const MxsImg &g) { return MxsTabRef{l.sc, g.tab}; }
 #ifdef JX_MXS_STAMP                    /* timing probe builds only: per-wave timestamps */
@@ -1234,6 +1343,15 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
     const unsigned wave = kMxsWPG == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     MxsLds &L = s_lds[wave];
     const MxsImg &gimg = g_mxs_img[g.force ? 1 : 0][g.quality];
+    /* B operands from global memory (JX_MXS_BGLOBAL): issued before every DMA, so that waiting
+     * for them never waits for a pixel DMA */
+    mx_u4 B[kParts][3];
+    if constexpr (kMxsBGlobal && !JX_MXS_BLDS && !JX_MXS_BLATE) {
+#pragma unroll
+        for (int p = 0; p < kParts; p++)
+#pragma unroll
+            for (int w = 0; w < 3; w++) B[p][w] = g_mxB[3 * p + w][lane];
+    }
     /* the image into LDS (LDS-DMA: piece p of thread t lands at 16 p) */
     if constexpr (kMxsWPG >= 2) {
         const uint8_t *img = (const uint8_t *)&gimg;
@@ -1275,6 +1393,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
     const uint32_t rcb = (kMxsLean ? 8u : 12u) * kBS + ro;
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
     const jx_mxtab &T = g_mxtab[g.force ? 1 : 0][g.quality];
+    const auto xt = mxs_xt(s_img, s_img.scan_t, T);
 
     /* the image has landed (it is older than the prologue's pixel operations), in every wave */
     if constexpr (kMxsWPG == 1) {
@@ -1294,15 +1413,16 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
 #pragma unroll
         for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
     }
-#ifndef JX_MXS_BLDS
-#define JX_MXS_BLDS 0                   /* 1: B operands read from the LDS image every step (fewer VGPRs) */
+#ifndef JX_MXS_NOEXACT
+#define JX_MXS_NOEXACT 0                /* timing probes only: skip the inline exact pass (NOT exact) */
 #endif
 #if !JX_MXS_BLDS
-    mx_u4 B[kParts][3];
+    if constexpr (!kMxsBGlobal || JX_MXS_BLATE) {
 #pragma unroll
-    for (int p = 0; p < kParts; p++)
+        for (int p = 0; p < kParts; p++)
 #pragma unroll
-        for (int w = 0; w < 3; w++) B[p][w] = mxs_B(s_img, gimg)[3 * p + w][lane];
+            for (int w = 0; w < 3; w++) B[p][w] = mxs_B(s_img, gimg)[3 * p + w][lane];
+    }
 #endif
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
     const auto &tb = mxs_tb(s_img, gimg);
@@ -1421,7 +1541,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
             if (__builtin_expect(__ballot((fl & 0xffffu) != 0) != 0, 0)) {
                 uint32_t f2 = fl & 0xffffu;
                 clamp(f2);
-                mx_exact_inline<true>(L, sp, f2, T);
+                mx_exact_inline<true>(L, sp, f2, T, xt);
             }
             if (S.simple) {
                 const mx_u4 v0 = *(const mx_u4 *)(L.stage + ro);
@@ -1438,7 +1558,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
             if (__builtin_expect(__ballot((fl >> 16) != 0) != 0, 0)) {
                 uint32_t f2 = fl & 0xff0000u;
                 clamp(f2);
-                mx_exact_inline<true>(L, sp, f2, T);
+                mx_exact_inline<true>(L, sp, f2, T, xt);
             }
             if (S.simple) {
                 const mx_u4 v2 = *(const mx_u4 *)(L.stage + rr);
@@ -1463,9 +1583,9 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         mx_column_t<8 * kBS, true>(acc[2], w0, limc2, tb, 2, j, za, fl, 2);
         keepc();
         mx_wave_sync();
-        if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
+        if (!JX_MXS_NOEXACT && __builtin_expect(__ballot(fl != 0) != 0, 0)) {
             clamp(fl);
-            mx_exact_inline(L, sp, fl, T);
+            mx_exact_inline(L, sp, fl, T, xt);
         }
 #endif
         /* stores: always three store instructions (the vmcnt accounting counts on it) */
@@ -1492,7 +1612,10 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         const auto step = [&](auto kc) __attribute__((always_inline)) {
             constexpr unsigned k = decltype(kc)::value < kMxsR ? decltype(kc)::value : kMxsR - 1;
             if (cmp.b >= g.total) return;
-            mx_wait_vm<2 * (kMxsR - 1 - k) + 3 * k>();
+            if (JX_MXS_DRAIN0 && k == 0)
+                mx_wait_vm<0>();
+            else
+                mx_wait_vm<2 * (kMxsR - 1 - k) + 3 * k>();
             body(cmp, L.ring[k]);
             mxs_next(cmp, g);
         };
@@ -1611,6 +1734,7 @@ __device__ __forceinline__ unsigned mx422_yblock(unsigned sl)
  * definition, oracle/cpu_ref.c cpuref_chroma_sample); Y: p = pixel x, d1 = 0 ((X + X) * 0.5 == X
  * exactly, so Y tasks share the code).  Valid in lane x == 7.
  */
+template <bool FAST = (JX_MX_FASTEXACT != 0)>
 __device__ __forceinline__ int mx_exact_pair(const lds_u8 *row0, unsigned rs, unsigned d1, unsigned ch,
                                              unsigned u, unsigned v, unsigned x, const jx_mxtab &T)
 {
@@ -1626,7 +1750,7 @@ __device__ __forceinline__ int mx_exact_pair(const lds_u8 *row0, unsigned rs, un
         const double X = (((Ac + Sc * t0) - 128.0) + ((Ac + Sc * t1) - 128.0)) * 0.5;
         prod[y] = X * cu * kMxCos[v][y];
     }
-    return mx_exact_sum(prod, ch, u, v, x, T);
+    return mx_exact_sum<FAST>(prod, ch, u, v, x, T, T.r[ch == 0 ? 0 : 1][u * 8 + v]);
 }
 
 /* lane x's first pixel (row 0) and row stride of chroma block cb in a step's slot; the right
@@ -1676,7 +1800,7 @@ __device__ __forceinline__ void mx422_exact_inline(Lds &L, const uint8_t *sp, ui
             d1 = 3;
             row0 = mx422_mcu_row0(L, sp, qmask, sl >> 4, x, rs);
         }
-        const int val = mx_exact_pair(row0, rs, d1, ch, u, v, x, T);
+        const int val = mx_exact_pair<false>(row0, rs, d1, ch, u, v, x, T);   /* k_mxs422 at 128 VGPRs: no room */
         if (live && x == 7)
             *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + (k ? kSt422C : 0u) + kBS * slot +
                                                            2u * (unsigned)kMxScan[v][u]) = (int16_t)val;
@@ -1701,8 +1825,8 @@ __device__ __forceinline__ void mx422_flush(Mx422Lds &L, int &nq, int &ns, const
         const bool act = vb != 0;
         const unsigned v = act ? (unsigned)__builtin_ctz(vb) : 0u;
         vb &= vb - 1u;
-        const int val = ch == 0 ? mx_exact_pair(px + 3u * x, 24u, 0u, 0u, u, v, x, T)
-                                : mx_exact_pair(px + 6u * x, 48u, 3u, ch, u, v, x, T);
+        const int val = ch == 0 ? mx_exact_pair<false>(px + 3u * x, 24u, 0u, 0u, u, v, x, T)   /* legacy k_mx422 */
+                                : mx_exact_pair<false>(px + 6u * x, 48u, 3u, ch, u, v, x, T);
         if (act && x == 7) dst[kMxScan[v][u]] = (int16_t)val;
     }
     mx_wave_sync();
@@ -2505,6 +2629,7 @@ __device__ __forceinline__ uint32_t mx420_true_rows(Lds &L, const MxG &g, const 
  * averages the quad ((ls(p00) + ls(p01)) + (ls(p10) + ls(p11))) * 0.25 of chroma row y
  * (oracle/cpu_ref.c cpuref_chroma_sample), then as mx_exact_coef.  row0 = the MCU's pixel (0, 0).
  * Valid in lane x == 7. */
+template <bool FAST = (JX_MX_FASTEXACT != 0)>
 __device__ __forceinline__ int mx_exact_quad(const uint8_t *row0, long long pitch, unsigned ch, unsigned u,
                                              unsigned v, unsigned x, const jx_mxtab &T)
 {
@@ -2522,7 +2647,7 @@ __device__ __forceinline__ int mx_exact_quad(const uint8_t *row0, long long pitc
         const double X = ((l00 + l01) + (l10 + l11)) * 0.25;
         prod[y] = X * cu * kMxCos[v][y];
     }
-    return mx_exact_sum(prod, ch, u, v, x, T);
+    return mx_exact_sum<FAST>(prod, ch, u, v, x, T, T.r[ch == 0 ? 0 : 1][u * 8 + v]);
 }
 
 /* the MCU's pixel (0, 0) */
@@ -2602,8 +2727,8 @@ __device__ __forceinline__ void mx420_flush(Mx420Lds &L, int &nq, int &ns, const
         const bool act = vb != 0;
         const unsigned v = act ? (unsigned)__builtin_ctz(vb) : 0u;
         vb &= vb - 1u;
-        const int val = ch ? mx_exact_quad(src, g.pitch, ch, u, v, x, T)
-                           : mx_exact_pair(mx_lds(L.pix[slot]) + 3u * x, 24u, 0u, 0u, u, v, x, T);
+        const int val = ch ? mx_exact_quad<false>(src, g.pitch, ch, u, v, x, T)   /* legacy k_mx420 */
+                           : mx_exact_pair<false>(mx_lds(L.pix[slot]) + 3u * x, 24u, 0u, 0u, u, v, x, T);
         if (act && x == 7) g.out[dst + kMxScan[v][u]] = (int16_t)val;
     }
     mx_wave_sync();
@@ -3181,7 +3306,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
         __builtin_amdgcn_sched_barrier(0);
         /* the Y products are done before anything writes a register again: a chained product may
          * wait in the matrix pipe and read its operands late (profiles/r04_mfma_valu_war.txt) */
-        mx_fence(accY[3]);
+        mx_fence_all(accY);
         mx_keep(midY);
         mx_keep_ops(Al1, Ah1);
         __builtin_amdgcn_sched_barrier(0);
@@ -3204,7 +3329,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, JX_MX420_WPE) void k_mxs420(const 
         }
         __builtin_amdgcn_sched_barrier(0);
         /* the same for the chroma products */
-        mx_fence(accC[1]);
+        mx_fence_all(accC);
         mx_keep(midC);
         mx_keep_ops(C1, C2);
         __builtin_amdgcn_sched_barrier(0);
@@ -3297,6 +3422,33 @@ float mx_lsq(float lim)
     return s;
 }
 
+/* the fast exact decision's R = fl(K / Q), K = fl((1/4 a(u)) a(v)) as the device computes it
+ * (mx_exact_sum; dct.c:54, quantise.c:58) */
+static void mx_fill_recip(jx_mxtab &t)
+{
+    const double qa0 = 0.25 * JX_ALPHA0;
+    for (int c = 0; c < 2; c++)
+        for (int u = 0; u < 8; u++)
+            for (int v = 0; v < 8; v++) {
+                const double K = (u == 0 ? qa0 : 0.25) * (v == 0 ? JX_ALPHA0 : 1.0);
+                t.r[c][u * 8 + v] = K / (double)t.q[c][u * 8 + v];
+            }
+}
+
+/* k_mxs's image head: the B operands, or (JX_MXS_BGLOBAL) the exact pass's tables */
+static void mxs_fill_head(MxsImgB &I, const uint16_t (*ops)[64][8], const jx_mxtab &)
+{
+    memcpy(I.B, ops, sizeof I.B);
+}
+static void mxs_fill_head(MxsImgX &I, const uint16_t (*)[64][8], const jx_mxtab &t)
+{
+    static const double cosx[8][8] = JX_COS_INIT;
+    static const double colour[3][5] = JX_MX_COLOUR_INIT;
+    memcpy(I.ex.cosx_, cosx, sizeof cosx);
+    memcpy(I.ex.colour_, colour, sizeof colour);
+    memcpy(I.ex.r_, t.r, sizeof t.r);
+}
+
 int mx_tables_for_current_device(int *waves)
 {
     int dev = 0;
@@ -3312,6 +3464,7 @@ int mx_tables_for_current_device(int *waves)
             for (int f = 0; f < 2; f++) {
                 jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
                 memcpy(t.q, qq, sizeof qq);
+                mx_fill_recip(t);
                 for (int n = 0; n < 24; n++)
                     for (int v = 0; v < 8; v++) {
                         t.w[n][v] = w[n][v] * kRScale;
@@ -3334,7 +3487,7 @@ int mx_tables_for_current_device(int *waves)
                 for (int q = 1; q <= JX_MAXQ; q++) {
                     MxsImg &I = img[f * (JX_MAXQ + 1) + q];
                     const jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
-                    memcpy(I.B, ops, sizeof I.B);
+                    mxs_fill_head(I, ops, t);
                     for (unsigned tt = 0; tt < 4; tt++)
                         for (unsigned jp = 0; jp < 16; jp++) {
                             const unsigned n = tt < 2 ? jp : 16u + (jp & 7u);
@@ -3402,6 +3555,7 @@ int mx422_tables_for_current_device(int *waves)
             for (int f = 0; f < 2; f++) {
                 jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
                 memcpy(t.q, qq, sizeof qq);
+                mx_fill_recip(t);
                 for (int n = 0; n < 24; n++)
                     for (int v = 0; v < 8; v++) {
                         t.w[n][v] = w[n][v] * kRScale;
@@ -3494,6 +3648,7 @@ int mx420_tables_for_current_device(int *waves)
             for (int f = 0; f < 2; f++) {
                 jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
                 memcpy(t.q, qq, sizeof qq);
+                mx_fill_recip(t);
                 for (int n = 0; n < 24; n++)
                     for (int v = 0; v < 8; v++) {
                         t.w[n][v] = w[n][v] * kRScale;

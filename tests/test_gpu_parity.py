@@ -253,3 +253,11 @@ def test_large_frames_hash(golden, cuda):
             # the 4:4:4 one (every sr1 golden above equals its sr0 hash)
             out = jpgx.encode_blocks(d, 75, sample_ratio=1, underflow=ent["underflow"]).cpu().numpy()
             assert coef_sha(out) == ent["coef_sha256"]["75"]
+
+
+@pytest.mark.parametrize("q", [10, 50, 75, 90])
+def test_force_exact_with_ties(cuda, q):
+    """FORCE_EXACT on a frame with flat tie blocks: batches of the exact pass mix coefficients the
+    fast decision settles with exact .5 ties that must take the sequential sum (mx_exact_sum)"""
+    rgb = _sparse_tie(256, 128, 11, 3)
+    assert np.array_equal(_gpu(rgb, q, cuda, flags=jpgx.FLAG_FORCE_EXACT), O.blocks(rgb, q))
