@@ -10,4 +10,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-me
 rc=$?; grep -E "passed|failed|FAILED|Error" "$OUT/gpu_tests.txt" | tail -8; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python tools/diag_rate.py ${RATE_N:-60} 0 1 2 > "$OUT/rate_product.txt" 2>&1 || exit $?
 grep -v amdgpu.ids "$OUT/rate_product.txt"
-ROUNDS=2 bash tools/gpu_r5_price.sh "$1" "r4 nox" r4 r4
+ROUNDS=2 bash tools/gpu_r5_price.sh "$1" "${KB444:-head nox}" ${KB422:-head} ${KB420:-head}
