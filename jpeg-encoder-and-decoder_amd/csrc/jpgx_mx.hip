@@ -418,6 +418,17 @@ __device__ __forceinline__ double mx_dpp64(double s)
  * the sequential sum -- wave-uniform, rare.
  * Valid in lane x == 7 (fast path: every lane).
  */
+/* The inline exact pass ends with every LDS operation retired (JX_MX_EXEND_LGKM).  Round 5
+ * (profiles/r05_exact_pass.txt): with the pass's tables in LDS -- no global read, hence no
+ * vmcnt / lgkmcnt(0) wait anywhere in it -- a later step's Cr tile came out wrong in rows 12..15
+ * in ~2 % of launches; an s_waitcnt vmcnt(0) at the pass's start did not help, lgkmcnt(0) at its
+ * end did (0 of 80 launches + 8 golden frames). */
+#ifndef JX_MX_EXSTART_VM
+#define JX_MX_EXSTART_VM 0              /* diagnostics: vmcnt(0) before the pass */
+#endif
+#ifndef JX_MX_EXEND_LGKM
+#define JX_MX_EXEND_LGKM 1
+#endif
 #ifndef JX_MX_FASTEXACT
 #define JX_MX_FASTEXACT 1
 #endif
@@ -450,8 +461,9 @@ __device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch
 }
 
 /* where the exact pass's constants come from: the __constant__ tables (MxExConst; k_mx, the
- * 4:2:x kernels) or a copy in the workgroup's LDS image (MxExTab; k_mxs: under full HBM load a
- * global read of a table costs the wave microseconds, round 5) */
+ * 4:2:x kernels) or the workgroup's LDS image and literals (MxExLds; k_mxs).  Round 5: a global
+ * read in the exact pass waits, through the in-order vmcnt, for every older VMEM operation of the
+ * wave -- the later steps' pixel DMA -- so it costs the wave microseconds under full HBM load. */
 struct MxExConst {
     const jx_mxtab &T;
     __device__ double cosx(unsigned k, unsigned i) const { return kMxCos[k][i]; }
@@ -461,16 +473,25 @@ struct MxExConst {
 };
 struct alignas(16) MxExTab {
     double cosx_[8][8];                 /* kMxCos                                    */
-    double colour_[3][5];               /* kMxColour                                 */
-    double pad_;
-    double r_[2][64];                   /* jx_mxtab.r of the workgroup's quality     */
+    int16_t q_[2][64];                  /* jx_mxtab.q of the workgroup's quality     */
 };
 struct MxExLds {
     const MxExTab &X;
     const uint8_t (&scan_t)[8][8];
     __device__ double cosx(unsigned k, unsigned i) const { return X.cosx_[k][i]; }
-    __device__ double colour(unsigned ch, unsigned i) const { return X.colour_[ch][i]; }
-    __device__ double recip(unsigned c, unsigned i) const { return X.r_[c][i]; }
+    /* kMxColour as literals (i is a compile-time constant at every use) */
+    __device__ double colour(unsigned ch, unsigned i) const
+    {
+        const double y[5] = {0.299, 0.587, 0.114, 0.0, 1.0}, b[5] = {0.168736, -0.331264, 0.5, 128.0, -1.0},
+                     r[5] = {0.5, -0.418688, -0.081312, 128.0, 1.0};
+        return ch == 0 ? y[i] : (ch == 1 ? b[i] : r[i]);
+    }
+    /* jx_mxtab.r: fl(fl((1/4 a(u)) a(v)) / Q), the same IEEE operations as the host's */
+    __device__ double recip(unsigned c, unsigned i) const
+    {
+        const double K = ((i >> 3) == 0 ? 0.25 * JX_ALPHA0 : 0.25) * ((i & 7u) == 0 ? JX_ALPHA0 : 1.0);
+        return K / (double)X.q_[c][i];
+    }
     __device__ unsigned scan(unsigned u, unsigned v) const { return scan_t[u][v]; }
 };
 
@@ -510,6 +531,9 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
                                                 const jx_mxtab &T, const XT &xt)
 {
     const unsigned lane = mx_lane();
+#if JX_MX_EXSTART_VM
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     mx_wave_sync();
     for (;;) {
         const uint64_t act = __ballot(bits != 0);
@@ -535,6 +559,9 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
                                                            2u * xt.scan(u, v)) = (int16_t)val;
         mx_wave_sync();
     }
+#if JX_MX_EXEND_LGKM
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
 }
 
 /* Deferred exact pass: up to kSide queued columns (pixels in L.pix), one per 8-lane group, each
@@ -700,6 +727,33 @@ __device__ __forceinline__ MxW mx_w(const MxsTabRef &tb, unsigned t0, unsigned j
 __device__ __forceinline__ MxW mx_l(const MxsTabRef &tb, unsigned t0, unsigned j)
 {
     return MxW{tb.g.wl[t0 + 1][0][j], tb.g.wl[t0 + 1][1][j]};
+}
+/* k_mxs's image table: MxTab with the Cr tables (2, 3) at 8 profiles -- a Cr column's profile is
+ * j % 8 (lanes j and j + 8 read the same entry: an LDS broadcast) -- which frees the 512 bytes
+ * per workgroup that the exact pass's tables take (MxExTab) */
+struct MxsTab {
+    mx_f4 yc[2][2][16];                 /* tables 0 (scales), 1 (squared limits): Y | Cb */
+    mx_f4 cr[2][2][8];                  /* tables 2, 3: Cr                              */
+};
+__device__ __forceinline__ MxW mx_w(const MxsTab &tb, unsigned t0, unsigned j)
+{
+    return t0 == 0 ? MxW{tb.yc[0][0][j], tb.yc[0][1][j]} : MxW{tb.cr[0][0][j & 7u], tb.cr[0][1][j & 7u]};
+}
+__device__ __forceinline__ MxW mx_l(const MxsTab &tb, unsigned t0, unsigned j)
+{
+    return t0 == 0 ? MxW{tb.yc[1][0][j], tb.yc[1][1][j]} : MxW{tb.cr[1][0][j & 7u], tb.cr[1][1][j & 7u]};
+}
+struct MxsTabRefC {
+    const MxsScales &s;
+    const MxsTab &g;
+};
+__device__ __forceinline__ MxW mx_w(const MxsTabRefC &tb, unsigned t0, unsigned j)
+{
+    return MxW{tb.s.w[t0 >> 1][0][j], tb.s.w[t0 >> 1][1][j]};
+}
+__device__ __forceinline__ MxW mx_l(const MxsTabRefC &tb, unsigned t0, unsigned j)
+{
+    return mx_l(tb.g, t0, j);
 }
 
 /*
@@ -1147,33 +1201,15 @@ static_assert(sizeof(MxsLds) % 16 == 0, "16-byte aligned LDS regions");
 #ifndef JX_MXS_BLDS
 #define JX_MXS_BLDS 0                   /* 1: B operands read from the LDS image every step (fewer VGPRs) */
 #endif
-/* Round-5 experiment (profiles/r05_exact_pass.txt): B operands from global memory (g_mxB) and the
- * exact pass's tables in the image instead.  The tables in LDS save ~3 us per launch, but every
- * build that loads B from global memory -- at the top of the wave, after the image barrier, with
- * or without a full drain before step 0 -- gives wrong C rows 12..15 (blocks 3 / 7 of a step,
- * mostly the chained Cr tile) in 10-100 % of launches, and tools/mfma_war_check.py finds no rule
- * violation in their ISA: not root-caused, so the product keeps B in the LDS image.  Diagnostics
- * only (NOT exact): JX_MXS_BGLOBAL=1, with JX_MXS_BLATE / JX_MXS_DRAIN0. */
-#ifndef JX_MXS_BLATE
-#define JX_MXS_BLATE 0
-#endif
-#ifndef JX_MXS_DRAIN0
-#define JX_MXS_DRAIN0 0
-#endif
-#ifndef JX_MXS_BGLOBAL
-#define JX_MXS_BGLOBAL 0
-#endif
-constexpr bool kMxsBGlobal = JX_MXS_BGLOBAL != 0;
-struct alignas(16) MxsImgB {
-    mx_u4 B[3 * JX_MX_PARTS][64];       /* B operands                                */
-};
-struct alignas(16) MxsImgX {
-    MxExTab ex;                         /* the exact pass's tables (B: g_mxB)        */
-};
-struct alignas(16) MxsImg : std::conditional<kMxsBGlobal, MxsImgX, MxsImgB>::type {
-    MxTab tab;
+/* Round-5 experiment (profiles/r05_exact_pass.txt, code removed): B operands from global memory
+ * (g_mxB) to make room for the exact tables gave wrong C rows 12..15 in 10-100 % of launches
+ * (not root-caused); the room comes from the compact Cr tables (MxsTab) instead. */
+struct alignas(16) MxsImg {
+    mx_u4 B[3 * JX_MX_PARTS][64];
+    MxsTab tab;
     float limc[2][16];
     uint8_t scan_t[8][8];               /* zig-zag position of (v, u) at [u][v] */
+    MxExTab ex;                         /* the exact pass's tables                      */
 };
 constexpr unsigned kMxsPieces = sizeof(MxsImg) / 16;
 static_assert(sizeof(MxsImg) % 16 == 0 && kMxsPieces <= 768, "three 16-byte pieces per thread");
@@ -1200,16 +1236,13 @@ __device__ MxsImg1 g_mxs_img1[2][JX_MAXQ + 1];
 using MxsShared = std::conditional<kMxsWPG == 1, MxsImg1, MxsImg>::type;
 /* where the B operands and the column tables come from (four-wave image / one-wave image) */
 typedef mx_u4 MxsBOps[3 * JX_MX_PARTS][64];
-__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImgB &l) { return l.B; }
-__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImgX &) { return g_mxB; }
-__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg &l, const MxsImg &) { return mxs_B(l); }
-[[maybe_unused]] __device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg1 &, const MxsImg &g) { return mxs_B(g); }
-/* the exact pass's tables: the LDS image's copy, or the __constant__ tables */
-__device__ __forceinline__ MxExLds mxs_xt(const MxsImgX &l, const uint8_t (&scan)[8][8], const jx_mxtab &) { return MxExLds{l.ex, scan}; }
-__device__ __forceinline__ MxExConst mxs_xt(const MxsImgB &, const uint8_t (&)[8][8], const jx_mxtab &T) { return MxExConst{T}; }
-[[maybe_unused]] __device__ __forceinline__ MxExConst mxs_xt(const MxsImg1 &, const uint8_t (&)[8][8], const jx_mxtab &T) { return MxExConst{T}; }
-__device__ __forceinline__ const MxTab &mxs_tb(const MxsImg &l, const MxsImg &) { return l.tab; }
-[[maybe_unused]] __device__ __forceinline__ MxsTabRef mxs_tb(const MxsImg1 &l, const MxsImg &g) { return MxsTabRef{l.sc, g.tab}; }
+__device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg &l, const MxsImg &) { return l.B; }
+[[maybe_unused]] __device__ __forceinline__ const MxsBOps &mxs_B(const MxsImg1 &, const MxsImg &g) { return g.B; }
+/* the exact pass's tables: the LDS image's copy (four-wave image), or the __constant__ tables */
+__device__ __forceinline__ MxExLds mxs_xt(const MxsImg &l, const jx_mxtab &) { return MxExLds{l.ex, l.scan_t}; }
+[[maybe_unused]] __device__ __forceinline__ MxExConst mxs_xt(const MxsImg1 &, const jx_mxtab &T) { return MxExConst{T}; }
+__device__ __forceinline__ const MxsTab &mxs_tb(const MxsImg &l, const MxsImg &) { return l.tab; }
+[[maybe_unused]] __device__ __forceinline__ MxsTabRefC mxs_tb(const MxsImg1 &l, const MxsImg &g) { return MxsTabRefC{l.sc, g.tab}; }
 #ifdef JX_MXS_STAMP                    /* timing probe builds only: per-wave timestamps */
 __device__ unsigned long long g_mxs_ts[1u << 20];
 #define JX_MXS_TS(i, v) do { if (lane == 0 && 8u * wv + 8u <= (1u << 20)) g_mxs_ts[8u * wv + (i)] = (v); } while (0)
@@ -1343,15 +1376,6 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
     const unsigned wave = kMxsWPG == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     MxsLds &L = s_lds[wave];
     const MxsImg &gimg = g_mxs_img[g.force ? 1 : 0][g.quality];
-    /* B operands from global memory (JX_MXS_BGLOBAL): issued before every DMA, so that waiting
-     * for them never waits for a pixel DMA */
-    mx_u4 B[kParts][3];
-    if constexpr (kMxsBGlobal && !JX_MXS_BLDS && !JX_MXS_BLATE) {
-#pragma unroll
-        for (int p = 0; p < kParts; p++)
-#pragma unroll
-            for (int w = 0; w < 3; w++) B[p][w] = g_mxB[3 * p + w][lane];
-    }
     /* the image into LDS (LDS-DMA: piece p of thread t lands at 16 p) */
     if constexpr (kMxsWPG >= 2) {
         const uint8_t *img = (const uint8_t *)&gimg;
@@ -1393,7 +1417,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
     const uint32_t rcb = (kMxsLean ? 8u : 12u) * kBS + ro;
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
     const jx_mxtab &T = g_mxtab[g.force ? 1 : 0][g.quality];
-    const auto xt = mxs_xt(s_img, s_img.scan_t, T);
+    const auto xt = mxs_xt(s_img, T);
 
     /* the image has landed (it is older than the prologue's pixel operations), in every wave */
     if constexpr (kMxsWPG == 1) {
@@ -1413,16 +1437,19 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
 #pragma unroll
         for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
     }
+#ifndef JX_MXS_UNCHAIN
+#define JX_MXS_UNCHAIN 1                /* 1: the Cr tile from independent products (no chained MFMA) */
+#endif
+constexpr bool kMxsUnchain = JX_MXS_UNCHAIN != 0 && kParts == 2;
 #ifndef JX_MXS_NOEXACT
 #define JX_MXS_NOEXACT 0                /* timing probes only: skip the inline exact pass (NOT exact) */
 #endif
 #if !JX_MXS_BLDS
-    if constexpr (!kMxsBGlobal || JX_MXS_BLATE) {
+    mx_u4 B[kParts][3];
 #pragma unroll
-        for (int p = 0; p < kParts; p++)
+    for (int p = 0; p < kParts; p++)
 #pragma unroll
-            for (int w = 0; w < 3; w++) B[p][w] = mxs_B(s_img, gimg)[3 * p + w][lane];
-    }
+        for (int w = 0; w < 3; w++) B[p][w] = mxs_B(s_img, gimg)[3 * p + w][lane];
 #endif
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
     const auto &tb = mxs_tb(s_img, gimg);
@@ -1490,19 +1517,53 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         __builtin_amdgcn_sched_barrier(0);
         mx_column_t<0>(acc[0], w0, limc0, tb, 0, j, za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
+        /* the Cr tile: the two sets' K halves.  Round 5 (kMxsUnchain): eight independent products
+         * and one VALU add per element, cr[0] + cr[1] -- bit-identical to the chained form, since in
+         * every column one of the two halves is an exact zero (B1 is zero in columns 8..15, B2 in
+         * 0..7) -- so no product of k_mxs waits in the matrix pipe for another;
+         * the products are issued in source order (cr[1][3] last: the fence) */
+        mx_f4 cr[2][4];
         const mx_f4 c0 = mx_mma(A00, B[0][1], z);
+        __builtin_amdgcn_sched_barrier(0);
         const mx_f4 c2 = mx_mma(A01, B[0][1], z);
+        __builtin_amdgcn_sched_barrier(0);
         const mx_f4 c1 = mx_mma(A00, B[1][1], z);
+        __builtin_amdgcn_sched_barrier(0);
         const mx_f4 c3 = mx_mma(A01, B[1][1], z);
-        acc[2][0] = mx_mma(A10, B[0][2], c0);
-        acc[2][2] = mx_mma(A11, B[0][2], c2);
-        acc[2][1] = mx_mma(A10, B[1][2], c1);
-        acc[2][3] = mx_mma(A11, B[1][2], c3);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (kMxsUnchain) {
+            cr[0][0] = c0;
+            cr[0][1] = c1;
+            cr[0][2] = c2;
+            cr[0][3] = c3;
+            cr[1][0] = mx_mma(A10, B[0][2], z);
+            __builtin_amdgcn_sched_barrier(0);
+            cr[1][2] = mx_mma(A11, B[0][2], z);
+            __builtin_amdgcn_sched_barrier(0);
+            cr[1][1] = mx_mma(A10, B[1][2], z);
+            __builtin_amdgcn_sched_barrier(0);
+            cr[1][3] = mx_mma(A11, B[1][2], z);
+        } else {
+            acc[2][0] = mx_mma(A10, B[0][2], c0);
+            acc[2][2] = mx_mma(A11, B[0][2], c2);
+            acc[2][1] = mx_mma(A10, B[1][2], c1);
+            acc[2][3] = mx_mma(A11, B[1][2], c3);
+            cr[1][3] = acc[2][3];
+        }
         mx_gap();
         const auto keepc = [&]() __attribute__((always_inline)) {
-            const mx_f4 cc[4] = {c0, c1, c2, c3};
-            mx_keep(cc);
-            mx_keep_ops(A00, A01, A10, A11, B[0][1], B[1][1], B[0][2], B[1][2]);
+            if constexpr (!kMxsUnchain) {
+                const mx_f4 cc[4] = {c0, c1, c2, c3};
+                mx_keep(cc);
+                mx_keep_ops(A00, A01, A10, A11, B[0][1], B[1][1], B[0][2], B[1][2]);
+            }
+        };
+        /* the Cr tile (unchained: its two halves' sum, every Cr product done after it) */
+        const auto cr_tile = [&]() __attribute__((always_inline)) {
+            if constexpr (kMxsUnchain) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) acc[2][i] = cr[0][i] + cr[1][i];
+            }
         };
         if (kParts == 3) {
             acc[2][1] = mx_mma(A00, B[kParts - 1][1], acc[2][1]);
@@ -1511,7 +1572,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
             acc[2][3] = mx_mma(A11, B[kParts - 1][2], acc[2][3]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<4 * kBS>(acc[1], w0, limc0, tb, 0, j, za, fl, 1, &acc[2][3]);
+        mx_column_t<4 * kBS>(acc[1], w0, limc0, tb, 0, j, za, fl, 1, &cr[1][3]);
         __builtin_amdgcn_sched_barrier(0);
         const uint8_t *const ob = (const uint8_t *)S.dst;
         /* the launch's last step: flags of its clamped copies are dropped (never stored) */
@@ -1535,8 +1596,9 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         };
         if constexpr (kMxsLean) {
             /* Y and Cb leave before the Cr column, which then takes their set-0 slots */
-            mx_fence(acc[2][3]);                       /* the Cr products are done (operand rule) */
+            mx_fence(cr[1][3]);                        /* the Cr products are done (operand rule) */
             keepc();
+            cr_tile();
             mx_wave_sync();
             if (__builtin_expect(__ballot((fl & 0xffffu) != 0) != 0, 0)) {
                 uint32_t f2 = fl & 0xffffu;
@@ -1571,7 +1633,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         }
         const bool early = S.simple && __ballot((fl & 0xffffu) != 0) == 0;
         if (early) {
-            mx_fence(acc[2][3]);                       /* the Cr products are done (operand rule) */
+            mx_fence(cr[1][3]);                        /* the Cr products are done (operand rule) */
             keepc();
             mx_wave_sync();
             const mx_u4 v0 = *(const mx_u4 *)(L.stage + ro);
@@ -1580,6 +1642,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
             __builtin_nontemporal_store(v1, (mx_u4 *)(ob + so1));
         }
         __builtin_amdgcn_sched_barrier(0);
+        cr_tile();
         mx_column_t<8 * kBS, true>(acc[2], w0, limc2, tb, 2, j, za, fl, 2);
         keepc();
         mx_wave_sync();
@@ -1612,10 +1675,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, JX_MX_WPE) void k_mxs(const jx_xform_
         const auto step = [&](auto kc) __attribute__((always_inline)) {
             constexpr unsigned k = decltype(kc)::value < kMxsR ? decltype(kc)::value : kMxsR - 1;
             if (cmp.b >= g.total) return;
-            if (JX_MXS_DRAIN0 && k == 0)
-                mx_wait_vm<0>();
-            else
-                mx_wait_vm<2 * (kMxsR - 1 - k) + 3 * k>();
+            mx_wait_vm<2 * (kMxsR - 1 - k) + 3 * k>();
             body(cmp, L.ring[k]);
             mxs_next(cmp, g);
         };
@@ -3435,20 +3495,6 @@ static void mx_fill_recip(jx_mxtab &t)
             }
 }
 
-/* k_mxs's image head: the B operands, or (JX_MXS_BGLOBAL) the exact pass's tables */
-static void mxs_fill_head(MxsImgB &I, const uint16_t (*ops)[64][8], const jx_mxtab &)
-{
-    memcpy(I.B, ops, sizeof I.B);
-}
-static void mxs_fill_head(MxsImgX &I, const uint16_t (*)[64][8], const jx_mxtab &t)
-{
-    static const double cosx[8][8] = JX_COS_INIT;
-    static const double colour[3][5] = JX_MX_COLOUR_INIT;
-    memcpy(I.ex.cosx_, cosx, sizeof cosx);
-    memcpy(I.ex.colour_, colour, sizeof colour);
-    memcpy(I.ex.r_, t.r, sizeof t.r);
-}
-
 int mx_tables_for_current_device(int *waves)
 {
     int dev = 0;
@@ -3487,7 +3533,11 @@ int mx_tables_for_current_device(int *waves)
                 for (int q = 1; q <= JX_MAXQ; q++) {
                     MxsImg &I = img[f * (JX_MAXQ + 1) + q];
                     const jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
-                    mxs_fill_head(I, ops, t);
+                    memcpy(I.B, ops, sizeof I.B);
+                    static const double cosx[8][8] = JX_COS_INIT;
+                    memcpy(I.ex.cosx_, cosx, sizeof cosx);
+                    memcpy(I.ex.q_, t.q, sizeof t.q);
+                    MxTab full;                            /* k_mx's layout; compacted below */
                     for (unsigned tt = 0; tt < 4; tt++)
                         for (unsigned jp = 0; jp < 16; jp++) {
                             const unsigned n = tt < 2 ? jp : 16u + (jp & 7u);
@@ -3497,12 +3547,17 @@ int mx_tables_for_current_device(int *waves)
                                     const int v = jx_pk_k(pp, h);
                                     x[2 * pp + h] = (tt & 1u) ? t.lsq[n][v] : t.w[n][v];
                                 }
-                            I.tab.wl[tt][0][jp] = mx_f4{x[0], x[1], x[2], x[3]};
-                            I.tab.wl[tt][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
+                            full.wl[tt][0][jp] = mx_f4{x[0], x[1], x[2], x[3]};
+                            full.wl[tt][1][jp] = mx_f4{x[4], x[5], x[6], x[7]};
                         }
                     for (unsigned jp = 0; jp < 16; jp++) {
-                        I.limc[0][jp] = mx_limc(I.tab, 1, jp);
-                        I.limc[1][jp] = mx_limc(I.tab, 3, jp);
+                        I.limc[0][jp] = mx_limc(full, 1, jp);
+                        I.limc[1][jp] = mx_limc(full, 3, jp);
+                        for (int tt = 0; tt < 2; tt++)
+                            for (int h = 0; h < 2; h++) {
+                                I.tab.yc[tt][h][jp] = full.wl[tt][h][jp];
+                                if (jp < 8) I.tab.cr[tt][h][jp] = full.wl[2 + tt][h][jp];
+                            }
                     }
                     static const int scan[8][8] = JX_SCAN_ORDER_INIT;
                     for (int uu = 0; uu < 8; uu++)
@@ -3514,8 +3569,8 @@ int mx_tables_for_current_device(int *waves)
             for (size_t i = 0; i < img.size(); i++) {
                 for (int h = 0; h < 2; h++)
                     for (int jp = 0; jp < 16; jp++) {
-                        img1[i].sc.w[0][h][jp] = img[i].tab.wl[0][h][jp];
-                        img1[i].sc.w[1][h][jp] = img[i].tab.wl[2][h][jp];
+                        img1[i].sc.w[0][h][jp] = img[i].tab.yc[0][h][jp];
+                        img1[i].sc.w[1][h][jp] = img[i].tab.cr[0][h][jp & 7];
                     }
                 memcpy(img1[i].limc, img[i].limc, sizeof img1[i].limc);
                 memcpy(img1[i].scan_t, img[i].scan_t, sizeof img1[i].scan_t);
