@@ -4,7 +4,7 @@
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
-OUT="$ROOT/gpurun_out/r4sub"; mkdir -p "$OUT"
+OUT="$ROOT/gpurun_out/${1:-r4sub}"; mkdir -p "$OUT"
 cd /tmp
 for sr in 1 2; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats$sr" -o run -- python "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --subsample --sample-ratio $sr --quality 75 > "$OUT/bench$sr.json" 2> "$OUT/bench$sr.err" || exit $?
