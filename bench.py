@@ -6,7 +6,7 @@ Workload (BASELINE.json metric "Mpixels/sec RGB->quantised-coeff, 4K 4:4:4 q=90"
   frames_per_gpu * N synthetic 3840x2160 RGB frames (4:4:4, q=90) -- configs[3]'s
   "batch of 64 x 4K frames, row-stripe sharded across 8 GPUs" at N=8, weak scaling.
   Frames are generated on the device (splitmix64) before timing; a step is one
-  jpgx_blocks_gpu() call over all frames of the stripe (one k_mx launch, whose in-kernel
+  jpgx_blocks_gpu() call over all frames of the stripe (one k_mxs launch, whose in-kernel
   exact path recomputes the guard-band coefficients).
   8 frames per GPU = 597 MB moved per step, more than the 256 MiB Infinity Cache.
 
@@ -238,7 +238,7 @@ def sub_kernel_name(sr):
 
 def mx_kernel_name(sr):
     """The MFMA kernel this library's launch runs for sample ratio sr (0 = 4:4:4): k_mxs /
-    k_mxs422 / k_mxs420 (short-lived waves), or the persistent k_mx* of a variant build."""
+    k_mxs422 / k_mxs420 (short-lived waves)."""
     import ctypes
 
     import jpgx
@@ -290,7 +290,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel", choices=["xform", "mx"], default=None,
-                    help="4:4:4 transform kernel: k_mx (the product: colour and row DCT on the "
+                    help="4:4:4 transform kernel: k_mxs (the product: colour and row DCT on the "
                          "matrix cores) or k_xform (all-VALU, from the test-only cross-check "
                          "library lib/libjpgx_alt.so), DESIGN.md 4")
     ap.add_argument("--subsample", action="store_true",

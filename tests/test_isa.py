@@ -19,7 +19,7 @@ def test_mfma_operand_rule(tmp_path):
                     "-fno-slp-vectorize", "-I" + os.path.join(REPO, "include"), "--cuda-device-only", "-S",
                     os.path.join(PKG, "csrc", "jpgx_mx.hip"), "-o", str(asm)],
                    check=True, capture_output=True)
-    names = ["k_mx", "k_mxs", "k_mx422", "k_mxs422", "k_mx420", "k_mxs420"]
+    names = ["k_mxs", "k_mxs422", "k_mxs420"]     # every __global__ MFMA kernel of the product
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), str(asm)] + names,
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout

@@ -1,0 +1,185 @@
+/*
+ * pk_hazard5.hip -- round-6 probe: WHICH packed-fp32 form goes wrong in lanes 48..63 after the same
+ * wave's MFMAs (pk_hazard4.hip: the packed DCT does, in 1.7e-4 of its runs; never without MFMAs in
+ * the wave).  Each wave, per iteration: eight v_mfma_f32_16x16x32_f16 products into AGPR/VGPR
+ * accumulators, per-lane pseudo-random inputs made by integer hashing (as pk_hazard4), then ONE
+ * inline-asm packed instruction of the form under test on a register pair whose halves the compiler
+ * has just written, compared with the scalar result.  Forms (MODE):
+ *   0 v_pk_add_f32 d, a, b                       1 v_pk_add_f32 with op_sel:[0,1] op_sel_hi:[1,0]
+ *   2 v_pk_fma_f32 d, a, s[k:k+1], b             3 v_pk_mul_f32 d, a, b
+ *   4 v_pk_add_f32 with s_nop 7 x 4 before it     5 v_pk_fma_f32 d, a, b, c (all VGPR)
+ *   6 v_pk_mov_b32 d, a, b op_sel:[1,0] (swap)    7 two v_add_f32 (scalar control)
+ *  (set 1) 1 without MFMA; 10 swap src0; 11 / 12 src0 hi / lo broadcast; 13 src1 lo broadcast;
+ *   14 swap src1 after 32 wait states; 15 v_pk_fma src2 lo broadcast; 16 the column pass's
+ *   v_pk_fma (src0 hi broadcast, SGPR pair, src2 lo broadcast); 17 swap src1 whose pair was written
+ *   an iteration earlier; 1 again
+ * Usage: ./pk_hazard5 [blocks] [iters] [set 0 | 1]
+ * Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -o tools/probes/pk_hazard5 tools/probes/pk_hazard5.hip
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                        \
+            exit(1);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+__device__ __forceinline__ uint32_t hash(uint32_t x)
+{
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    return x ^ (x >> 16);
+}
+
+template <int MODE, bool MFMA = true>
+__global__ __launch_bounds__(256) void k_form(unsigned *bad, int iters, float kx, float ky)
+{
+    const unsigned gid = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63u;
+    h8 a0, a1, b0, b1;
+    for (int i = 0; i < 8; i++) {
+        a0[i] = (_Float16)(float)((hash(gid * 8 + i) & 255u) * (1.0f / 64.0f) - 2.0f);
+        a1[i] = (_Float16)(float)((hash(gid * 8 + i + 99) & 255u) * (1.0f / 64.0f) - 2.0f);
+        b0[i] = (_Float16)(float)((hash(lane * 8 + i + 7) & 255u) * (1.0f / 64.0f) - 2.0f);
+        b1[i] = (_Float16)(float)((hash(lane * 8 + i + 77) & 255u) * (1.0f / 64.0f) - 2.0f);
+    }
+    unsigned nbad = 0;
+    uint32_t keep = 0, seed = gid * 0x9E3779B9u;
+    const f2 K = {kx, ky};                       /* wave-uniform: an SGPR pair */
+    f2 Bold = {1.5f, -2.5f};
+    for (int it = 0; it < iters; it++) {
+        f4 cr[8] = {};
+        if (MFMA) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                cr[k] = __builtin_amdgcn_mfma_f32_16x16x32_f16((k & 1) ? a1 : a0, (k & 2) ? b1 : b0, f4{}, 0, 0, 0);
+                a0[k] = (_Float16)((float)a0[k] + 0.0625f);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        float in[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            seed = hash(seed + (uint32_t)k);
+            in[k] = (float)(int)(seed & 0xffffu) * (1.0f / 4096.0f) - 8.0f;
+        }
+        f2 A = {in[0], in[1]}, B = {in[2], in[3]}, C = {in[4], in[5]}, D;
+        if (MODE == 17 && it == 0) Bold = B;
+        float wx, wy;
+        if (MODE == 0) {
+            asm volatile("v_pk_add_f32 %0, %1, %2" : "=v"(D) : "v"(A), "v"(B));
+            wx = A.x + B.x, wy = A.y + B.y;
+        } else if (MODE == 1) {
+            asm volatile("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(D) : "v"(A), "v"(B));
+            wx = A.x + B.y, wy = A.y + B.x;
+        } else if (MODE == 2) {
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(D) : "v"(A), "s"(K), "v"(B));
+            wx = __builtin_fmaf(A.x, K.x, B.x), wy = __builtin_fmaf(A.y, K.y, B.y);
+        } else if (MODE == 3) {
+            asm volatile("v_pk_mul_f32 %0, %1, %2" : "=v"(D) : "v"(A), "v"(B));
+            wx = A.x * B.x, wy = A.y * B.y;
+        } else if (MODE == 4) {
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\tv_pk_add_f32 %0, %1, %2" : "=v"(D) : "v"(A), "v"(B));
+            wx = A.x + B.x, wy = A.y + B.y;
+        } else if (MODE == 5) {
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(D) : "v"(A), "v"(B), "v"(C));
+            wx = __builtin_fmaf(A.x, B.x, C.x), wy = __builtin_fmaf(A.y, B.y, C.y);
+        } else if (MODE == 6) {
+            asm volatile("v_pk_mov_b32 %0, %1, %2 op_sel:[1,0]" : "=v"(D) : "v"(A), "v"(B));
+            wx = A.y, wy = B.x;
+        } else if (MODE == 7) {
+            float dx, dy;
+            asm volatile("v_add_f32 %0, %2, %3\n\tv_add_f32 %1, %4, %5" : "=&v"(dx), "=&v"(dy)
+                         : "v"(A.x), "v"(B.x), "v"(A.y), "v"(B.y));
+            D = f2{dx, dy};
+            wx = A.x + B.x, wy = A.y + B.y;
+        } else if (MODE == 10) {                 /* swap src0 */
+            asm volatile("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(D) : "v"(A), "v"(B));
+            wx = A.y + B.x, wy = A.x + B.y;
+        } else if (MODE == 11) {                 /* src0 hi broadcast */
+            asm volatile("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(D) : "v"(A), "v"(B));
+            wx = A.y + B.x, wy = A.y + B.y;
+        } else if (MODE == 12) {                 /* src0 lo broadcast */
+            asm volatile("v_pk_add_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(D) : "v"(A), "v"(B));
+            wx = A.x + B.x, wy = A.x + B.y;
+        } else if (MODE == 13) {                 /* src1 lo broadcast */
+            asm volatile("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(D) : "v"(A), "v"(B));
+            wx = A.x + B.x, wy = A.y + B.x;
+        } else if (MODE == 14) {                 /* swap src1, 32 wait states before */
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\tv_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]"
+                         : "=v"(D) : "v"(A), "v"(B));
+            wx = A.x + B.y, wy = A.y + B.x;
+        } else if (MODE == 15) {                 /* fma, src2 lo broadcast */
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,1,0]" : "=v"(D) : "v"(A), "v"(B), "v"(C));
+            wx = __builtin_fmaf(A.x, B.x, C.x), wy = __builtin_fmaf(A.y, B.y, C.x);
+        } else if (MODE == 16) {                 /* the column pass's form: src0 hi broadcast, SGPR, src2 lo broadcast */
+            asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,0]" : "=v"(D) : "v"(A), "s"(K), "v"(C));
+            wx = __builtin_fmaf(A.y, K.x, C.x), wy = __builtin_fmaf(A.y, K.y, C.x);
+        } else {                                 /* 17: swap src1, both halves of B old (written one iteration early) */
+            asm volatile("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(D) : "v"(A), "v"(Bold));
+            wx = A.x + Bold.y, wy = A.y + Bold.x;
+        }
+        asm volatile("s_nop 1" ::: "memory");
+        const bool ok = __float_as_uint(D.x) == __float_as_uint(wx) && __float_as_uint(D.y) == __float_as_uint(wy);
+        nbad += ok ? 0u : 1u;
+        for (int k = 0; k < 8; k++) keep += __float_as_uint(cr[k].w);
+        if (MODE == 17) Bold = f2{Bold.y * 0.5f + in[0], Bold.x * 0.25f - in[1]};
+    }
+    if (nbad) atomicAdd(&bad[lane >> 4], nbad);
+    if (keep == 0x12345678u) bad[9] = 1u;
+}
+
+template <int MODE, bool MFMA = true>
+static void run(unsigned *d_bad, int blocks, int iters)
+{
+    CK(hipMemset(d_bad, 0, 16 * sizeof(unsigned)));
+    hipLaunchKernelGGL((k_form<MODE, MFMA>), dim3(blocks), dim3(256), 0, 0, d_bad, iters, 1.25f, -0.75f);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    unsigned h[16];
+    CK(hipMemcpy(h, d_bad, sizeof h, hipMemcpyDeviceToHost));
+    printf("form %d%s: wrong results per lane group [0-15, 16-31, 32-47, 48-63]: %u %u %u %u of %.0f\n", MODE, MFMA ? "" : " (no MFMA)", h[0],
+           h[1], h[2], h[3], (double)blocks * 256.0 * iters);
+    fflush(stdout);
+}
+
+int main(int argc, char **argv)
+{
+    const int blocks = argc > 1 ? atoi(argv[1]) : 8192, iters = argc > 2 ? atoi(argv[2]) : 400;
+    unsigned *d_bad;
+    CK(hipMalloc(&d_bad, 16 * sizeof(unsigned)));
+    const int which = argc > 3 ? atoi(argv[3]) : 0;
+    if (which == 0) {
+        run<0>(d_bad, blocks, iters);
+        run<1>(d_bad, blocks, iters);
+        run<2>(d_bad, blocks, iters);
+        run<3>(d_bad, blocks, iters);
+        run<4>(d_bad, blocks, iters);
+        run<5>(d_bad, blocks, iters);
+        run<6>(d_bad, blocks, iters);
+        run<7>(d_bad, blocks, iters);
+    } else {
+        run<1, false>(d_bad, blocks, iters);
+        run<10>(d_bad, blocks, iters);
+        run<11>(d_bad, blocks, iters);
+        run<12>(d_bad, blocks, iters);
+        run<13>(d_bad, blocks, iters);
+        run<14>(d_bad, blocks, iters);
+        run<15>(d_bad, blocks, iters);
+        run<16>(d_bad, blocks, iters);
+        run<17>(d_bad, blocks, iters);
+        run<1>(d_bad, blocks, iters);
+    }
+    return 0;
+}
