@@ -1,7 +1,7 @@
 /*
  * jpgx_mx.hip -- the gfx950 block-transform kernels of libjpgx.so: colour conversion and the row
  * DCT on the matrix cores (v_mfma_f32_16x16x32_f16), the column DCT, quantiser, guard band and
- * zig-zag in packed fp32 VALU (v_pk_*_f32), and the exact-order fp64 pass for guard-band
+ * zig-zag in scalar fp32 VALU, and the exact-order fp64 pass for guard-band
  * coefficients inline, from the pixels already in LDS.
  *
  *   k_mxs     4:4:4 / reference-parity output (sample ratio 0, and 1 / 2 without
@@ -28,10 +28,10 @@
  *           j/8's Cr at u = j%8.  B = Bh + Bl (two f16 parts); acc_h = A Bh is EXACT in any
  *           summation order (jpgx_plan.cpp); R = acc_h + acc_l (Bl encoded at Bh's scale).
  *   Columns every lane then holds three whole columns (8 rows, registers 0..3 of the two
- *           halves): (set 0, c = j/8, u), (set 1, same), (Cr, set j/8, u).  Each runs jx_fdct8_pk
- *           (lane by lane the FOps code the band is derived for), the quantiser tm = F w +
- *           1.5 2^23 (low 16 bits = the rounded int16) per v_pk_fma pair, the int16 to the LDS
- *           stage at its zig-zag position, and the band test d^2 - lsq >= 0 (d = F w - rint,
+ *           halves): (set 0, c = j/8, u), (set 1, same), (Cr, set j/8, u).  Each runs jx_fdct8
+ *           in scalar fp32 (the FOps code the band is derived for; no packed-fp32 instruction in
+ *           these kernels, mx_unpack8), the quantiser tm = F w + 1.5 2^23 (low 16 bits = the
+ *           rounded int16), the int16 to the LDS stage at its zig-zag position, and the band test d^2 - lsq >= 0 (d = F w - rint,
  *           exact) folded into a running max.
  *   Exact   (rare) a column whose max says "some coefficient in the band" records its flagged
  *           v's; the step recomputes them from the pixels still in its LDS slot into the stage
@@ -66,7 +66,6 @@ namespace {
 typedef _Float16 mx_h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 mx_h2 __attribute__((ext_vector_type(2)));
 typedef float mx_f4 __attribute__((ext_vector_type(4)));
-typedef float mx_f2 __attribute__((ext_vector_type(2)));
 typedef uint32_t mx_u4 __attribute__((ext_vector_type(4)));
 typedef uint32_t mx_u2 __attribute__((ext_vector_type(2)));
 
@@ -94,17 +93,9 @@ struct MxTab {
 };
 
 __device__ jx_mxtab g_mxtab[2][JX_MAXQ + 1];     /* [force][quality]                        */
-__constant__ double kMxCos[8][8] = JX_COS_INIT;
-__constant__ int kMxScan[8][8] = JX_SCAN_ORDER_INIT;
 /* ((0.25 a(u)) a(v)) of dct.c:54, 0.25 a(u) exact in a double */
 __constant__ double kMxQuarterAlpha[8] = {0.25 * JX_ALPHA0, 0.25, 0.25, 0.25, 0.25, 0.25, 0.25, 0.25};
 __constant__ double kMxAlpha[8] = {JX_ALPHA0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0};
-/* per channel the reference's colour constants as the exact pass uses them: t = (k0 r + k1 g)
- * + k2 b (the signs of its subtractions folded into k1, k2: a - b*k == a + b*(-k) exactly),
- * then (A + S t) - 128 with (A, S) = (0, 1) Y, (128, -1) Cb, (128, 1) Cr */
-#define JX_MX_COLOUR_INIT                                                                          \
-    {{0.299, 0.587, 0.114, 0.0, 1.0}, {0.168736, -0.331264, 0.5, 128.0, -1.0}, {0.5, -0.418688, -0.081312, 128.0, 1.0}}
-__constant__ double kMxColour[3][5] = JX_MX_COLOUR_INIT;
 
 /* Keep the compiler from moving this wave's LDS accesses across this point (a wave's LDS
  * instructions execute in program order; no fence: that would drain the memory counters). */
@@ -151,18 +142,6 @@ __device__ __forceinline__ mx_f4 mx_mma(mx_h8 a, mx_u4 b, mx_f4 c)
 {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, __builtin_bit_cast(mx_h8, b), c, 0, 0, 0);
 }
-
-/* v_pk_*_f32 pairs for jx_fdct8_pk (lane by lane the scalar FOps operations) */
-struct MxPair {
-    typedef mx_f2 V;
-    static __device__ __forceinline__ V mk(float a, float b) { return V{a, b}; }
-    static __device__ __forceinline__ float lo(V a) { return a.x; }
-    static __device__ __forceinline__ float hi(V a) { return a.y; }
-    static __device__ __forceinline__ V add(V a, V b) { return a + b; }
-    static __device__ __forceinline__ V sub(V a, V b) { return a - b; }
-    static __device__ __forceinline__ V mul(V a, V b) { return a * b; }
-    static __device__ __forceinline__ V fma(V a, V b, V c) { return __builtin_elementwise_fma(a, b, c); }
-};
 
 /* The launch geometry as plain values */
 struct MxG {
@@ -330,26 +309,22 @@ __device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch
     return (int)round(F / (double)q);
 }
 
-/* where the exact pass's constants come from: the __constant__ tables (MxExConst; the 4:2:x
- * kernels) or the workgroup's LDS image and literals (MxExLds; k_mxs).  Round 5: a global
- * read in the exact pass waits, through the in-order vmcnt, for every older VMEM operation of the
- * wave -- the later steps' pixel DMA -- so it costs the wave microseconds under full HBM load. */
-struct MxExConst {
-    const jx_mxtab &T;
-    __device__ double cosx(unsigned k, unsigned i) const { return kMxCos[k][i]; }
-    __device__ double colour(unsigned ch, unsigned i) const { return kMxColour[ch][i]; }
-    __device__ double recip(unsigned c, unsigned i) const { return T.r[c][i]; }
-    __device__ unsigned scan(unsigned u, unsigned v) const { return (unsigned)kMxScan[v][u]; }
-};
+/* where the exact pass's constants come from: the workgroup's LDS image and literals (MxExLds;
+ * every kernel since round 6).  Round 5: a global read in the exact pass waits, through the
+ * in-order vmcnt, for every older VMEM operation of the wave -- the later steps' pixel DMA -- so it
+ * costs the wave microseconds under full HBM load. */
 struct alignas(16) MxExTab {
-    double cosx_[8][8];                 /* kMxCos                                    */
+    double cosx_[8][8];                 /* the glibc cosines (JX_COS_INIT, jx_consts.h)  */
     int16_t q_[2][64];                  /* jx_mxtab.q of the workgroup's quality     */
 };
 struct MxExLds {
     const MxExTab &X;
     const uint8_t (&scan_t)[8][8];
     __device__ double cosx(unsigned k, unsigned i) const { return X.cosx_[k][i]; }
-    /* kMxColour as literals (i is a compile-time constant at every use) */
+    /* per channel the reference's colour constants, as literals (i is a compile-time constant at
+     * every use): t = (k0 r + k1 g) + k2 b (the signs of its subtractions folded into k1, k2:
+     * a - b*k == a + b*(-k) exactly), then (A + S t) - 128 with (A, S) = (0, 1) Y, (128, -1) Cb,
+     * (128, 1) Cr */
     __device__ double colour(unsigned ch, unsigned i) const
     {
         const double y[5] = {0.299, 0.587, 0.114, 0.0, 1.0}, b[5] = {0.168736, -0.331264, 0.5, 128.0, -1.0},
@@ -365,26 +340,144 @@ struct MxExLds {
     __device__ unsigned scan(unsigned u, unsigned v) const { return scan_t[u][v]; }
 };
 
-template <class XT>
-__device__ __forceinline__ int mx_exact_coef(const lds_u8 *px, unsigned rs, unsigned ch, unsigned u,
-                                             unsigned v, unsigned x, const jx_mxtab &T, const XT &xt)
+/* the level-shifted channel ch of the pixel at p, in the reference's double colour arithmetic and
+ * operation order (preprocess.c:160-162,186-188): (A + S ((k0 r + k1 g) + k2 b)) - 128 */
+template <class P, class XT>
+__device__ __forceinline__ double mx_ls(const P *p, unsigned ch, const XT &xt)
+{
+    const double t = (xt.colour(ch, 0) * (double)p[0] + xt.colour(ch, 1) * (double)p[1]) +
+                     xt.colour(ch, 2) * (double)p[2];
+    return (xt.colour(ch, 3) + xt.colour(ch, 4) * t) - 128.0;
+}
+
+/* The exact pass's samples X(x, y) of one block-channel (functors over the pixels):
+ *   MxSmp1  4:4:4 and every Y block: the pixel (x, y), rows rs bytes apart;
+ *   MxSmp2  4:2:2 chroma: (ls(2x, y) + ls(2x + 1, y)) 0.5 (oracle/cpu_ref.c cpuref_chroma_sample);
+ *           the right half (x >= 4) from its own base -- a row-last MCU's true rows (L.qtrue);
+ *   MxSmp4  4:2:0 chroma: ((ls(2x, 2y) + ls(2x+1, 2y)) + (ls(2x, 2y+1) + ls(2x+1, 2y+1))) 0.25,
+ *           pixel rows rs bytes apart (LDS slots, or global memory for a general pair). */
+struct MxSmp1 {
+    const lds_u8 *p0;
+    unsigned rs;
+    template <class XT>
+    __device__ double operator()(unsigned x, unsigned y, unsigned ch, const XT &xt) const
+    {
+        return mx_ls(p0 + rs * y + 3u * x, ch, xt);
+    }
+};
+struct MxSmp2 {
+    const lds_u8 *pl, *pr;
+    unsigned rl, rr;
+    template <class XT>
+    __device__ double operator()(unsigned x, unsigned y, unsigned ch, const XT &xt) const
+    {
+        const lds_u8 *p = x >= 4 ? pr + rr * y + 6u * (x - 4u) : pl + rl * y + 6u * x;
+        return (mx_ls(p, ch, xt) + mx_ls(p + 3, ch, xt)) * 0.5;
+    }
+};
+template <class P, class S>
+struct MxSmp4 {
+    const P *p0;
+    S rs;
+    template <class XT>
+    __device__ double operator()(unsigned x, unsigned y, unsigned ch, const XT &xt) const
+    {
+        const P *p = p0 + (S)(2u * y) * rs + 6u * x, *q = p + rs;
+        return ((mx_ls(p, ch, xt) + mx_ls(p + 3, ch, xt)) + (mx_ls(q, ch, xt) + mx_ls(q + 3, ch, xt))) * 0.25;
+    }
+};
+
+/* one exact coefficient per 8-lane group (lane 8 i + x): lane x forms the products
+ * (X(x, y) c_u[x]) c_v[y] (dct.c:48-50), mx_exact_sum sums them and rounds.  Valid in lane x == 7. */
+template <bool FAST, class SMP, class XT>
+__device__ __forceinline__ int mx_exact_coef(const SMP &smp, unsigned ch, unsigned u, unsigned v, unsigned x,
+                                             const jx_mxtab &T, const XT &xt)
 {
     const double cu = xt.cosx(u, x);
-    const double k0c = xt.colour(ch, 0), k1c = xt.colour(ch, 1), k2c = xt.colour(ch, 2);
-    const double Ac = xt.colour(ch, 3), Sc = xt.colour(ch, 4);
     double prod[8];
 #pragma unroll
-    for (int y = 0; y < 8; y++) {
-        const lds_u8 *p = px + rs * (unsigned)y + 3u * x;
-        const double rr = (double)p[0], gv = (double)p[1], bv = (double)p[2];
-        const double tt = (k0c * rr + k1c * gv) + k2c * bv;
-        const double X = (Ac + Sc * tt) - 128.0;
-        prod[y] = X * cu * xt.cosx(v, y);
-    }
-    return mx_exact_sum(prod, ch, u, v, x, T, xt.recip(ch == 0 ? 0 : 1, u * 8 + v));
+    for (int y = 0; y < 8; y++) prod[y] = smp(x, (unsigned)y, ch, xt) * cu * xt.cosx(v, y);
+    return mx_exact_sum<FAST>(prod, ch, u, v, x, T, xt.recip(ch == 0 ? 0 : 1, u * 8 + v));
 }
 
 __device__ __forceinline__ lds_u8 *mx_lds(void *p) { return (lds_u8 *)p; }
+
+/* s of the lane in the other 16-lane row of the pair (W = 16) or the other 32-lane half (W = 32),
+ * added to s: v_permlane16_swap / v_permlane32_swap with both operands s give one register with
+ * the even rows' values and one with the odd rows' (or the halves'), summed in the same order in
+ * every lane */
+template <int W>
+__device__ __forceinline__ double mx_xsum64(double s)
+{
+    const uint64_t b = __builtin_bit_cast(uint64_t, s);
+    const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+    if constexpr (W == 16) {
+        const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        return __builtin_bit_cast(double, (uint64_t)l[0] | ((uint64_t)h[0] << 32)) +
+               __builtin_bit_cast(double, (uint64_t)l[1] | ((uint64_t)h[1] << 32));
+    } else {
+        const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        return __builtin_bit_cast(double, (uint64_t)l[0] | ((uint64_t)h[0] << 32)) +
+               __builtin_bit_cast(double, (uint64_t)l[1] | ((uint64_t)h[1] << 32));
+    }
+}
+
+/* the sum of s over the wave, in every lane: the 8-lane butterfly of mx_exact_sum, row_mirror
+ * (16 lanes), then the row pairs and the halves -- every term passes at most 6 additions */
+__device__ __forceinline__ double mx_wave_sum64(double s)
+{
+    s += mx_dpp64<0xB1>(s);                      /* lane x ^ 1 */
+    s += mx_dpp64<0x4E>(s);                      /* lane x ^ 2 */
+    s += mx_dpp64<0x141>(s);                     /* row_half_mirror: the other 4 of the 8 */
+    s += mx_dpp64<0x140>(s);                     /* row_mirror: the other 8 of the 16 */
+    s = mx_xsum64<16>(s);
+    return mx_xsum64<32>(s);
+}
+
+/*
+ * A step whose flagged set is ONE coefficient (the common case: at q90 on random data ~0.13
+ * flagged coefficients per step, so ~94 % of flagged steps hold one): the whole wave computes it.
+ * Lane l = 8 y + x forms the reference's product (X(x,y) c_u[x]) c_v[y] (preprocess.c:160-162,
+ * 186-188; dct.c:48-50) in its operation order; the 64 products meet in mx_wave_sum64 -- every term
+ * through at most 6 additions, fewer than the 10 mx_exact_sum's bound allows, so that bound and its
+ * 2^-33 margin hold unchanged -- and t' = s R decides as mx_exact_sum's fast path.  Every lane holds
+ * the same t'; returns false on a near-tie (the caller then takes the sequential 8-lane path).
+ * Round 6: one instruction stream for the wave instead of eight 8-lane groups of which seven idle.
+ */
+template <class SMP, class XT>
+__device__ __forceinline__ bool mx_exact_one(const SMP &smp, unsigned ch, unsigned u, unsigned v, const XT &xt,
+                                             int &val)
+{
+    const unsigned l = mx_lane(), x = l & 7u, y = l >> 3;
+    const double sum = mx_wave_sum64(smp(x, y, ch, xt) * xt.cosx(u, x) * xt.cosx(v, y));
+    const double t = sum * xt.recip(ch == 0 ? 0 : 1, u * 8 + v), r = __builtin_rint(t);
+    val = (int)r;
+    return 0.5 - __builtin_fabs(t - r) > 0x1p-33;                          /* t - r: exact */
+}
+
+/* The single-coefficient case of an inline exact pass: when exactly one lane holds exactly one
+ * flag, one(sl, bit) computes it with the whole wave (mx_exact_one) and, unless it was a near-tie,
+ * writes it from lane 0 and returns true; the flag is then cleared. */
+template <class F>
+__device__ __forceinline__ void mx_exact_single(uint32_t &bits, F &&one)
+{
+    const uint64_t act = __ballot(bits != 0);
+    if (__popcll(act) == 1) {
+        const unsigned sl = __builtin_amdgcn_readfirstlane((unsigned)__builtin_ctzll(act));
+        const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)sl);
+        if (__popc(b1) == 1 && one(sl, (unsigned)__builtin_ctz(b1))) bits = 0;
+    }
+}
+
+/* lane 0 writes a whole-wave result into the stage (byte offset off) */
+__device__ __forceinline__ bool mx_put_one(const void *stage, unsigned off, bool ok, int val)
+{
+    if (!__builtin_amdgcn_readfirstlane((int)ok)) return false;
+    if (mx_lane() == 0) *(__attribute__((address_space(3))) int16_t *)(mx_lds((void *)stage) + off) = (int16_t)val;
+    return true;
+}
 
 /* the step's block jb and channel of a lane's column k (k_mxs column layout) */
 __device__ __forceinline__ unsigned mx_col_block(unsigned k, unsigned sl)
@@ -402,6 +495,14 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
 {
     const unsigned lane = mx_lane();
     mx_wave_sync();
+    mx_exact_single(bits, [&](unsigned sl, unsigned bt) __attribute__((always_inline)) {
+        const unsigned k = bt >> 3, v = bt & 7u;
+        const unsigned jj = sl & 15u, u = jj & 7u, ch = k < 2 ? (jj >> 3) : 2u;
+        const unsigned jb = mx_col_block(k, sl);
+        int val;
+        const bool ok = mx_exact_one(MxSmp1{mx_lds((void *)slot) + 24u * jb, 192u}, ch, u, v, xt, val);
+        return mx_put_one(L.stage, kBS * mx_pos(ch, jb) + 2u * xt.scan(u, v), ok, val);
+    });
     for (;;) {
         const uint64_t act = __ballot(bits != 0);
         if (!act) break;
@@ -419,7 +520,7 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
         const unsigned sl = code >> 8, k = (code >> 3) & 3u, v = code & 7u;
         const unsigned jj = sl & 15u, u = jj & 7u, ch = k < 2 ? (jj >> 3) : 2u;
         const unsigned jb = mx_col_block(k, sl);
-        const int val = mx_exact_coef(mx_lds((void *)slot) + 24u * jb, 192u, ch, u, v, x, T, xt);
+        const int val = mx_exact_coef<true>(MxSmp1{mx_lds((void *)slot) + 24u * jb, 192u}, ch, u, v, x, T, xt);
         if (live && x == 7)
             *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + kBS * mx_pos(ch, jb) +
                                                            2u * xt.scan(u, v)) = (int16_t)val;
@@ -428,38 +529,47 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-/* rare: the flagged v's of one column (the same arithmetic as mx_column_t) */
-__device__ __forceinline__ uint32_t mx_flags(const mx_f2 (&F)[4], const mx_f2 (&W)[4], const mx_f2 (&Lq)[4])
+/*
+ * The column pass computes in SCALAR fp32 (v_add_f32 / v_fma_f32): no packed-fp32 VALU instruction
+ * (v_pk_add_f32, v_pk_mul_f32, v_pk_fma_f32) is allowed in these kernels.  Round 6 found the cause
+ * of the rows-12..15 fault: on gfx950, a packed-fp32 instruction of a wave that
+ * also issues MFMAs intermittently writes wrong values in lanes 48..63 -- reproduced in isolation
+ * (tools/probes/pk_hazard4.hip: the packed 8-point DCT wrong in 1.7e-4 of its runs when the wave's
+ * own v_mfma_f32_16x16x32_f16 precede it, never without; tools/probes/pk_hazard5.hip: an op_sel
+ * swap of a source's halves suffices).  Lanes 48..63 of the column pass are blocks 3 and 7 of a
+ * step, i.e. the C rows 12..15 seen since round 3.  The scalar code is the very FOps sequence the
+ * guard band is derived for (xform_math.h), so the output is bit-identical; tools/mfma_war_check.py
+ * --no-pk rejects any packed-fp32 arithmetic in the built ISA (tests/test_isa.py).
+ */
+/* F[k] -> scale of output k of jx_fdct8 from the table's [half][4] layout (jx_pk_k order) */
+__device__ __forceinline__ void mx_unpack8(const mx_f4 &a, const mx_f4 &b, float (&o)[8])
 {
-    const mx_f2 M2 = {kMagic, kMagic};
+    o[0] = a.x, o[4] = a.y, o[2] = a.z, o[6] = a.w;
+    o[1] = b.x, o[3] = b.y, o[5] = b.z, o[7] = b.w;
+}
+
+/* rare: the flagged v's of one column (the same arithmetic as mx_column_r) */
+__device__ __forceinline__ uint32_t mx_flags(const float (&F)[8], const float (&W)[8], const float (&Lq)[8])
+{
     uint32_t m = 0;
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
-        const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
-        const mx_f2 rr = tm - M2;
-        const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
-        const mx_f2 e = __builtin_elementwise_fma(d, d, -Lq[p]);
-        m |= (e.x >= 0.0f ? 1u : 0u) << jx_pk_k(p, 0);
-        m |= (e.y >= 0.0f ? 1u : 0u) << jx_pk_k(p, 1);
+    for (int k = 0; k < 8; k++) {
+        const float tm = __builtin_fmaf(F[k], W[k], kMagic);
+        const float rr = tm - kMagic;
+        const float d = __builtin_fmaf(F[k], W[k], -rr);
+        const float e = __builtin_fmaf(d, d, -Lq[k]);
+        m |= (e >= 0.0f ? 1u : 0u) << k;
     }
     return m;
 }
 
-/* R pairs (y, y+1) of one column from the lo (rows 0..3) and hi (rows 4..7) tiles */
-__device__ __forceinline__ void mx_combine(mx_f4 hl, mx_f4 ll, mx_f4 hh, mx_f4 lh, mx_f2 (&R)[4])
+/* R rows 0..7 of one column from the lo (rows 0..3) and hi (rows 4..7) tiles: the lo B part is
+ * encoded at the hi part's scale (JX_MX_LOEXP = 0), so R = fl(acc_h + acc_l) */
+static_assert(JX_MX_LOEXP == 0, "the kernels take R = acc_h + acc_l");
+__device__ __forceinline__ void mx_combine(mx_f4 hl, mx_f4 ll, mx_f4 hh, mx_f4 lh, float (&R)[8])
 {
-    if (JX_MX_LOEXP == 0) {                     /* lo parts at the hi scale: fl(acc_h + acc_l) */
-        R[0] = mx_f2{ll.x, ll.y} + mx_f2{hl.x, hl.y};
-        R[1] = mx_f2{ll.z, ll.w} + mx_f2{hl.z, hl.w};
-        R[2] = mx_f2{lh.x, lh.y} + mx_f2{hh.x, hh.y};
-        R[3] = mx_f2{lh.z, lh.w} + mx_f2{hh.z, hh.w};
-        return;
-    }
-    const mx_f2 s = {0x1p-12f, 0x1p-12f};
-    R[0] = __builtin_elementwise_fma(mx_f2{ll.x, ll.y}, s, mx_f2{hl.x, hl.y});
-    R[1] = __builtin_elementwise_fma(mx_f2{ll.z, ll.w}, s, mx_f2{hl.z, hl.w});
-    R[2] = __builtin_elementwise_fma(mx_f2{lh.x, lh.y}, s, mx_f2{hh.x, hh.y});
-    R[3] = __builtin_elementwise_fma(mx_f2{lh.z, lh.w}, s, mx_f2{hh.z, hh.w});
+    R[0] = ll.x + hl.x, R[1] = ll.y + hl.y, R[2] = ll.z + hl.z, R[3] = ll.w + hl.w;
+    R[4] = lh.x + hh.x, R[5] = lh.y + hh.y, R[6] = lh.z + hh.z, R[7] = lh.w + hh.w;
 }
 
 /* a column's scales from the workgroup table; t0 = 0 (4:4:4: Y|Cb, 4:2:x: Y) or 2 (4:4:4: Cr,
@@ -475,23 +585,6 @@ __device__ __forceinline__ MxW mx_w(const MxTab &tb, unsigned t0, unsigned j)
 __device__ __forceinline__ MxW mx_l(const MxTab &tb, unsigned t0, unsigned j)
 {
     return MxW{tb.wl[t0 + 1][0][j], tb.wl[t0 + 1][1][j]};
-}
-/* k_mxs422: the scales (tables 0 and 2) in the workgroup's LDS image, the limits read from the
- * global image on the rare path */
-struct MxsScales {
-    mx_f4 w[2][2][16];
-};
-struct MxsTabRef {
-    const MxsScales &s;
-    const MxTab &g;
-};
-__device__ __forceinline__ MxW mx_w(const MxsTabRef &tb, unsigned t0, unsigned j)
-{
-    return MxW{tb.s.w[t0 >> 1][0][j], tb.s.w[t0 >> 1][1][j]};
-}
-__device__ __forceinline__ MxW mx_l(const MxsTabRef &tb, unsigned t0, unsigned j)
-{
-    return MxW{tb.g.wl[t0 + 1][0][j], tb.g.wl[t0 + 1][1][j]};
 }
 /* k_mxs's image table: MxTab with the Cr tables (2, 3) at 8 profiles -- a Cr column's profile is
  * j % 8 (lanes j and j + 8 read the same entry: an LDS broadcast) -- which frees the 512 bytes
@@ -576,35 +669,34 @@ __device__ __forceinline__ void mx_keep_ops(const T &...x)
     (void)k;
 }
 
-/* Column pass of one column (R pairs), quantiser, stage writes at za[v] + OFF, band flags (rare
+/* Column pass of one column (R rows), quantiser, stage writes at za[v] + OFF, band flags (rare
  * path: the exact per-coefficient test with the limits of table t0 + 1, after mx_fence(*fence)
- * when an MFMA may be in flight) into fl */
+ * when an MFMA may be in flight) into fl.  Scalar fp32 throughout (see mx_unpack8). */
 template <unsigned OFF, class TB>
-__device__ __forceinline__ void mx_column_r(const mx_f2 (&R)[4], const MxW &t, float limc, const TB &tb,
+__device__ __forceinline__ void mx_column_r(const float (&R)[8], const MxW &t, float limc, const TB &tb,
                                              unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc,
                                              const mx_f4 *fence = nullptr)
 {
-    mx_f2 F[4];
-    jx_fdct8_pk<MxPair>(R, F);
-    const mx_f4 w01 = t.w01, w23 = t.w23;
-    const mx_f2 W[4] = {mx_f2{w01.x, w01.y}, mx_f2{w01.z, w01.w}, mx_f2{w23.x, w23.y}, mx_f2{w23.z, w23.w}};
-    const mx_f2 M2 = {kMagic, kMagic};
+    float F[8], W[8];
+    jx_fdct8<FOps>(R, F);
+    mx_unpack8(t.w01, t.w23, W);
     typedef __attribute__((address_space(3))) uint16_t l16;
     float em = 0.0f;
 #pragma unroll
     for (int p = 0; p < 4; p++) {
-        const mx_f2 tm = __builtin_elementwise_fma(F[p], W[p], M2);
-        *(l16 *)(uintptr_t)(za[jx_pk_k(p, 0)] + OFF) = (uint16_t)__float_as_uint(tm.x);
-        *(l16 *)(uintptr_t)(za[jx_pk_k(p, 1)] + OFF) = (uint16_t)__float_as_uint(tm.y);
-        const mx_f2 rr = tm - M2;
-        const mx_f2 d = __builtin_elementwise_fma(F[p], W[p], -rr);
-        em = __builtin_fmaxf(__builtin_fmaxf(em, __builtin_fabsf(d.x)), __builtin_fabsf(d.y));
+        const int k0 = jx_pk_k(p, 0), k1 = jx_pk_k(p, 1);
+        const float t0v = __builtin_fmaf(F[k0], W[k0], kMagic), t1v = __builtin_fmaf(F[k1], W[k1], kMagic);
+        *(l16 *)(uintptr_t)(za[k0] + OFF) = (uint16_t)__float_as_uint(t0v);
+        *(l16 *)(uintptr_t)(za[k1] + OFF) = (uint16_t)__float_as_uint(t1v);
+        const float d0 = __builtin_fmaf(F[k0], W[k0], -(t0v - kMagic));
+        const float d1 = __builtin_fmaf(F[k1], W[k1], -(t1v - kMagic));
+        em = __builtin_fmaxf(__builtin_fmaxf(em, __builtin_fabsf(d0)), __builtin_fabsf(d1));
     }
     if (__builtin_expect(__ballot(em >= limc) != 0, 0)) {
         if (fence) mx_fence(*fence);
         const MxW lw = mx_l(tb, t0, j);
-        const mx_f4 l01 = lw.w01, l23 = lw.w23;
-        const mx_f2 Lq[4] = {mx_f2{l01.x, l01.y}, mx_f2{l01.z, l01.w}, mx_f2{l23.x, l23.y}, mx_f2{l23.z, l23.w}};
+        float Lq[8];
+        mx_unpack8(lw.w01, lw.w23, Lq);
         fl |= mx_flags(F, W, Lq) << (8 * kc);
     }
 }
@@ -620,7 +712,7 @@ __device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t,
                                              unsigned t0, unsigned j, const uint32_t (&za)[8], uint32_t &fl, int kc,
                                              const mx_f4 *fence = nullptr, const KF &keep = KF{})
 {
-    mx_f2 R[4];
+    float R[8];
     mx_combine(acc[0], acc[1], acc[2], acc[3], R);
     if (LAZY) {
         __builtin_amdgcn_sched_barrier(0);
@@ -922,7 +1014,9 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < 4; i++) acc[2][i] = cr[0][i] + cr[1][i];
+        for (int i = 0; i < 4; i++)                    /* scalar adds (no packed fp32, mx_unpack8) */
+            acc[2][i] = mx_f4{cr[0][i].x + cr[1][i].x, cr[0][i].y + cr[1][i].y, cr[0][i].z + cr[1][i].z,
+                              cr[0][i].w + cr[1][i].w};
         mx_column_t<8 * kBS, true>(acc[2], w0, limc2, tb, 2, j, za, fl, 2);
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
@@ -995,50 +1089,35 @@ __device__ __forceinline__ unsigned mx422_yblock(unsigned sl)
     return (sl & 15u) < 8 ? (sl >> 4) : 4u + (sl >> 4);
 }
 
-/*
- * One exact coefficient per 8-lane group from pixel pairs: lane x's samples are the averages
- * (X(p) + X(p + d1)) * 0.5 over rows y of p = row0 + rs y, X = the level-shifted channel value
- * in the reference's colour arithmetic.  Chroma (4:2:2): p = pixel 2x, d1 = 3 (the extension's
- * definition, oracle/cpu_ref.c cpuref_chroma_sample); Y: p = pixel x, d1 = 0 ((X + X) * 0.5 == X
- * exactly, so Y tasks share the code).  Valid in lane x == 7.
- */
-template <bool FAST = true>
-__device__ __forceinline__ int mx_exact_pair(const lds_u8 *row0, unsigned rs, unsigned d1, unsigned ch,
-                                             unsigned u, unsigned v, unsigned x, const jx_mxtab &T)
+/* the samples of chroma block cb of a step (MCU cb: pixels 16 cb .. 16 cb + 15 of the slot's rows);
+ * the right Y block's rows come from L.qtrue when it is a row-last block (bit cb of qmask) */
+template <class Lds>
+__device__ __forceinline__ MxSmp2 mx422_smp(Lds &L, const uint8_t *sp, uint32_t qmask, unsigned cb)
 {
-    const double cu = kMxCos[u][x];
-    const double k0c = kMxColour[ch][0], k1c = kMxColour[ch][1], k2c = kMxColour[ch][2];
-    const double Ac = kMxColour[ch][3], Sc = kMxColour[ch][4];
-    double prod[8];
-#pragma unroll
-    for (int y = 0; y < 8; y++) {
-        const lds_u8 *p = row0 + rs * (unsigned)y, *p1 = p + d1;
-        const double t0 = (k0c * (double)p[0] + k1c * (double)p[1]) + k2c * (double)p[2];
-        const double t1 = (k0c * (double)p1[0] + k1c * (double)p1[1]) + k2c * (double)p1[2];
-        const double X = (((Ac + Sc * t0) - 128.0) + ((Ac + Sc * t1) - 128.0)) * 0.5;
-        prod[y] = X * cu * kMxCos[v][y];
-    }
-    return mx_exact_sum<FAST>(prod, ch, u, v, x, T, T.r[ch == 0 ? 0 : 1][u * 8 + v]);
+    const bool q = (qmask >> cb) & 1u;
+    const lds_u8 *pl = mx_lds((void *)sp) + 48u * cb;
+    return MxSmp2{pl, q ? mx_lds(L.qtrue[cb]) : pl + 24u, 192u, q ? 24u : 192u};
 }
 
-/* lane x's first pixel (row 0) and row stride of chroma block cb in a step's slot; the right
- * Y block's rows come from L.qtrue when it is a row-last block (bit cb of qmask) */
-template <class Lds>
-__device__ __forceinline__ const lds_u8 *mx422_mcu_row0(Lds &L, const uint8_t *sp, uint32_t qmask,
-                                                        unsigned cb, unsigned x, unsigned &rs)
-{
-    const bool q = ((qmask >> cb) & 1u) && x >= 4;
-    rs = q ? 24u : 192u;
-    return q ? mx_lds(L.qtrue[cb]) + 6u * (x - 4u) : mx_lds((void *)sp) + 48u * cb + 6u * x;
-}
-
-/* Inline exact pass of one step: bit 8 col + v of a lane's bits (col 0 Y, 1 chroma) */
-template <class Lds>
+/* Inline exact pass of one step: bit 8 col + v of a lane's bits (col 0 Y, 1 chroma); the single-
+ * coefficient case on the whole wave, then eight tasks at a time (8 lanes each) */
+template <class Lds, class XT>
 __device__ __forceinline__ void mx422_exact_inline(Lds &L, const uint8_t *sp, uint32_t qmask,
-                                                   uint32_t bits, const jx_mxtab &T)
+                                                   uint32_t bits, const jx_mxtab &T, const XT &xt)
 {
     const unsigned lane = mx_lane();
     mx_wave_sync();
+    mx_exact_single(bits, [&](unsigned sl, unsigned bt) __attribute__((always_inline)) {
+        const unsigned k = bt >> 3, v = bt & 7u, jj = sl & 15u, u = jj & 7u;
+        const unsigned slot = mx422_yblock(sl);
+        int val;
+        bool ok;
+        if (k == 0)
+            ok = mx_exact_one(MxSmp1{mx_lds((void *)sp) + 24u * slot, 192u}, 0u, u, v, xt, val);
+        else
+            ok = mx_exact_one(mx422_smp(L, sp, qmask, sl >> 4), 1u + (jj >> 3), u, v, xt, val);
+        return mx_put_one(L.stage, (k ? kSt422C : 0u) + kBS * slot + 2u * xt.scan(u, v), ok, val);
+    });
     for (;;) {
         const uint64_t act = __ballot(bits != 0);
         if (!act) break;
@@ -1056,22 +1135,14 @@ __device__ __forceinline__ void mx422_exact_inline(Lds &L, const uint8_t *sp, ui
         const unsigned sl = code >> 8, k = (code >> 3) & 1u, v = code & 7u;
         const unsigned jj = sl & 15u, u = jj & 7u;
         const unsigned slot = mx422_yblock(sl);       /* Y block, or 4 c + cb for chroma */
-        unsigned ch, rs, d1;
-        const lds_u8 *row0;
-        if (k == 0) {
-            ch = 0;
-            rs = 192u;
-            d1 = 0;
-            row0 = mx_lds((void *)sp) + 24u * slot + 3u * x;
-        } else {
-            ch = 1u + (jj >> 3);
-            d1 = 3;
-            row0 = mx422_mcu_row0(L, sp, qmask, sl >> 4, x, rs);
-        }
-        const int val = mx_exact_pair<false>(row0, rs, d1, ch, u, v, x, T);   /* k_mxs422 at 128 VGPRs: no room */
+        int val;
+        if (k == 0)
+            val = mx_exact_coef<true>(MxSmp1{mx_lds((void *)sp) + 24u * slot, 192u}, 0u, u, v, x, T, xt);
+        else
+            val = mx_exact_coef<true>(mx422_smp(L, sp, qmask, sl >> 4), 1u + (jj >> 3), u, v, x, T, xt);
         if (live && x == 7)
             *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + (k ? kSt422C : 0u) + kBS * slot +
-                                                           2u * (unsigned)kMxScan[v][u]) = (int16_t)val;
+                                                           2u * xt.scan(u, v)) = (int16_t)val;
         mx_wave_sync();
     }
 }
@@ -1120,32 +1191,27 @@ struct alignas(16) Mxs422Lds {
     uint8_t qtrue[4][192];
     uint16_t task[8];
 };
-/* the per-wave part of the image (round 4's one-wave workgroups had it alone): the scales (tables
- * 0 and 2), the hot-path limits and the zig-zag positions */
-struct alignas(16) MxsImg1 {
-    MxsScales sc;
+/* the LDS image: B operands [part * 3 + which][lane] (which 0: the two Y sets' operands merged --
+ * B_Y0 is zero in columns 8..15, B_Y1 in 0..7, so lane l keeps set (l & 15) / 8's and the kernel
+ * rebuilds the zeros; 1, 2: chroma), the scale / limit table (round 6: the band limits of the rare
+ * path too, no global read there), the hot-path limits, the zig-zag positions and the exact pass's
+ * tables */
+struct alignas(16) MxsImg422 {
+    mx_u4 B[JX_MX_PARTS * 3][64];
+    MxTab tab;
     float limc[2][16];
     uint8_t scan_t[8][8];
+    MxExTab ex;
 };
-/* the global image: k_mx422's scale / limit table (the band limits of the rare path) */
-struct alignas(16) MxsImg422 {
-    MxTab tab;
-};
-__device__ MxsImg422 g_mxs422_img[2][JX_MAXQ + 1];
-/* the LDS image: B operands [part * 4 + which][lane], the per-wave part */
-struct alignas(16) MxsImg422w {
-    mx_u4 B[JX_MX_PARTS * 4][64];
-    MxsImg1 s;
-};
-constexpr unsigned kMxs422Pieces = sizeof(MxsImg422w) / 16;
-static_assert(sizeof(Mxs422Lds) % 16 == 0 && sizeof(Mxs422Lds) * kMxs422WPG + sizeof(MxsImg422w) <= 40 * 1024,
+constexpr unsigned kMxs422Pieces = sizeof(MxsImg422) / 16;
+static_assert(sizeof(Mxs422Lds) % 16 == 0 && sizeof(Mxs422Lds) * kMxs422WPG + sizeof(MxsImg422) <= 40 * 1024,
               "4 workgroups of 4 waves per CU");
-__device__ MxsImg422w g_mxs422_imgw[2][JX_MAXQ + 1];
+__device__ MxsImg422 g_mxs422_img[2][JX_MAXQ + 1];
 
 __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform_args a)
 {
     __shared__ __attribute__((aligned(16))) Mxs422Lds s_lds[kMxs422WPG];
-    __shared__ __attribute__((aligned(16))) MxsImg422w s_img;
+    __shared__ __attribute__((aligned(16))) MxsImg422 s_img;
     MxG g;
     g.rgb = a.g.rgb;
     g.out = a.g.out;
@@ -1167,9 +1233,8 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
     const unsigned lane = threadIdx.x & 63u;
     const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     Mxs422Lds &L = s_lds[wave];
-    const MxsImg422 &gimg = g_mxs422_img[g.force ? 1 : 0][g.quality];
     {
-        const uint8_t *img = (const uint8_t *)&g_mxs422_imgw[g.force ? 1 : 0][g.quality];
+        const uint8_t *img = (const uint8_t *)&g_mxs422_img[g.force ? 1 : 0][g.quality];
 #pragma unroll
         for (unsigned i = 0; i < (kMxs422Pieces + 64u * kMxs422WPG - 1u) / (64u * kMxs422WPG); i++) {
             const unsigned piece = 64u * kMxs422WPG * i + threadIdx.x;
@@ -1200,8 +1265,6 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
     const uint32_t t0 = q < 2 ? kSelLo : (q == 2 ? kSelOne : kSelZero);
     const uint32_t t1 = q < 2 ? kSelHi : kSelZero;
     const uint32_t t2 = q < 2 ? kSelLo : kSelZero;
-    const uint32_t soy = lane * 16u, soc = (lane & 31u) * 16u + (lane >> 5) * (g.nb / 2u) * 128u;
-    const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
     const jx_mxtab &T = g_mx422tab[g.force ? 1 : 0][g.quality];
 
@@ -1209,21 +1272,29 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
     __builtin_amdgcn_s_barrier();
     mx_wave_sync();
     if (cmp.b >= g.total) return;
-    const MxsImg1 &si = s_img.s;
     uint32_t za[8];
     {
         const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * ((j >> 3) * 4u + gq);
-        const mx_u2 sc = *(const mx_u2 *)&si.scan_t[u][0];
+        const mx_u2 sc = *(const mx_u2 *)&s_img.scan_t[u][0];
 #pragma unroll
         for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
     }
+    /* the B operands; reloaded after an exact pass, so that their registers are free during it */
     mx_u4 B[kParts][4];
+    const auto load_b = [&](unsigned l) __attribute__((always_inline)) {
 #pragma unroll
-    for (int p = 0; p < kParts; p++)
-#pragma unroll
-        for (int w = 0; w < 4; w++) B[p][w] = s_img.B[4 * p + w][lane];
-    const float limc0 = si.limc[0][j], limc2 = si.limc[1][j];
-    const MxsTabRef tb{si.sc, gimg.tab};
+        for (int p = 0; p < kParts; p++) {
+            const mx_u4 by = s_img.B[3 * p][l], zero = {};
+            B[p][0] = (l & 15u) < 8 ? by : zero;
+            B[p][1] = (l & 15u) < 8 ? zero : by;
+            B[p][2] = s_img.B[3 * p + 1][l];
+            B[p][3] = s_img.B[3 * p + 2][l];
+        }
+    };
+    load_b(lane);
+    const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
+    const MxTab &tb = s_img.tab;
+    const MxExLds xt{s_img.ex, s_img.scan_t};
 
     const auto body = [&](const MxsCur &S, uint8_t *sp) __attribute__((always_inline)) {
         if (!S.simple) {
@@ -1304,10 +1375,15 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
                 if (mx422_yblock(lane) >= nvalid) fl &= ~0xffu;
                 if (2u * (lane >> 4) >= nvalid) fl &= ~0xff00u;
             }
-            mx422_exact_inline(L, sp, qmask, fl, T);
+            mx422_exact_inline(L, sp, qmask, fl, T, xt);
+            load_b(mx_lane());
         }
         /* always two store instructions (the vmcnt accounting counts on it) */
         if (S.simple) {
+            /* the store's lane offsets, re-derived here (no VGPRs held across the step for them) */
+            const unsigned l = mx_lane();
+            const uint32_t soy = l * 16u, soc = (l & 31u) * 16u + (l >> 5) * (g.nb / 2u) * 128u;
+            const uint32_t ro = (l >> 3) * kBS + (l & 7u) * 16u;
             const mx_u4 vy = *(const mx_u4 *)(L.stage + ro);
             const mx_u4 vc = *(const mx_u4 *)(L.stage + kSt422C + ro);
             __builtin_nontemporal_store(vy, (mx_u4 *)((const uint8_t *)S.dst + soy));
@@ -1471,31 +1547,6 @@ __device__ __forceinline__ uint32_t mx420_true_rows(Lds &L, const MxG &g, const 
     return qm;
 }
 
-/* One exact chroma coefficient per 8-lane group from the MCU's pixels in global memory: lane x
- * averages the quad ((ls(p00) + ls(p01)) + (ls(p10) + ls(p11))) * 0.25 of chroma row y
- * (oracle/cpu_ref.c cpuref_chroma_sample), then as mx_exact_coef.  row0 = the MCU's pixel (0, 0).
- * Valid in lane x == 7. */
-template <bool FAST = true>
-__device__ __forceinline__ int mx_exact_quad(const uint8_t *row0, long long pitch, unsigned ch, unsigned u,
-                                             unsigned v, unsigned x, const jx_mxtab &T)
-{
-    const double cu = kMxCos[u][x];
-    const double k0c = kMxColour[ch][0], k1c = kMxColour[ch][1], k2c = kMxColour[ch][2];
-    const double Ac = kMxColour[ch][3], Sc = kMxColour[ch][4];
-    double prod[8];
-#pragma unroll
-    for (int y = 0; y < 8; y++) {
-        const uint8_t *p = row0 + (2ll * y) * pitch + 6u * x, *q = p + pitch;
-        const double l00 = (Ac + Sc * ((k0c * (double)p[0] + k1c * (double)p[1]) + k2c * (double)p[2])) - 128.0;
-        const double l01 = (Ac + Sc * ((k0c * (double)p[3] + k1c * (double)p[4]) + k2c * (double)p[5])) - 128.0;
-        const double l10 = (Ac + Sc * ((k0c * (double)q[0] + k1c * (double)q[1]) + k2c * (double)q[2])) - 128.0;
-        const double l11 = (Ac + Sc * ((k0c * (double)q[3] + k1c * (double)q[4]) + k2c * (double)q[5])) - 128.0;
-        const double X = ((l00 + l01) + (l10 + l11)) * 0.25;
-        prod[y] = X * cu * kMxCos[v][y];
-    }
-    return mx_exact_sum<FAST>(prod, ch, u, v, x, T, T.r[ch == 0 ? 0 : 1][u * 8 + v]);
-}
-
 /* the MCU's pixel (0, 0) */
 __device__ __forceinline__ const uint8_t *mx420_mcu_src(const MxG &g, const Mx420G &h, unsigned m)
 {
@@ -1507,13 +1558,38 @@ __device__ __forceinline__ const uint8_t *mx420_mcu_src(const MxG &g, const Mx42
 /* pair-MCU of a chroma-column lane group (the permlane16 swap's order) */
 __device__ __forceinline__ unsigned mx420_pm(unsigned gq) { return (gq & 1u) * 2u + (gq >> 1); }
 
-/* Inline exact pass: Y bits (col 0) of this step and chroma bits (col 1, pair base mp) */
-template <class Lds>
+/* Inline exact pass: Y bits (col 0) of this step and chroma bits (col 1, pair base mp).  A chroma
+ * task's MCU pm of the pair lies in slot pm / 2 (bytes 48 (pm & 1) of each of its 16 pixel rows) of
+ * a simple pair (both slots intact after step 1's rows); a general pair's MCUs (quirk rows, frame
+ * or launch ends) read their pixels from global memory. */
+template <class Lds, class XT>
 __device__ __forceinline__ void mx420_exact_inline(Lds &L, const uint8_t *sp, uint32_t bits, unsigned mp,
-                                                   const MxG &g, const Mx420G &h, const jx_mxtab &T)
+                                                   bool simple, const MxG &g, const Mx420G &h, const jx_mxtab &T,
+                                                   const XT &xt)
 {
     const unsigned lane = mx_lane();
     mx_wave_sync();
+    const auto chroma = [&](unsigned gq, auto &&fn) __attribute__((always_inline)) {
+        const unsigned pm = mx420_pm(gq);
+        if (simple)
+            return fn(MxSmp4<lds_u8, unsigned>{mx_lds(L.ring[pm >> 1]) + 48u * (pm & 1u), 96u});
+        unsigned m = mp + pm;
+        m = m < h.tm ? m : h.tm - 1u;
+        return fn(MxSmp4<uint8_t, long long>{mx420_mcu_src(g, h, m), g.pitch});
+    };
+    mx_exact_single(bits, [&](unsigned sl, unsigned bt) __attribute__((always_inline)) {
+        const unsigned k = bt >> 3, v = bt & 7u, jj = sl & 15u, u = jj & 7u, gq = sl >> 4;
+        const unsigned slot = 4u * (jj >> 3) + gq;
+        int val;
+        bool ok;
+        if (k == 0)
+            ok = mx_exact_one(MxSmp1{mx_lds((void *)sp) + 768u * (jj >> 3) + 24u * gq, 96u}, 0u, u, v, xt, val);
+        else
+            ok = chroma(gq, [&](const auto &smp) __attribute__((always_inline)) {
+                return mx_exact_one(smp, 1u + (jj >> 3), u, v, xt, val);
+            });
+        return mx_put_one(L.stage, (k ? kSt420C : 0u) + kBS * slot + 2u * xt.scan(u, v), ok, val);
+    });
     for (;;) {
         const uint64_t act = __ballot(bits != 0);
         if (!act) break;
@@ -1532,17 +1608,16 @@ __device__ __forceinline__ void mx420_exact_inline(Lds &L, const uint8_t *sp, ui
         const unsigned jj = sl & 15u, u = jj & 7u, gq = sl >> 4;
         const unsigned slot = 4u * (jj >> 3) + gq;     /* Y: set (j / 8), block gq; chroma: (c, gq) */
         int val;
-        if (k == 0) {
-            val = mx_exact_pair(mx_lds((void *)sp) + 96u * 8u * (jj >> 3) + 24u * gq + 3u * x, 96u, 0u, 0u, u, v,
-                                x, T);
-        } else {
-            unsigned m = mp + mx420_pm(gq);
-            m = m < h.tm ? m : h.tm - 1u;
-            val = mx_exact_quad(mx420_mcu_src(g, h, m), g.pitch, 1u + (jj >> 3), u, v, x, T);
-        }
+        if (k == 0)
+            val = mx_exact_coef<true>(MxSmp1{mx_lds((void *)sp) + 768u * (jj >> 3) + 24u * gq, 96u}, 0u, u, v, x, T,
+                                      xt);
+        else
+            val = chroma(gq, [&](const auto &smp) __attribute__((always_inline)) {
+                return mx_exact_coef<true>(smp, 1u + (jj >> 3), u, v, x, T, xt);
+            });
         if (live && x == 7)
             *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + (k ? kSt420C : 0u) + kBS * slot +
-                                                           2u * (unsigned)kMxScan[v][u]) = (int16_t)val;
+                                                           2u * xt.scan(u, v)) = (int16_t)val;
         mx_wave_sync();
     }
 }
@@ -1576,6 +1651,7 @@ struct alignas(16) MxsImg420 {
     MxTab tab;
     float limc[2][16];
     uint8_t scan_t[8][8];
+    MxExTab ex;
 };
 constexpr unsigned kMxs420Pieces = sizeof(MxsImg420) / 16;
 static_assert(sizeof(MxsImg420) % 16 == 0 && kMxs420Pieces <= 1024, "four 16-byte pieces per thread");
@@ -1678,6 +1754,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
         for (int w = 0; w < 5; w++) B[p][w] = s_img.B[5 * p + w][lane];
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
     const MxTab &tb = s_img.tab;
+    const MxExLds xt{s_img.ex, s_img.scan_t};
 
     const auto step = [&](auto kc) __attribute__((always_inline)) {
         constexpr unsigned k = decltype(kc)::value;
@@ -1767,13 +1844,11 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
         __builtin_amdgcn_sched_barrier(0);
         mx_column_t<0, true>(accY, MxW{}, limc0, tb, 0, j, za, fl, 0);
         __builtin_amdgcn_sched_barrier(0);
-        const float sl = JX_MX_LOEXP == 0 ? 1.0f : 0x1p-12f;
-        const mx_f4 s12 = {sl, sl, sl, sl};
-        const mx_f4 rc4 = JX_MX_LOEXP == 0 ? accC[1] + accC[0] : __builtin_elementwise_fma(accC[1], s12, accC[0]);
+        const mx_f4 rc4 = {accC[1].x + accC[0].x, accC[1].y + accC[0].y, accC[1].z + accC[0].z,
+                           accC[1].w + accC[0].w};   /* scalar adds (no packed fp32, mx_unpack8) */
         __builtin_amdgcn_sched_barrier(0);
         if (second) {
             const mx_f4 rA0 = L.rA[lane];
-            mx_f2 R[4];
             float lo4[4], hi4[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
@@ -1782,10 +1857,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
                 lo4[i] = __uint_as_float(r[0]);
                 hi4[i] = __uint_as_float(r[1]);
             }
-            R[0] = mx_f2{lo4[0], lo4[1]};
-            R[1] = mx_f2{lo4[2], lo4[3]};
-            R[2] = mx_f2{hi4[0], hi4[1]};
-            R[3] = mx_f2{hi4[2], hi4[3]};
+            const float R[8] = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
             mx_column_r<kSt420C>(R, mx_w(tb, 2, j), limc2, tb, 2, j, za, fl, 1);
         } else {
             L.rA[lane] = rc4;
@@ -1796,7 +1868,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
                 if (ms + (gq >> 1) >= h.tm) fl &= ~0xffu;
                 if (m0 + mx420_pm(gq) >= h.tm) fl &= ~0xff00u;
             }
-            mx420_exact_inline(L, sp, fl, m0, g, h, T);
+            mx420_exact_inline(L, sp, fl, m0, simple, g, h, T, xt);
         }
         /* stores: the Y store; on the second step also the pair's chroma */
         if (simple) {
@@ -1916,6 +1988,14 @@ void mx_scan_t(uint8_t (&st)[8][8])
         for (int v = 0; v < 8; v++) st[uu][v] = (uint8_t)scan[v][uu];
 }
 
+/* the exact pass's LDS tables: the glibc cosines and this quality's divisors */
+void mx_ex_tab(MxExTab &x, const jx_mxtab &t)
+{
+    static const double cosx[8][8] = JX_COS_INIT;
+    memcpy(x.cosx_, cosx, sizeof cosx);
+    memcpy(x.q_, t.q, sizeof t.q);
+}
+
 std::once_flag g_mx_once[kMaxDev];
 int g_mx_rc[kMaxDev];
 
@@ -1936,14 +2016,12 @@ int mx_tables_for_current_device()
              * table, the zig-zag positions and the exact pass's tables */
             std::vector<MxsImg> img(2 * (JX_MAXQ + 1));
             memset(img.data(), 0, img.size() * sizeof(MxsImg));
-            static const double cosx[8][8] = JX_COS_INIT;
             for (int f = 0; f < 2; f++)
                 for (int q = 1; q <= JX_MAXQ; q++) {
                     MxsImg &I = img[f * (JX_MAXQ + 1) + q];
                     const jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
                     memcpy(I.B, ops, sizeof I.B);
-                    memcpy(I.ex.cosx_, cosx, sizeof cosx);
-                    memcpy(I.ex.q_, t.q, sizeof t.q);
+                    mx_ex_tab(I.ex, t);
                     MxTab full;
                     mx_layout_tab(full, t, [](unsigned tt, unsigned jp) { return tt < 2 ? jp : 16u + (jp & 7u); });
                     for (unsigned jp = 0; jp < 16; jp++) {
@@ -1979,30 +2057,30 @@ int mx422_tables_for_current_device()
         if (!rc) rc = jx_mx422_operands(ops);
         if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx422tab), tab.data(), tab.size() * sizeof(jx_mxtab)));
         if (!rc) {
-            /* k_mxs422's images: the global scale / limit table (Y at plan column j % 8, chroma at
-             * 8 + j) and the LDS image (B operands; scales, hot-path limits, zig-zag positions) */
+            /* k_mxs422's image: B operands, the scale / limit table (Y at plan column j % 8,
+             * chroma at 8 + j), hot-path limits, zig-zag positions, the exact pass's tables */
             std::vector<MxsImg422> img(2 * (JX_MAXQ + 1));
-            std::vector<MxsImg422w> imgw(img.size());
             memset(img.data(), 0, img.size() * sizeof(MxsImg422));
-            memset(imgw.data(), 0, imgw.size() * sizeof(MxsImg422w));
             for (size_t i = 0; i < img.size(); i++) {
                 mx_layout_tab(img[i].tab, tab[i], [](unsigned tt, unsigned jp) { return tt < 2 ? (jp & 7u) : 8u + jp; });
-                memcpy(imgw[i].B, ops, sizeof imgw[i].B);
-                MxsImg1 &s1 = imgw[i].s;
-                for (int h = 0; h < 2; h++)
-                    for (int jp = 0; jp < 16; jp++) {
-                        s1.sc.w[0][h][jp] = img[i].tab.wl[0][h][jp];
-                        s1.sc.w[1][h][jp] = img[i].tab.wl[2][h][jp];
+                for (int p = 0; p < JX_MX_PARTS; p++)
+                    for (unsigned l = 0; l < 64; l++) {
+                        const bool set0 = (l & 15u) < 8;
+                        const uint16_t *keep = ops[p][set0 ? 0 : 1][l], *zero = ops[p][set0 ? 1 : 0][l];
+                        for (int e = 0; e < 8; e++)
+                            if (zero[e]) rc = JPGX_EARG;      /* the merge needs the zero halves (as jpgx_plan.cpp) */
+                        memcpy(&img[i].B[3 * p][l], keep, 16);
+                        memcpy(&img[i].B[3 * p + 1][l], ops[p][2][l], 16);
+                        memcpy(&img[i].B[3 * p + 2][l], ops[p][3][l], 16);
                     }
                 for (unsigned jp = 0; jp < 16; jp++) {
-                    s1.limc[0][jp] = mx_limc(img[i].tab, 1, jp);
-                    s1.limc[1][jp] = mx_limc(img[i].tab, 3, jp);
+                    img[i].limc[0][jp] = mx_limc(img[i].tab, 1, jp);
+                    img[i].limc[1][jp] = mx_limc(img[i].tab, 3, jp);
                 }
-                mx_scan_t(s1.scan_t);
+                mx_scan_t(img[i].scan_t);
+                mx_ex_tab(img[i].ex, tab[i]);
             }
-            rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs422_img), img.data(), img.size() * sizeof(MxsImg422)));
-            if (!rc)
-                rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs422_imgw), imgw.data(), imgw.size() * sizeof(MxsImg422w)));
+            if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs422_img), img.data(), img.size() * sizeof(MxsImg422)));
         }
         g_mx422_rc[dev] = rc;
     });
@@ -2035,6 +2113,7 @@ int mx420_tables_for_current_device()
                     img[i].limc[1][jp] = mx_limc(img[i].tab, 3, jp);
                 }
                 mx_scan_t(img[i].scan_t);
+                mx_ex_tab(img[i].ex, tab[i]);
             }
             rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs420_img), img.data(), img.size() * sizeof(MxsImg420)));
         }

@@ -248,10 +248,12 @@ static void encode_block(BW *w, const int16_t *z, int *pred, const HuffCodes *dc
 size_t jpgx_jfif_bound(int width, int height)
 {
     if (width <= 0 || height <= 0) return 0;
-    /* headers + worst case per block (DC 2+11 bits, 63 AC x (16+10 bits)) + stuffing x2, plus
-     * the restart markers (at most one per MCU row) */
+    /* headers + a per-block maximum with margin -- DC code + magnitude <= 16 + 16 bits, 63 AC
+     * codes + magnitudes <= 63 x (16 + 16) bits, EOB <= 16 bits -- doubled for 0xFF stuffing,
+     * plus per restart interval (at most one per MCU row) the padding byte, its possible stuffing
+     * byte and RSTm: 4 bytes */
     const size_t blocks = (size_t)(width / 8 + 1) * (height / 8 + 1) * 3;
-    return 1024 + blocks * 2 * (13 + 63 * 26 + 7) / 8 + 2 * (size_t)(height / 8 + 1);
+    return 1024 + blocks * 2 * (32 + 63 * 32 + 16) / 8 + 4 * (size_t)(height / 8 + 1);
 }
 
 /* The scan's geometry and tables, shared by the coding threads */
@@ -437,17 +439,19 @@ int jpgx_write_jfif_ex(const int16_t *coef, int width, int height, int quality, 
     Job *jobs = (Job *)calloc((size_t)T, sizeof(Job));
     pthread_t *tid = (pthread_t *)calloc((size_t)T, sizeof(pthread_t));
     int rc = (jobs && tid) ? JPGX_OK : JPGX_ENOMEM;
-    long started = 0;
+    long nthr = T;                                         /* jobs 1 .. nthr - 1 run on threads */
     for (long t = 0; t < T && !rc; t++) {
         jobs[t].S = &S;
         jobs[t].i0 = (size_t)t * S.nintervals / (size_t)T;
         jobs[t].i1 = (size_t)(t + 1) * S.nintervals / (size_t)T;
-        if (t == 0) continue;                              /* the calling thread codes job 0 */
-        if (pthread_create(&tid[t], NULL, job_main, &jobs[t])) rc = JPGX_ENOMEM;
-        else started = t;
+        if (t == 0 || t >= nthr) continue;                 /* the calling thread codes job 0 */
+        if (pthread_create(&tid[t], NULL, job_main, &jobs[t])) nthr = t;   /* no thread: code it here */
     }
-    if (!rc) job_main(&jobs[0]);
-    for (long t = 1; t <= started; t++) pthread_join(tid[t], NULL);
+    if (!rc) {
+        job_main(&jobs[0]);
+        for (long t = nthr; t < T; t++) job_main(&jobs[t]);   /* the jobs no thread took */
+    }
+    for (long t = 1; t < nthr; t++) pthread_join(tid[t], NULL);
     for (long t = 0; t < T && !rc; t++)
         if (jobs[t].w.oom) rc = JPGX_ENOMEM;
     if (!rc) {

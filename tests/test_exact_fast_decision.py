@@ -1,7 +1,10 @@
-"""CPU check of the exact pass's fast decision (csrc/jpgx_mx.hip mx_exact_sum, JX_MX_FASTEXACT):
-when the tree-ordered fp64 sum gives t = fl(fl(K s) / Q) with |frac(|t|) - 1/2| > 2^-33, rint(t)
-must equal round() of the reference's sequential sum (dct.c:46-54, quantise.c:58) -- here on
-random, extreme and tie-heavy blocks, in numpy fp64 (IEEE double, one rounding per operation)."""
+"""CPU check of the exact pass's fast decision (csrc/jpgx_mx.hip mx_exact_sum / mx_exact_one): the
+device forms t' = fl(s_par R) with R = fl(K / Q) (jx_mxtab.r, MxExLds::recip) from a tree-ordered
+fp64 sum s_par; when |frac(|t'|) - 1/2| > 2^-33, rint(t') must equal round() of the reference's
+t = fl(fl(K s_seq) / Q) from its sequential sum (dct.c:46-54, quantise.c:58).  Both device trees are
+modelled: the 8-lane groups' (8 in-lane additions + 3 butterfly levels) and the whole wave's of a
+single flagged coefficient (6 levels: x ^ 1, x ^ 2, 7 - x, row_mirror, permlane16 / permlane32
+swaps).  Random, extreme and tie-heavy blocks, in numpy fp64 (IEEE double, one rounding per op)."""
 import numpy as np
 
 M = 2.0 ** -33
@@ -23,7 +26,7 @@ def _round_away(t):
     return np.sign(t) * r
 
 
-def _decide(X, u, v, q):
+def _decide(X, u, v, q, wave=False):
     """X: (N, 8, 8) [x][y] level-shifted values; returns (reference, fast, decided)"""
     C = _cos()
     cu, cv = C[u][:, :, None], C[v][:, None, :]          # (N, 8, 1), (N, 1, 8)
@@ -32,19 +35,33 @@ def _decide(X, u, v, q):
     for x in range(8):
         for y in range(8):
             seq = seq + t[:, x, y]
-    lane = t[:, :, 0].copy()
-    for y in range(1, 8):
-        lane = lane + t[:, :, y]
-    l1 = lane + lane[:, [1, 0, 3, 2, 5, 4, 7, 6]]
-    l2 = l1 + l1[:, [2, 3, 0, 1, 6, 7, 4, 5]]
-    par = l2 + l2[:, [7, 6, 5, 4, 3, 2, 1, 0]]
-    assert np.all(par == par[:, :1])                      # every lane holds the same total
-    par = par[:, 0]
+    if wave:
+        # mx_exact_one: lane 8 y + x holds t[x, y]; 3 levels over x, then y pairs, quads, halves
+        w = t.copy()                                      # (N, x, y)
+        w = w + w[:, [1, 0, 3, 2, 5, 4, 7, 6], :]
+        w = w + w[:, [2, 3, 0, 1, 6, 7, 4, 5], :]
+        w = w + w[:, [7, 6, 5, 4, 3, 2, 1, 0], :]
+        assert np.all(w == w[:, :1, :])
+        r = w[:, 0, :]                                    # (N, y): the row sums
+        r = r + r[:, [1, 0, 3, 2, 5, 4, 7, 6]]            # row_mirror: y pairs
+        r = r + r[:, [2, 3, 0, 1, 6, 7, 4, 5]]            # permlane16 swap: y quads
+        r = r + r[:, [4, 5, 6, 7, 0, 1, 2, 3]]            # permlane32 swap: halves
+        assert np.all(r == r[:, :1])
+        par = r[:, 0]
+    else:
+        lane = t[:, :, 0].copy()
+        for y in range(1, 8):
+            lane = lane + t[:, :, y]
+        l1 = lane + lane[:, [1, 0, 3, 2, 5, 4, 7, 6]]
+        l2 = l1 + l1[:, [2, 3, 0, 1, 6, 7, 4, 5]]
+        par = l2 + l2[:, [7, 6, 5, 4, 3, 2, 1, 0]]
+        assert np.all(par == par[:, :1])                  # every lane holds the same total
+        par = par[:, 0]
     qa = np.where(u == 0, 0.25 * ALPHA0, 0.25)
     al = np.where(v == 0, ALPHA0, 1.0)
     K = qa * al
     ref = _round_away((K * seq) / q)
-    tp = (K * par) / q
+    tp = par * (K / q)                                    # the device: t' = fl(s_par fl(K / Q))
     a = np.abs(tp)
     decided = np.abs((a - np.floor(a)) - 0.5) > M
     return ref, np.rint(tp), decided
@@ -59,9 +76,10 @@ def test_fast_decision_matches_the_sequential_sum():
     u = rng.integers(0, 8, n)
     v = rng.integers(0, 8, n)
     q = rng.integers(1, 256, n).astype(np.float64)
-    ref, fast, decided = _decide(X, u, v, q)
-    assert decided.mean() > 0.99
-    assert np.array_equal(ref[decided], fast[decided])
+    for wave in (False, True):
+        ref, fast, decided = _decide(X, u, v, q, wave)
+        assert decided.mean() > 0.99
+        assert np.array_equal(ref[decided], fast[decided])
 
 
 def test_flat_blocks_fall_back():
@@ -73,7 +91,8 @@ def test_flat_blocks_fall_back():
     v = np.zeros(n, np.int64)
     for qv in (1, 2, 4, 8, 16, 32):
         q = np.full(n, float(qv))
-        ref, fast, decided = _decide(X, u, v, q)
-        assert np.array_equal(ref[decided], fast[decided])
-        if qv == 16:
-            assert not decided.all()                          # X odd: 8 X / 16 is a half
+        for wave in (False, True):
+            ref, fast, decided = _decide(X, u, v, q, wave)
+            assert np.array_equal(ref[decided], fast[decided])
+            if qv == 16:
+                assert not decided.all()                      # X odd: 8 X / 16 is a half

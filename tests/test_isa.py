@@ -30,6 +30,12 @@ def test_mfma_operand_rule(tmp_path):
                        + short, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
     assert r.stdout.count(" 0 load(s) or VALU write(s) into live MFMA operands") == len(short), r.stdout
+    # the root cause of the rows-12..15 fault: no packed-fp32 VALU arithmetic in a
+    # kernel that issues MFMAs
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), "--no-pk", str(asm)]
+                       + names, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert r.stdout.count(" 0 packed-fp32 VALU instruction(s)") == len(names), r.stdout
     # and no scratch, no VGPR / SGPR spills
     text = asm.read_text()
     for n in ("k_mxs", "k_mxs422", "k_mxs420"):
@@ -155,3 +161,63 @@ def test_mfma_chained_operand_rule(tmp_path):
         "\tv_perm_b32 v0, s0, v20, v21",
         "\tv_add_f32_e32 v30, v8, v9"])
     assert independent.returncode == 0, independent.stdout
+
+
+# The acc[1] column pass right after the Cr products of the round-5 "bgl" reproducer (B operands from
+# global memory at the wave's top: 20/20 launches wrong, gpurun_out/r6a), k_mxs step 0 -- every build
+# of rounds 3-5 that showed the rows-12..15 fault had this form (packed fp32 after the wave's MFMAs).
+_BGL_EXCERPT = [
+    "\tv_mfma_f32_16x16x32_f16 v[74:77], v[46:49], v[2:5], 0",
+    "\tv_mfma_f32_16x16x32_f16 v[42:45], v[42:45], v[6:9], 0",
+    "\tv_mfma_f32_16x16x32_f16 v[38:41], v[46:49], v[6:9], 0",
+    "\tv_add_f32_e64 v0, v60, v64",
+    "\tv_add_f32_e64 v1, v61, v65",
+    "\tv_pk_add_f32 v[46:47], v[58:59], v[62:63]",
+    "\tv_pk_add_f32 v[48:49], v[52:53], v[56:57]",
+    "\tv_pk_add_f32 v[50:51], v[50:51], v[54:55]",
+    "\tv_pk_add_f32 v[52:53], v[46:47], v[48:49] op_sel:[0,1] op_sel_hi:[1,0]",
+    "\tv_pk_fma_f32 v[52:53], v[46:47], s[12:13], v[46:47] op_sel:[1,0,0] op_sel_hi:[1,1,0]",
+    "\ts_endpgm"]
+
+
+def test_no_packed_fp32_rule(tmp_path):
+    """--no-pk: packed-fp32 arithmetic in a kernel that issues MFMAs is rejected (the recorded failing
+    build's column pass is), its scalar form passes, and a kernel without MFMAs may use packed fp32"""
+    tool = os.path.join(REPO, "tools", "mfma_war_check.py")
+    s = tmp_path / "fake.s"
+
+    def run(lines):
+        s.write_text("\n".join(["_ZN12_GLOBAL__N_14k_mxE13jx_xform_args:"] + lines + [".Lfunc_end0:", ""]))
+        return subprocess.run([sys.executable, tool, "--no-pk", str(s), "k_mx"], capture_output=True, text=True)
+
+    bad = run(_BGL_EXCERPT)
+    assert bad.returncode == 1 and " 5 packed-fp32 VALU instruction(s)" in bad.stdout, bad.stdout
+    scalar = run(_BGL_EXCERPT[:5] + ["\tv_add_f32_e32 v46, v58, v62", "\tv_add_f32_e32 v47, v59, v63",
+                                     "\tv_fmac_f32_e32 v52, 0x3f5906bd, v46", "\ts_endpgm"])
+    assert scalar.returncode == 0, scalar.stdout
+    no_mfma = run(["\tv_pk_fma_f32 v[0:1], v[2:3], v[4:5], v[6:7] op_sel_hi:[0,1,1]", "\ts_endpgm"])
+    assert no_mfma.returncode == 0, no_mfma.stdout
+    moves = run(["\tv_mfma_f32_16x16x32_f16 v[8:11], v[0:3], v[4:7], 0",
+                 "\tv_pk_mov_b32 v[20:21], v[22:23], v[22:23] op_sel:[1,0]", "\ts_endpgm"])
+    assert moves.returncode == 0, moves.stdout
+
+
+def test_no_packed_fp32_rule_rejects_recorded_failing_builds():
+    """every recorded failing build of the MFMA kernels (round-5 variants, built by
+    tools/build_variants.sh from tools/probes/jpgx_mx_r5_knobs.patch) fails --no-pk, whatever the
+    other rules said of it: bgl / bglpad (B from global memory), w1 (one-wave workgroups), and the
+    compact-table exact pass without its lgkmcnt(0) (ucc); the round-5 product too -- it passed by
+    timing.  Checked on the ISA files that exist in this checkout (build/variants, gitignored)."""
+    tool = os.path.join(REPO, "tools", "mfma_war_check.py")
+    vdir = os.path.join(PKG, "build", "variants")
+    seen = 0
+    for name in ("bgl", "bglpad", "w1", "ucc", "dump3"):
+        f = os.path.join(vdir, name + ".s")
+        if not os.path.exists(f):
+            continue
+        seen += 1
+        r = subprocess.run([sys.executable, tool, "--no-pk", f, "k_mxs"], capture_output=True, text=True)
+        assert r.returncode == 1 and "packed-fp32" in r.stdout, (name, r.stdout)
+    if seen == 0:
+        import pytest
+        pytest.skip("no variant ISA in this checkout")

@@ -22,7 +22,16 @@ With --valu-all, for a product that may start late -- a chained one (C input fro
 waits for its producer in the matrix pipe) or one issued behind it in the same burst -- no VALU
 instruction may write ANY of its operands (A, B or C) either: such a product reads them late, after
 hipcc's hazard padding, which counts from issue (profiles/r04_mfma_valu_war.txt).
-Usage: python tools/mfma_war_check.py [--valu-srcc | --valu-all] FILE.s [kernel ...]   (exit 1 on a violation)
+With --no-pk (round 6, the root cause of the rows-12..15 fault): no packed-fp32 VALU arithmetic
+(v_pk_add_f32, v_pk_mul_f32, v_pk_fma_f32) anywhere in a kernel that issues MFMAs.  On gfx950 such
+an instruction intermittently writes wrong values in lanes 48..63 when the same wave issues
+v_mfma_f32_16x16x32_f16 products (tools/probes/pk_hazard4.hip reproduces it in isolation: 0 wrong
+without MFMAs in the wave, ~1.7e-4 of packed 8-point DCTs with them; pk_hazard5.hip: an op_sel
+swap of a source's halves suffices).  Lanes 48..63 of k_mxs's column pass are blocks 3 / 7 of a
+step -- the "C rows 12..15" of rounds 3-5, which every earlier rule only moved around
+(DESIGN.md 4.3f).
+Usage: python tools/mfma_war_check.py [--valu-srcc | --valu-all] [--no-pk] FILE.s [kernel ...]
+(exit 1 on a violation)
 """
 import re
 import sys
@@ -163,11 +172,22 @@ def check(ins, labels, valu_srcc=False, valu_all=False):
     return bad
 
 
+PK_F32 = re.compile(r"^v_pk_(add|mul|fma)_f32$")
+
+
+def packed_f32(ins):
+    """indices of packed-fp32 arithmetic instructions, if the kernel issues MFMAs"""
+    if not any(t.startswith("v_mfma") for t in ins):
+        return []
+    return [i for i, t in enumerate(ins) if PK_F32.match(operands(t)[0])]
+
+
 def main():
     args = sys.argv[1:]
     valu_all = "--valu-all" in args
     valu_srcc = "--valu-srcc" in args or valu_all
-    args = [a for a in args if a not in ("--valu-srcc", "--valu-all")]
+    no_pk = "--no-pk" in args
+    args = [a for a in args if a not in ("--valu-srcc", "--valu-all", "--no-pk")]
     path = args[0]
     names = args[1:] or ["k_mx", "k_mx422", "k_mx420"]
     text = open(path).read()
@@ -177,6 +197,13 @@ def main():
         if ins is None:
             print(f"{n}: not found")
             rc = 1
+            continue
+        if no_pk:
+            pk = packed_f32(ins)
+            print(f"{n}: {sum(1 for x in ins if x.startswith('v_mfma'))} MFMAs, {len(pk)} packed-fp32 VALU instruction(s)")
+            for i in pk[:12]:
+                print(f"   at {i}: {ins[i][:72]}")
+            rc |= 1 if pk else 0
             continue
         bad = check(ins, labels, valu_srcc, valu_all)
         what = ("load(s) or VALU write(s)" if valu_all else

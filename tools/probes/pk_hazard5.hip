@@ -13,7 +13,9 @@
  *   14 swap src1 after 32 wait states; 15 v_pk_fma src2 lo broadcast; 16 the column pass's
  *   v_pk_fma (src0 hi broadcast, SGPR pair, src2 lo broadcast); 17 swap src1 whose pair was written
  *   an iteration earlier; 1 again
- * Usage: ./pk_hazard5 [blocks] [iters] [set 0 | 1]
+ *  (set 2) fp64 VALU (the exact pass's arithmetic): 20 v_add_f64, 21 v_fma_f64, 22 v_mul_f64,
+ *   23 v_add_f64 of a DPP row_half_mirror'd value; 1 again
+ * Usage: ./pk_hazard5 [blocks] [iters] [set 0 | 1 | 2]
  * Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -o tools/probes/pk_hazard5 tools/probes/pk_hazard5.hip
  */
 #include <hip/hip_runtime.h>
@@ -126,6 +128,32 @@ __global__ __launch_bounds__(256) void k_form(unsigned *bad, int iters, float kx
         } else if (MODE == 16) {                 /* the column pass's form: src0 hi broadcast, SGPR, src2 lo broadcast */
             asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,0]" : "=v"(D) : "v"(A), "s"(K), "v"(C));
             wx = __builtin_fmaf(A.y, K.x, C.x), wy = __builtin_fmaf(A.y, K.y, C.x);
+        } else if (MODE == 20 || MODE == 21 || MODE == 22) { /* fp64: v_add_f64 / v_fma_f64 / v_mul_f64 */
+            const double da = (double)A.x * 3.0 + (double)A.y, db = (double)B.x - (double)B.y * 0.5,
+                         dc = (double)C.x;
+            double dd;
+            if (MODE == 20) asm volatile("v_add_f64 %0, %1, %2" : "=v"(dd) : "v"(da), "v"(db));
+            else if (MODE == 21) asm volatile("v_fma_f64 %0, %1, %2, %3" : "=v"(dd) : "v"(da), "v"(db), "v"(dc));
+            else asm volatile("v_mul_f64 %0, %1, %2" : "=v"(dd) : "v"(da), "v"(db));
+            const double wd = MODE == 20 ? da + db : (MODE == 21 ? __builtin_fma(da, db, dc) : da * db);
+            const uint64_t gb = __builtin_bit_cast(uint64_t, dd), wb = __builtin_bit_cast(uint64_t, wd);
+            D = f2{__uint_as_float((uint32_t)gb), __uint_as_float((uint32_t)(gb >> 32))};
+            wx = __uint_as_float((uint32_t)wb), wy = __uint_as_float((uint32_t)(wb >> 32));
+        } else if (MODE == 23) {                 /* the exact pass's DPP step: v_add_f64 of a row_half_mirror'd value */
+            const double da = (double)A.x * 3.0 + (double)A.y;
+            const uint64_t b = __builtin_bit_cast(uint64_t, da);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x141, 0xf, 0xf, false);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x141, 0xf, 0xf, false);
+            const double dm = __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+            double dd;
+            asm volatile("v_add_f64 %0, %1, %2" : "=v"(dd) : "v"(da), "v"(dm));
+            /* the reference: the mirrored lane's value via LDS-free recomputation is not possible here,
+             * so compare with the same add done after a fence-like dependency chain */
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+            const double wd = da + dm;
+            const uint64_t gb = __builtin_bit_cast(uint64_t, dd), wb = __builtin_bit_cast(uint64_t, wd);
+            D = f2{__uint_as_float((uint32_t)gb), __uint_as_float((uint32_t)(gb >> 32))};
+            wx = __uint_as_float((uint32_t)wb), wy = __uint_as_float((uint32_t)(wb >> 32));
         } else {                                 /* 17: swap src1, both halves of B old (written one iteration early) */
             asm volatile("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(D) : "v"(A), "v"(Bold));
             wx = A.x + Bold.y, wy = A.y + Bold.x;
@@ -169,6 +197,12 @@ int main(int argc, char **argv)
         run<5>(d_bad, blocks, iters);
         run<6>(d_bad, blocks, iters);
         run<7>(d_bad, blocks, iters);
+    } else if (which == 2) {
+        run<20>(d_bad, blocks, iters);
+        run<21>(d_bad, blocks, iters);
+        run<22>(d_bad, blocks, iters);
+        run<23>(d_bad, blocks, iters);
+        run<1>(d_bad, blocks, iters);
     } else {
         run<1, false>(d_bad, blocks, iters);
         run<10>(d_bad, blocks, iters);
