@@ -92,10 +92,6 @@ struct MxTab {
     mx_f4 wl[4][2][16];
 };
 
-__device__ jx_mxtab g_mxtab[2][JX_MAXQ + 1];     /* [force][quality]                        */
-/* ((0.25 a(u)) a(v)) of dct.c:54, 0.25 a(u) exact in a double */
-__constant__ double kMxQuarterAlpha[8] = {0.25 * JX_ALPHA0, 0.25, 0.25, 0.25, 0.25, 0.25, 0.25, 0.25};
-__constant__ double kMxAlpha[8] = {JX_ALPHA0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0};
 
 /* Keep the compiler from moving this wave's LDS accesses across this point (a wave's LDS
  * instructions execute in program order; no fence: that would drain the memory counters). */
@@ -274,17 +270,18 @@ __device__ __forceinline__ double mx_dpp64(double s)
  * summation (Higham, Thm 4.4): |s_seq - s| <= g63 sum|t|, |s_par - s| <= g10 sum|t| (g_n = n u /
  * (1 - n u)), so |s_seq - s_par| <= 73.01 u 10944.01 < 8.9e-11.  The reference's t = fl(fl(K s) /
  * Q) (K = (1/4 a(u)) a(v) in (0, 0.25], Q >= 1, |t| <= 2736) and the fast t' = fl(s_par R), R =
- * fl(K / Q) from the table (jx_mxtab.r, R), differ by at most 0.25 * 8.9e-11 + 4.01 u 2736 < 2.4e-11.
+ * fl(K / Q) (MxExLds::recip, the host's jx_mxtab.r), differ by at most 0.25 * 8.9e-11 + 4.01 u 2736 < 2.4e-11.
  * So when t' is more than 2^-33 (1.16e-10) away from every half-integer (|t' - rint(t')| < 1/2 -
  * 2^-33; the difference is exact), no half-integer lies between t' and the reference's t, and
  * round(t) == rint(t').  Otherwise (near-ties: flat blocks, exact DC halves) the whole batch takes
  * the sequential sum -- wave-uniform, rare.
  * Valid in lane x == 7 (fast path: every lane).
  */
-template <bool FAST = true>
+template <bool FAST, class XT>
 __device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch, unsigned u, unsigned v,
-                                            unsigned x, const jx_mxtab &T, double R)
+                                            unsigned x, const XT &xt)
 {
+    const unsigned c = ch == 0 ? 0u : 1u;
     if constexpr (FAST) {
         double p = prod[0];
 #pragma unroll
@@ -292,7 +289,7 @@ __device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch
         p += mx_dpp64<0xB1>(p);                  /* quad_perm [1,0,3,2]: lane x ^ 1 */
         p += mx_dpp64<0x4E>(p);                  /* quad_perm [2,3,0,1]: lane x ^ 2 */
         p += mx_dpp64<0x141>(p);                 /* row_half_mirror: lane 7 - x      */
-        const double t = p * R, r = __builtin_rint(t);
+        const double t = p * xt.recip(c, u * 8 + v), r = __builtin_rint(t);
         if (__ballot(0.5 - __builtin_fabs(t - r) <= 0x1p-33) == 0) return (int)r;   /* t - r: exact */
     }
     double sum = 0.0;
@@ -304,9 +301,7 @@ __device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch
         }
         if (xx < 7) sum = mx_shr1(sum);
     }
-    const double F = kMxQuarterAlpha[u] * kMxAlpha[v] * sum;
-    const int q = T.q[ch == 0 ? 0 : 1][u * 8 + v];
-    return (int)round(F / (double)q);
+    return (int)round(xt.kfac(u * 8 + v) * sum / xt.div(c, u * 8 + v));
 }
 
 /* where the exact pass's constants come from: the workgroup's LDS image and literals (MxExLds;
@@ -331,12 +326,15 @@ struct MxExLds {
                      r[5] = {0.5, -0.418688, -0.081312, 128.0, 1.0};
         return ch == 0 ? y[i] : (ch == 1 ? b[i] : r[i]);
     }
-    /* jx_mxtab.r: fl(fl((1/4 a(u)) a(v)) / Q), the same IEEE operations as the host's */
-    __device__ double recip(unsigned c, unsigned i) const
+    /* K = fl((1/4 a(u)) a(v)) of dct.c:54 (0.25 a(u) is exact in a double), i = 8 u + v */
+    __device__ double kfac(unsigned i) const
     {
-        const double K = ((i >> 3) == 0 ? 0.25 * JX_ALPHA0 : 0.25) * ((i & 7u) == 0 ? JX_ALPHA0 : 1.0);
-        return K / (double)X.q_[c][i];
+        return ((i >> 3) == 0 ? 0.25 * JX_ALPHA0 : 0.25) * ((i & 7u) == 0 ? JX_ALPHA0 : 1.0);
     }
+    /* the transposed divisor Q of quantise.c:58 (channel class c: 0 luminance, 1 chrominance) */
+    __device__ double div(unsigned c, unsigned i) const { return (double)X.q_[c][i]; }
+    /* jx_mxtab.r: fl(K / Q), the same IEEE operations as the host's */
+    __device__ double recip(unsigned c, unsigned i) const { return kfac(i) / div(c, i); }
     __device__ unsigned scan(unsigned u, unsigned v) const { return scan_t[u][v]; }
 };
 
@@ -391,13 +389,13 @@ struct MxSmp4 {
  * (X(x, y) c_u[x]) c_v[y] (dct.c:48-50), mx_exact_sum sums them and rounds.  Valid in lane x == 7. */
 template <bool FAST, class SMP, class XT>
 __device__ __forceinline__ int mx_exact_coef(const SMP &smp, unsigned ch, unsigned u, unsigned v, unsigned x,
-                                             const jx_mxtab &T, const XT &xt)
+                                             const XT &xt)
 {
     const double cu = xt.cosx(u, x);
     double prod[8];
 #pragma unroll
     for (int y = 0; y < 8; y++) prod[y] = smp(x, (unsigned)y, ch, xt) * cu * xt.cosx(v, y);
-    return mx_exact_sum<FAST>(prod, ch, u, v, x, T, xt.recip(ch == 0 ? 0 : 1, u * 8 + v));
+    return mx_exact_sum<FAST>(prod, ch, u, v, x, xt);
 }
 
 __device__ __forceinline__ lds_u8 *mx_lds(void *p) { return (lds_u8 *)p; }
@@ -487,10 +485,11 @@ __device__ __forceinline__ unsigned mx_col_block(unsigned k, unsigned sl)
 }
 
 /* Inline exact pass of one step: every flagged coefficient (bit 8 col + v of a lane's `bits`),
- * eight at a time, patching the stage.  It ends with its LDS operations retired (lgkmcnt(0); see
- * DESIGN.md 4.3f for what that wait is and is not). */
+ * the single-coefficient case on the whole wave, otherwise eight at a time, patching the stage.
+ * (Round 5 ended it with lgkmcnt(0) against a fault that round 6 traced to packed fp32, DESIGN.md
+ * 4.3f; the wait is gone.) */
 template <class Lds, class XT>
-__device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uint32_t bits, const jx_mxtab &T,
+__device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uint32_t bits,
                                                 const XT &xt)
 {
     const unsigned lane = mx_lane();
@@ -520,13 +519,12 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
         const unsigned sl = code >> 8, k = (code >> 3) & 3u, v = code & 7u;
         const unsigned jj = sl & 15u, u = jj & 7u, ch = k < 2 ? (jj >> 3) : 2u;
         const unsigned jb = mx_col_block(k, sl);
-        const int val = mx_exact_coef<true>(MxSmp1{mx_lds((void *)slot) + 24u * jb, 192u}, ch, u, v, x, T, xt);
+        const int val = mx_exact_coef<true>(MxSmp1{mx_lds((void *)slot) + 24u * jb, 192u}, ch, u, v, x, xt);
         if (live && x == 7)
             *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + kBS * mx_pos(ch, jb) +
                                                            2u * xt.scan(u, v)) = (int16_t)val;
         mx_wave_sync();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 /*
@@ -904,7 +902,6 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
     const uint32_t rr = ro + ((lane >> 3) < 4 ? 8u : 16u) * kBS;
     const uint32_t rcb = 12u * kBS + ro;
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
-    const jx_mxtab &T = g_mxtab[g.force ? 1 : 0][g.quality];
     const MxExLds xt{s_img.ex, s_img.scan_t};
 
     /* the image has landed (it is older than the prologue's pixel operations), in every wave */
@@ -921,11 +918,15 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
 #pragma unroll
         for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
     }
+    /* the B operands; reloaded after an exact pass, so that their registers are free during it */
     mx_u4 B[kParts][3];
+    const auto load_b = [&](unsigned l) __attribute__((always_inline)) {
 #pragma unroll
-    for (int p = 0; p < kParts; p++)
+        for (int p = 0; p < kParts; p++)
 #pragma unroll
-        for (int w = 0; w < 3; w++) B[p][w] = s_img.B[3 * p + w][lane];
+            for (int w = 0; w < 3; w++) B[p][w] = s_img.B[3 * p + w][l];
+    };
+    load_b(lane);
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
     const MxsTab &tb = s_img.tab;
 
@@ -1021,7 +1022,8 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
             clamp(fl);
-            mx_exact_inline(L, sp, fl, T, xt);
+            mx_exact_inline(L, sp, fl, xt);
+            load_b(mx_lane());
         }
         /* stores: always three store instructions (the vmcnt accounting counts on it) */
         if (early) {
@@ -1081,7 +1083,6 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
  *           chroma in preprocess.c's operation order.
  */
 constexpr unsigned kSt422C = 8 * kBS;         /* chroma (c, cb) at kSt422C + kBS (4 c + cb) */
-__device__ jx_mxtab g_mx422tab[2][JX_MAXQ + 1];  /* n = 8 c + u: c = 0 Y, 1 Cb, 2 Cr */
 
 /* Y block of a lane's columns (lane (gq, j): set j / 8); also the chroma column's stage slot */
 __device__ __forceinline__ unsigned mx422_yblock(unsigned sl)
@@ -1103,7 +1104,7 @@ __device__ __forceinline__ MxSmp2 mx422_smp(Lds &L, const uint8_t *sp, uint32_t 
  * coefficient case on the whole wave, then eight tasks at a time (8 lanes each) */
 template <class Lds, class XT>
 __device__ __forceinline__ void mx422_exact_inline(Lds &L, const uint8_t *sp, uint32_t qmask,
-                                                   uint32_t bits, const jx_mxtab &T, const XT &xt)
+                                                   uint32_t bits, const XT &xt)
 {
     const unsigned lane = mx_lane();
     mx_wave_sync();
@@ -1137,9 +1138,9 @@ __device__ __forceinline__ void mx422_exact_inline(Lds &L, const uint8_t *sp, ui
         const unsigned slot = mx422_yblock(sl);       /* Y block, or 4 c + cb for chroma */
         int val;
         if (k == 0)
-            val = mx_exact_coef<true>(MxSmp1{mx_lds((void *)sp) + 24u * slot, 192u}, 0u, u, v, x, T, xt);
+            val = mx_exact_coef<true>(MxSmp1{mx_lds((void *)sp) + 24u * slot, 192u}, 0u, u, v, x, xt);
         else
-            val = mx_exact_coef<true>(mx422_smp(L, sp, qmask, sl >> 4), 1u + (jj >> 3), u, v, x, T, xt);
+            val = mx_exact_coef<true>(mx422_smp(L, sp, qmask, sl >> 4), 1u + (jj >> 3), u, v, x, xt);
         if (live && x == 7)
             *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + (k ? kSt422C : 0u) + kBS * slot +
                                                            2u * xt.scan(u, v)) = (int16_t)val;
@@ -1266,7 +1267,6 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
     const uint32_t t1 = q < 2 ? kSelHi : kSelZero;
     const uint32_t t2 = q < 2 ? kSelLo : kSelZero;
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
-    const jx_mxtab &T = g_mx422tab[g.force ? 1 : 0][g.quality];
 
     mx_wait_vm<2u * kMxs422C>();                    /* the image (older than the pixel DMA) */
     __builtin_amdgcn_s_barrier();
@@ -1375,7 +1375,7 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
                 if (mx422_yblock(lane) >= nvalid) fl &= ~0xffu;
                 if (2u * (lane >> 4) >= nvalid) fl &= ~0xff00u;
             }
-            mx422_exact_inline(L, sp, qmask, fl, T, xt);
+            mx422_exact_inline(L, sp, qmask, fl, xt);
             load_b(mx_lane());
         }
         /* always two store instructions (the vmcnt accounting counts on it) */
@@ -1444,7 +1444,6 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
  *           memory, in the oracle's order: ((ls(p00) + ls(p01)) + (ls(p10) + ls(p11))) * 0.25.
  */
 constexpr unsigned kSt420C = 8 * kBS;         /* chroma (c, lane group gq) at kSt420C + kBS (4 c + gq) */
-__device__ jx_mxtab g_mx420tab[2][JX_MAXQ + 1];
 
 /* MCU geometry of the launch */
 struct Mx420G {
@@ -1564,8 +1563,7 @@ __device__ __forceinline__ unsigned mx420_pm(unsigned gq) { return (gq & 1u) * 2
  * or launch ends) read their pixels from global memory. */
 template <class Lds, class XT>
 __device__ __forceinline__ void mx420_exact_inline(Lds &L, const uint8_t *sp, uint32_t bits, unsigned mp,
-                                                   bool simple, const MxG &g, const Mx420G &h, const jx_mxtab &T,
-                                                   const XT &xt)
+                                                   bool simple, const MxG &g, const Mx420G &h, const XT &xt)
 {
     const unsigned lane = mx_lane();
     mx_wave_sync();
@@ -1609,11 +1607,10 @@ __device__ __forceinline__ void mx420_exact_inline(Lds &L, const uint8_t *sp, ui
         const unsigned slot = 4u * (jj >> 3) + gq;     /* Y: set (j / 8), block gq; chroma: (c, gq) */
         int val;
         if (k == 0)
-            val = mx_exact_coef<true>(MxSmp1{mx_lds((void *)sp) + 768u * (jj >> 3) + 24u * gq, 96u}, 0u, u, v, x, T,
-                                      xt);
+            val = mx_exact_coef<true>(MxSmp1{mx_lds((void *)sp) + 768u * (jj >> 3) + 24u * gq, 96u}, 0u, u, v, x, xt);
         else
             val = chroma(gq, [&](const auto &smp) __attribute__((always_inline)) {
-                return mx_exact_coef<true>(smp, 1u + (jj >> 3), u, v, x, T, xt);
+                return mx_exact_coef<true>(smp, 1u + (jj >> 3), u, v, x, xt);
             });
         if (live && x == 7)
             *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + (k ? kSt420C : 0u) + kBS * slot +
@@ -1734,7 +1731,6 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
     const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
     const uint32_t rc = kSt420C + kBS * (4u * (lane >> 5) + mx420_pm((lane >> 3) & 3u)) + (lane & 7u) * 16u;
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
-    const jx_mxtab &T = g_mx420tab[g.force ? 1 : 0][g.quality];
 
     mx_wait_vm<4>();                                    /* the image (older than the pixel DMA) */
     __builtin_amdgcn_s_barrier();
@@ -1747,11 +1743,15 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
 #pragma unroll
         for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
     }
+    /* the B operands; reloaded after step 0's exact pass, so that their registers are free during it */
     mx_u4 B[kParts][5];
+    const auto load_b = [&](unsigned l) __attribute__((always_inline)) {
 #pragma unroll
-    for (int p = 0; p < kParts; p++)
+        for (int p = 0; p < kParts; p++)
 #pragma unroll
-        for (int w = 0; w < 5; w++) B[p][w] = s_img.B[5 * p + w][lane];
+            for (int w = 0; w < 5; w++) B[p][w] = s_img.B[5 * p + w][l];
+    };
+    load_b(lane);
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
     const MxTab &tb = s_img.tab;
     const MxExLds xt{s_img.ex, s_img.scan_t};
@@ -1868,7 +1868,8 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
                 if (ms + (gq >> 1) >= h.tm) fl &= ~0xffu;
                 if (m0 + mx420_pm(gq) >= h.tm) fl &= ~0xff00u;
             }
-            mx420_exact_inline(L, sp, fl, m0, simple, g, h, T, xt);
+            mx420_exact_inline(L, sp, fl, m0, simple, g, h, xt);
+            if (!second) load_b(mx_lane());
         }
         /* stores: the Y store; on the second step also the pair's chroma */
         if (simple) {
@@ -2009,7 +2010,6 @@ int mx_tables_for_current_device()
         std::unique_ptr<uint16_t[][64][8]> opsp(new uint16_t[3 * JX_MX_PARTS][64][8]);   /* heap: reentrant */
         auto ops = opsp.get();
         if (!rc) rc = jx_mx_operands(ops);
-        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxtab), tab.data(), tab.size() * sizeof(jx_mxtab)));
         if (!rc) {
             /* k_mxs's workgroup images: B operands, the scale / limit table (Y|Cb at 16 lane
              * profiles, Cr compacted to 8), the hot-path limits mx_limc computes from the full
@@ -2055,7 +2055,6 @@ int mx422_tables_for_current_device()
         std::unique_ptr<uint16_t[][4][64][8]> opsp(new uint16_t[JX_MX_PARTS][4][64][8]);   /* heap: reentrant */
         auto ops = opsp.get();
         if (!rc) rc = jx_mx422_operands(ops);
-        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx422tab), tab.data(), tab.size() * sizeof(jx_mxtab)));
         if (!rc) {
             /* k_mxs422's image: B operands, the scale / limit table (Y at plan column j % 8,
              * chroma at 8 + j), hot-path limits, zig-zag positions, the exact pass's tables */
@@ -2100,7 +2099,6 @@ int mx420_tables_for_current_device()
         std::unique_ptr<uint16_t[][5][64][8]> opsp(new uint16_t[JX_MX_PARTS][5][64][8]);   /* heap: reentrant */
         auto ops = opsp.get();
         if (!rc) rc = jx_mx420_operands(ops);
-        if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mx420tab), tab.data(), tab.size() * sizeof(jx_mxtab)));
         if (!rc) {
             /* k_mxs420's image (the 4:2:2 table layout) */
             std::vector<MxsImg420> img(2 * (JX_MAXQ + 1));
