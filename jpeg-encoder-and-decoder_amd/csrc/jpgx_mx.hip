@@ -41,7 +41,7 @@
  *           F = ((1/4 a(u)) a(v)) s, round(F / Q).
  *   Output  channel c's 8 blocks x 128 B leave as one 1-KiB nontemporal store.
  * The round-3 persistent kernels (k_mx, k_mx422, k_mx420) and the timing / diagnostic build knobs
- * (round-5 A/Bs and the round-6 fault probes) live in tools/probes/jpgx_mx_r5_knobs.patch:
+ * (round-4b A/Bs and the round-5 fault probes) live in tools/probes/jpgx_mx_r5_knobs.patch:
  * `patch -p1 < tools/probes/jpgx_mx_r5_knobs.patch` at the repository root restores them.
  */
 #include <hip/hip_runtime.h>
@@ -261,7 +261,7 @@ __device__ __forceinline__ double mx_dpp64(double s)
 /*
  * The x-outer / y-inner sum of the products (lane x holds the 8 of its x), F and round(F / Q).
  *
- * Fast decision (round 5): the reference's 64-term sum runs sequentially
+ * Fast decision (round 4b): the reference's 64-term sum runs sequentially
  * (dct.c:46-50), but only round(F / Q) is kept.  Each lane sums its 8 products in order, the 8
  * partial sums meet in a 3-level butterfly (every lane ends with the same total, a + b == b + a):
  * every term passes at most 10 additions.  Terms: |X| <= 171 (the Cb quirk, preprocess.c:161:
@@ -305,7 +305,7 @@ __device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch
 }
 
 /* where the exact pass's constants come from: the workgroup's LDS image and literals (MxExLds;
- * every kernel since round 6).  Round 5: a global read in the exact pass waits, through the
+ * every kernel since round 5).  Round 4b: a global read in the exact pass waits, through the
  * in-order vmcnt, for every older VMEM operation of the wave -- the later steps' pixel DMA -- so it
  * costs the wave microseconds under full HBM load. */
 struct alignas(16) MxExTab {
@@ -442,7 +442,7 @@ __device__ __forceinline__ double mx_wave_sum64(double s)
  * through at most 6 additions, fewer than the 10 mx_exact_sum's bound allows, so that bound and its
  * 2^-33 margin hold unchanged -- and t' = s R decides as mx_exact_sum's fast path.  Every lane holds
  * the same t'; returns false on a near-tie (the caller then takes the sequential 8-lane path).
- * Round 6: one instruction stream for the wave instead of eight 8-lane groups of which seven idle.
+ * Round 5: one instruction stream for the wave instead of eight 8-lane groups of which seven idle.
  */
 template <class SMP, class XT>
 __device__ __forceinline__ bool mx_exact_one(const SMP &smp, unsigned ch, unsigned u, unsigned v, const XT &xt,
@@ -486,7 +486,7 @@ __device__ __forceinline__ unsigned mx_col_block(unsigned k, unsigned sl)
 
 /* Inline exact pass of one step: every flagged coefficient (bit 8 col + v of a lane's `bits`),
  * the single-coefficient case on the whole wave, otherwise eight at a time, patching the stage.
- * (Round 5 ended it with lgkmcnt(0) against a fault that round 6 traced to packed fp32, DESIGN.md
+ * (Round 4b ended it with lgkmcnt(0) against a fault that round 5 traced to packed fp32, DESIGN.md
  * 4.3f; the wait is gone.) */
 template <class Lds, class XT>
 __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uint32_t bits,
@@ -529,7 +529,7 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
 
 /*
  * The column pass computes in SCALAR fp32 (v_add_f32 / v_fma_f32): no packed-fp32 VALU instruction
- * (v_pk_add_f32, v_pk_mul_f32, v_pk_fma_f32) is allowed in these kernels.  Round 6 found the cause
+ * (v_pk_add_f32, v_pk_mul_f32, v_pk_fma_f32) is allowed in these kernels.  Round 5 found the cause
  * of the rows-12..15 fault: on gfx950, a packed-fp32 instruction of a wave that
  * also issues MFMAs intermittently writes wrong values in lanes 48..63 -- reproduced in isolation
  * (tools/probes/pk_hazard4.hip: the packed 8-point DCT wrong in 1.7e-4 of its runs when the wave's
@@ -748,9 +748,9 @@ struct alignas(16) MxsLds {
 };
 static_assert(sizeof(MxsLds) % 16 == 0, "16-byte aligned LDS regions");
 /* the workgroup image: B operands, scale / limit table, hot-path limits (mx_limc) per lane
- * profile and column kind, zig-zag positions, the exact pass's tables (round 5: the B operands
+ * profile and column kind, zig-zag positions, the exact pass's tables (round 4b: the B operands
  * from global memory instead -- to make room -- gave wrong C rows 12..15 in 10-100 % of launches,
- * profiles/r05_exact_pass.txt; the room comes from the compact Cr tables of MxsTab) */
+ * profiles/r04b_exact_pass.txt; the room comes from the compact Cr tables of MxsTab) */
 struct alignas(16) MxsImg {
     mx_u4 B[3 * JX_MX_PARTS][64];
     MxsTab tab;
@@ -1194,7 +1194,7 @@ struct alignas(16) Mxs422Lds {
 };
 /* the LDS image: B operands [part * 3 + which][lane] (which 0: the two Y sets' operands merged --
  * B_Y0 is zero in columns 8..15, B_Y1 in 0..7, so lane l keeps set (l & 15) / 8's and the kernel
- * rebuilds the zeros; 1, 2: chroma), the scale / limit table (round 6: the band limits of the rare
+ * rebuilds the zeros; 1, 2: chroma), the scale / limit table (round 5: the band limits of the rare
  * path too, no global read there), the hot-path limits, the zig-zag positions and the exact pass's
  * tables */
 struct alignas(16) MxsImg422 {

@@ -163,7 +163,7 @@ def test_mfma_chained_operand_rule(tmp_path):
     assert independent.returncode == 0, independent.stdout
 
 
-# The acc[1] column pass right after the Cr products of the round-5 "bgl" reproducer (B operands from
+# The acc[1] column pass right after the Cr products of the round-4b "bgl" reproducer (B operands from
 # global memory at the wave's top: 20/20 launches wrong, gpurun_out/r6a), k_mxs step 0 -- every build
 # of rounds 3-5 that showed the rows-12..15 fault had this form (packed fp32 after the wave's MFMAs).
 _BGL_EXCERPT = [
@@ -203,10 +203,10 @@ def test_no_packed_fp32_rule(tmp_path):
 
 
 def test_no_packed_fp32_rule_rejects_recorded_failing_builds():
-    """every recorded failing build of the MFMA kernels (round-5 variants, built by
+    """every recorded failing build of the MFMA kernels (round-4b variants, built by
     tools/build_variants.sh from tools/probes/jpgx_mx_r5_knobs.patch) fails --no-pk, whatever the
     other rules said of it: bgl / bglpad (B from global memory), w1 (one-wave workgroups), and the
-    compact-table exact pass without its lgkmcnt(0) (ucc); the round-5 product too -- it passed by
+    compact-table exact pass without its lgkmcnt(0) (ucc); the round-4b product too -- it passed by
     timing.  Checked on the ISA files that exist in this checkout (build/variants, gitignored)."""
     tool = os.path.join(REPO, "tools", "mfma_war_check.py")
     vdir = os.path.join(PKG, "build", "variants")

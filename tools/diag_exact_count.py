@@ -1,6 +1,6 @@
 """Diagnostics (GPU box): how often each kernel's inline exact pass runs on the bench workload
 (8 x 4K splitmix frames; q90 for 4:4:4, q75 for 4:2:2 / 4:2:0), from the counting build
-(libjpgx_cnt.so: build/vsrc/cnt.hip, made by the round-6 session notes in profiles/r06_*): per
+(libjpgx_cnt.so: build/vsrc/cnt.hip, made by the round-5 session notes in profiles/r05_*): per
 launch the exact-pass entries, those the whole-wave single-coefficient path finished, the 8-lane
 batches, and the flagged coefficients.
 Usage: JPGX_LIB=.../libjpgx_cnt.so python tools/diag_exact_count.py [launches]"""

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: GPU tests on the product, then timing A/Bs (tools/gpu_r5_price.sh).
+# Round 4b: GPU tests on the product, then timing A/Bs (tools/gpu_r5_price.sh).
 # Usage: bash tools/gpu_r5_fast.sh OUT "444 variants" ["422 variants"] ["420 variants"]
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

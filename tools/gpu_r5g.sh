@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: GPU tests, wrong-launch rates (tools/diag_rate.py, every sample ratio) and the timing
+# Round 4b: GPU tests, wrong-launch rates (tools/diag_rate.py, every sample ratio) and the timing
 # A/B against the round-4 exact pass (variant r4) and the no-exact probe.  Usage: bash tools/gpu_r5g.sh OUT
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

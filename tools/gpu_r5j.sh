@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: the unchained Cr tile (product) and the unchained + compact-table variant (ucc):
+# Round 4b: the unchained Cr tile (product) and the unchained + compact-table variant (ucc):
 # GPU tests, wrong-launch rates, the golden 4K frame, timing.  Usage: bash tools/gpu_r5j.sh OUT
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5 diagnostics: wrong-launch rates of the divisors-in-LDS (qlds) and padded-image (pad)
+# Round 4b diagnostics: wrong-launch rates of the divisors-in-LDS (qlds) and padded-image (pad)
 # variants of k_mxs.  Usage: bash tools/gpu_r5k.sh OUT
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

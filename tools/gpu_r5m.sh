@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: validation of the product with the exact pass's tables in LDS (GPU tests, wrong-launch
+# Round 4b: validation of the product with the exact pass's tables in LDS (GPU tests, wrong-launch
 # rates in every mode, the golden 4K frame) and its timing against the previous product (r5head).
 # Usage: bash tools/gpu_r5m.sh OUT
 set -u

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6 fault probes: wrong-launch rates (tools/diag_rate.py, 20 x 2 x 4K q75, 4:4:4) of the
+# Round 5 fault probes: wrong-launch rates (tools/diag_rate.py, 20 x 2 x 4K q75, 4:4:4) of the
 # B-from-global (bgl*) and one-wave-workgroup (w1*) reproducers with padding after each product
 # group (pad) or every A operand kept live to the step's end (keep).  Usage: bash tools/gpu_r6a.sh OUT
 set -u

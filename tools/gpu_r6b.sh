@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6 fault probe: the dumped R / scale values of k_mxs across launches (tools/diag_dump.py) in
+# Round 5 fault probe: the dumped R / scale values of k_mxs across launches (tools/diag_dump.py) in
 # the padded and unpadded B-from-global reproducers.  Usage: bash tools/gpu_r6b.sh OUT
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: validation of the scalar column pass (no packed fp32 in the MFMA kernels): GPU tests,
+# Round 5: validation of the scalar column pass (no packed fp32 in the MFMA kernels): GPU tests,
 # wrong-launch rates in every mode, the golden 4K frame, timing against the packed build (pkd),
 # and the packed-form probe.  Usage: bash tools/gpu_r6m.sh OUT
 set -u

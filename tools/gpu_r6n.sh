@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: A/B of the next k_mxs / k_mxs420 candidates against the product, and the wrong-launch
+# Round 5: A/B of the next k_mxs / k_mxs420 candidates against the product, and the wrong-launch
 # rates of the two that break the round-4 chained-product rule (crchain, nof420) -- a direct test of
 # that rule now that packed fp32 is gone.  Usage: bash tools/gpu_r6n.sh OUT
 set -u

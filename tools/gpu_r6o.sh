@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: exact-pass counts per kernel on the bench workload (counting build).  Usage: bash tools/gpu_r6o.sh OUT
+# Round 5: exact-pass counts per kernel on the bench workload (counting build).  Usage: bash tools/gpu_r6o.sh OUT
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"

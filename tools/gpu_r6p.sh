@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: the product after the B-operand reload and without the exact pass's lgkmcnt(0): GPU
+# Round 5: the product after the B-operand reload and without the exact pass's lgkmcnt(0): GPU
 # tests, wrong-launch rates, golden frames, timing against the r6m build.  Usage: bash tools/gpu_r6p.sh OUT
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

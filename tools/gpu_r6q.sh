@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: where k_mxs420's exact-pass time goes (timing-only dissection builds).  Usage: bash tools/gpu_r6q.sh OUT
+# Round 5: where k_mxs420's exact-pass time goes (timing-only dissection builds).  Usage: bash tools/gpu_r6q.sh OUT
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"

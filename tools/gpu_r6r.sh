@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: PMC counter groups of k_mxs420 in the product and in the build without its exact pass
+# Round 5: PMC counter groups of k_mxs420 in the product and in the build without its exact pass
 # (noex420), on the 4:2:0 bench workload.  Usage: bash tools/gpu_r6r.sh OUT
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

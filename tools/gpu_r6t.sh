@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: prefilter rates (counting build cnt2) and the no-exact builds that keep every flag bit
+# Round 5: prefilter rates (counting build cnt2) and the no-exact builds that keep every flag bit
 # live (noex420b / noex444b).  Usage: bash tools/gpu_r6t.sh OUT
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

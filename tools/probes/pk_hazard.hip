@@ -1,5 +1,5 @@
 /*
- * pk_hazard.hip -- round-6 probe of the rows-12..15 fault: do packed-fp32 VALU chains
+ * pk_hazard.hip -- round-5 probe of the rows-12..15 fault: do packed-fp32 VALU chains
  * (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32) give wrong lanes on gfx950 when MFMAs run on the
  * same SIMD?  Each wave runs, per iteration, an optional burst of eight independent
  * v_mfma_f32_16x16x32_f16 products (as k_mxs's Cr group) and then a dependent chain of 16 packed

@@ -1,5 +1,5 @@
 /*
- * pk_hazard3.hip -- round-6 probe of the rows-12..15 fault, k_mxs's step structure in isolation:
+ * pk_hazard3.hip -- round-5 probe of the rows-12..15 fault, k_mxs's step structure in isolation:
  * a Y|Cb-like group of four v_mfma_f32_16x16x32_f16 products, a Cr-like group of eight independent
  * products issued behind it, then the column pass of the first tile exactly as the kernel's source
  * writes it (mx_combine: v_pk_add_f32 of the hi / lo tiles; jx_fdct8_pk: v_pk_*_f32 with op_sel

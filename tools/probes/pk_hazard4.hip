@@ -1,5 +1,5 @@
 /*
- * pk_hazard4.hip -- round-6 probe of the rows-12..15 fault: packed-fp32 VALU (jx_fdct8_pk's
+ * pk_hazard4.hip -- round-5 probe of the rows-12..15 fault: packed-fp32 VALU (jx_fdct8_pk's
  * v_pk_*_f32, as k_mxs's column pass) on one wave while OTHER waves of the same SIMD have memory
  * data returning into their VGPRs.  Workgroups alternate roles: even blocks compute (per iteration
  * optionally four + eight v_mfma_f32_16x16x32_f16 products, then the packed 8-point DCT of per-lane

@@ -1,5 +1,5 @@
 /*
- * pk_hazard5.hip -- round-6 probe: WHICH packed-fp32 form goes wrong in lanes 48..63 after the same
+ * pk_hazard5.hip -- round-5 probe: WHICH packed-fp32 form goes wrong in lanes 48..63 after the same
  * wave's MFMAs (pk_hazard4.hip: the packed DCT does, in 1.7e-4 of its runs; never without MFMAs in
  * the wave).  Each wave, per iteration: eight v_mfma_f32_16x16x32_f16 products into AGPR/VGPR
  * accumulators, per-lane pseudo-random inputs made by integer hashing (as pk_hazard4), then ONE
