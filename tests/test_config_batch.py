@@ -7,9 +7,10 @@ stitched and hashed against tests/golden/big_golden.json (the oracle restatement
 the real reference on frame 1000 and at 4K in test_oracle.py).
 
 Every stripe seam crosses the x0 = -8 quirk (src/preprocess.c:199-211: the last block of a
-block-row reads the previous pixel row, i.e. the halo row for a stripe's first block-row), and
-every launch gives each persistent wave several tiles (the multi-tile path, mid-run queue
-drains, the end-of-kernel exact pass over items of many tiles)."""
+block-row reads the previous pixel row, i.e. the halo row for a stripe's first block-row), so
+general steps (register-loaded, with the quirk block) fall at every stripe's block-row ends and
+frame ends inside one launch of k_mxs's short-lived waves (three 8-block steps per wave), with
+the inline exact pass on the flagged steps of every frame."""
 import hashlib
 import json
 import os

@@ -96,8 +96,9 @@ def test_tie_frame_every_dc_is_a_tie(cuda):
 
 def _sparse_tie(W, H, seed, every):
     """Random frame with every `every`-th block replaced by a flat tie block (gen_tie): at q50 its
-    Y DC is an exact .5 tie, so steps carry a few flagged columns -- the deferred exact pass
-    (queue of flagged columns, flushes between steps) rather than the inline one."""
+    Y DC is an exact .5 tie, so steps carry one flagged coefficient (the inline exact pass's
+    whole-wave path, whose tree sum then sees a near-tie and falls back) or several (its 8-lane
+    batches)."""
     rgb = O.gen_splitmix(seed, W, H)
     tie = O.gen_tie(W, H)
     bpr = W // 8
@@ -110,13 +111,14 @@ def _sparse_tie(W, H, seed, every):
 # Gray blocks whose rows are constant across x (only column u = 0 non-zero) with two coefficients
 # of that column at (or within 1e-5 of) a .5 boundary: at q50 v = 0 and v = 4 are both exact ties
 # (found by a search over the reference's double arithmetic), at q90 v = 1 and v = 2 -- one
-# deferred column with a multi-bit v-mask per such block.
+# column with two flagged coefficients per such block (a lane with several flag bits: the exact
+# pass's 8-lane batches, never the single-coefficient path).
 MULTI_V = {50: [[182, 101, 34, 200, 52, 82, 221, 160], [143, 34, 169, 120, 73, 231, 148, 66], [80, 198, 94, 81, 204, 128, 10, 29], [165, 172, 249, 77, 160, 231, 2, 120], [115, 230, 107, 220, 81, 126, 15, 122], [93, 65, 27, 115, 251, 160, 158, 227]],
            90: [[53, 16, 72, 210, 179, 226, 163, 184]]}
 
 
 @pytest.mark.parametrize("q", [50, 90])
-def test_deferred_multi_v_columns(cuda, q):
+def test_multi_v_flagged_columns(cuda, q):
     rgb = O.gen_splitmix(900 + q, 1024, 128)
     pats = MULTI_V[q]
     bpr = 1024 // 8
@@ -128,7 +130,7 @@ def test_deferred_multi_v_columns(cuda, q):
 
 
 @pytest.mark.parametrize("every", [5, 13, 61])
-def test_deferred_exact_queue(cuda, every):
+def test_sparse_tie_exact_pass(cuda, every):
     rgb = _sparse_tie(1024, 256, 77 + every, every)
     for q in (50, 90, 97):
         assert np.array_equal(_gpu(rgb, q, cuda), O.blocks(rgb, q)), f"q{q}"

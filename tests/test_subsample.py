@@ -123,9 +123,9 @@ def test_gpu_subsample_tie_and_flat(cuda, impl, sr):
 @pytest.mark.gpu
 @pytest.mark.parametrize("sr", [1, 2])
 @pytest.mark.parametrize("every", [5, 29])
-def test_gpu_subsample_deferred_queue(cuda, impl, sr, every):
-    """sparse flat tie blocks in a random frame: few flagged columns per step (the deferred
-    queue of flagged columns and its flushes), Y and chroma"""
+def test_gpu_subsample_sparse_ties(cuda, impl, sr, every):
+    """sparse flat tie blocks in a random frame: one or a few flagged coefficients per step (the
+    inline exact pass's whole-wave path and its 8-lane batches), Y and chroma"""
     rgb = O.gen_splitmix(500 + every, 1024, 256)
     tie = O.gen_tie(1024, 256)
     for bi in range(3, 128 * 32, every):
@@ -137,9 +137,9 @@ def test_gpu_subsample_deferred_queue(cuda, impl, sr, every):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sr", [1, 2])
-def test_gpu_subsample_deferred_multi_v(cuda, impl, sr):
+def test_gpu_subsample_multi_v(cuda, impl, sr):
     """Y blocks whose column u = 0 holds two flagged coefficients (test_gpu_parity.MULTI_V at q50):
-    deferred Y columns with multi-bit v-masks beside the chroma of the same MCUs"""
+    Y columns with several flag bits (8-lane batches) beside the chroma of the same MCUs"""
     from test_gpu_parity import MULTI_V
     rgb = O.gen_splitmix(940 + sr, 1024, 128)
     pats = MULTI_V[50]
@@ -248,8 +248,8 @@ def test_gpu_sub420_partial_tiles_and_frames(cuda, impl, W, H):
 def test_gpu_sub422_small_rows(cuda, impl, W, H, F, kind):
     """Block-rows of 2, 6, 10 and 18 blocks: several row-last (x0 = -8 quirk) Y blocks in one
     8-block step, MCUs whose right block is the quirk block, steps across rows and frames and a
-    partial last step; tie frames flag chroma coefficients there (deferred exact pass), FORCE_EXACT
-    sends every coefficient through the inline exact pass."""
+    partial last step; tie frames flag chroma coefficients there (the inline exact pass reads a
+    quirk MCU's right half from its true rows), FORCE_EXACT sends every coefficient through it."""
     import torch
     q = 50 if kind == "tie" else 85
     frames = [O.gen_tie(W, H) if kind == "tie" else O.gen_splitmix(500 + W + f, W, H)
@@ -279,8 +279,9 @@ def test_gpu_sub420_small_rows(cuda, impl, W, H, F, kind):
     """MCU rows of 1, 3, 5, 9 and 25 MCUs: every MCU or many of them the row's last (x0 = -8
     quirk in both block rows of its right column), steps and step pairs across MCU rows and
     frames, an odd MCU count (a pair whose second step lies past the end); tie frames flag
-    chroma coefficients (deferred exact pass from global memory), FORCE_EXACT sends every
-    coefficient through the inline pass; a sentinel region after the output must stay intact."""
+    chroma coefficients (the inline exact pass: a general pair's MCUs from global memory, a simple
+    pair's from its LDS slots), FORCE_EXACT sends every coefficient through it; a sentinel region
+    after the output must stay intact."""
     import torch
     q = 50 if kind == "tie" else 85
     frames = [O.gen_tie(W, H) if kind == "tie" else O.gen_splitmix(700 + W + f, W, H)
