@@ -310,6 +310,7 @@ __device__ __forceinline__ int mx_exact_sum(const double (&prod)[8], unsigned ch
  * costs the wave microseconds under full HBM load. */
 struct alignas(16) MxExTab {
     double cosx_[8][8];                 /* the glibc cosines (JX_COS_INIT, jx_consts.h)  */
+    double r_[2][64];                   /* jx_mxtab.r: fl(K / Q), the fast decision's R   */
     int16_t q_[2][64];                  /* jx_mxtab.q of the workgroup's quality     */
 };
 struct MxExLds {
@@ -333,8 +334,8 @@ struct MxExLds {
     }
     /* the transposed divisor Q of quantise.c:58 (channel class c: 0 luminance, 1 chrominance) */
     __device__ double div(unsigned c, unsigned i) const { return (double)X.q_[c][i]; }
-    /* jx_mxtab.r: fl(K / Q), the same IEEE operations as the host's */
-    __device__ double recip(unsigned c, unsigned i) const { return kfac(i) / div(c, i); }
+    /* jx_mxtab.r: fl(K / Q), computed on the host (mx_fill_recip) */
+    __device__ double recip(unsigned c, unsigned i) const { return X.r_[c][i]; }
     __device__ unsigned scan(unsigned u, unsigned v) const { return scan_t[u][v]; }
 };
 
@@ -731,7 +732,7 @@ __device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t,
  * profiles/r03_skeleton_wgrank.txt; the memory skeleton reads 0.72-0.76 non-persistent vs
  * 0.67-0.70 persistent, profiles/r04_*).  What a short wave needs is a cheap start:
  *   - its pixel DMA for all three steps is issued first (step k lives in slot k);
- *   - the B operands (6 KiB, quality-independent), this quality's scale / limit table with the
+ *   - the B operands (4 KiB, quality-independent; the two Cr sets' operands merged), this quality's scale / limit table with the
  *     hot-path band limits, the zig-zag positions and the exact pass's tables are one pre-laid-out
  *     image (g_mxs_img) that the workgroup's four waves copy into LDS with LDS-DMA (16-byte
  *     pieces), one s_barrier;
@@ -752,7 +753,7 @@ static_assert(sizeof(MxsLds) % 16 == 0, "16-byte aligned LDS regions");
  * from global memory instead -- to make room -- gave wrong C rows 12..15 in 10-100 % of launches,
  * profiles/r04b_exact_pass.txt; the room comes from the compact Cr tables of MxsTab) */
 struct alignas(16) MxsImg {
-    mx_u4 B[3 * JX_MX_PARTS][64];
+    mx_u4 B[2 * JX_MX_PARTS][64];       /* [part * 2 + which]: Y|Cb, the two Cr sets merged */
     MxsTab tab;
     float limc[2][16];
     uint8_t scan_t[8][8];               /* zig-zag position of (v, u) at [u][v] */
@@ -922,9 +923,12 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
     mx_u4 B[kParts][3];
     const auto load_b = [&](unsigned l) __attribute__((always_inline)) {
 #pragma unroll
-        for (int p = 0; p < kParts; p++)
-#pragma unroll
-            for (int w = 0; w < 3; w++) B[p][w] = s_img.B[3 * p + w][l];
+        for (int p = 0; p < kParts; p++) {
+            const mx_u4 bc = s_img.B[2 * p + 1][l], zero = {};
+            B[p][0] = s_img.B[2 * p][l];
+            B[p][1] = (l & 15u) < 8 ? bc : zero;
+            B[p][2] = (l & 15u) < 8 ? zero : bc;
+        }
     };
     load_b(lane);
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
@@ -1995,6 +1999,7 @@ void mx_ex_tab(MxExTab &x, const jx_mxtab &t)
     static const double cosx[8][8] = JX_COS_INIT;
     memcpy(x.cosx_, cosx, sizeof cosx);
     memcpy(x.q_, t.q, sizeof t.q);
+    memcpy(x.r_, t.r, sizeof t.r);
 }
 
 std::once_flag g_mx_once[kMaxDev];
@@ -2020,7 +2025,17 @@ int mx_tables_for_current_device()
                 for (int q = 1; q <= JX_MAXQ; q++) {
                     MxsImg &I = img[f * (JX_MAXQ + 1) + q];
                     const jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
-                    memcpy(I.B, ops, sizeof I.B);
+                    for (int p = 0; p < JX_MX_PARTS; p++)
+                        for (unsigned l = 0; l < 64; l++) {
+                            /* the Cr sets' operands are zero in opposite column halves (B1 in
+                             * 8..15, B2 in 0..7): lane l keeps set (l & 15) / 8's */
+                            const bool set0 = (l & 15u) < 8;
+                            const uint16_t *keep = ops[3 * p + (set0 ? 1 : 2)][l], *zero = ops[3 * p + (set0 ? 2 : 1)][l];
+                            for (int e = 0; e < 8; e++)
+                                if (zero[e]) rc = JPGX_EARG;
+                            memcpy(&I.B[2 * p][l], ops[3 * p][l], 16);
+                            memcpy(&I.B[2 * p + 1][l], keep, 16);
+                        }
                     mx_ex_tab(I.ex, t);
                     MxTab full;
                     mx_layout_tab(full, t, [](unsigned tt, unsigned jp) { return tt < 2 ? jp : 16u + (jp & 7u); });
@@ -2035,7 +2050,7 @@ int mx_tables_for_current_device()
                     }
                     mx_scan_t(I.scan_t);
                 }
-            rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs_img), img.data(), img.size() * sizeof(MxsImg)));
+            if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs_img), img.data(), img.size() * sizeof(MxsImg)));
         }
         g_mx_rc[dev] = rc;
     });
@@ -2113,7 +2128,7 @@ int mx420_tables_for_current_device()
                 mx_scan_t(img[i].scan_t);
                 mx_ex_tab(img[i].ex, tab[i]);
             }
-            rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs420_img), img.data(), img.size() * sizeof(MxsImg420)));
+            if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs420_img), img.data(), img.size() * sizeof(MxsImg420)));
         }
         g_mx420_rc[dev] = rc;
     });
