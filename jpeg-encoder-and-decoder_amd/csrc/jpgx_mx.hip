@@ -909,7 +909,10 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
     mx_wait_vm<2u * kMxsC>();
     __builtin_amdgcn_s_barrier();
     mx_wave_sync();
-    if (cmp.b >= g.total) return;
+    if (cmp.b >= g.total) {
+        mx_wait_vm<0>();                                /* no LDS-DMA outlives the wave */
+        return;
+    }
     /* stage addresses of this lane's column at v = 0..7: the zig-zag positions from the image (no
      * global load: its wait would drain the pixel DMA too) */
     uint32_t za[8];
@@ -1051,7 +1054,10 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
      * stores */
     const auto step = [&](auto kc) __attribute__((always_inline)) {
         constexpr unsigned k = decltype(kc)::value;
-        if (cmp.b >= g.total) return;
+        if (cmp.b >= g.total) {
+            mx_wait_vm<0>();                            /* no LDS-DMA outlives the wave */
+            return;
+        }
         mx_wait_vm<2 * (kMxsC - 1 - k) + 3 * k>();
         body(cmp, L.ring[k]);
         mxs_next(cmp, g);
@@ -1275,7 +1281,10 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
     mx_wait_vm<2u * kMxs422C>();                    /* the image (older than the pixel DMA) */
     __builtin_amdgcn_s_barrier();
     mx_wave_sync();
-    if (cmp.b >= g.total) return;
+    if (cmp.b >= g.total) {
+        mx_wait_vm<0>();                                /* no LDS-DMA outlives the wave */
+        return;
+    }
     uint32_t za[8];
     {
         const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * ((j >> 3) * 4u + gq);
@@ -1413,7 +1422,10 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
     };
     const auto step = [&](auto kc) __attribute__((always_inline)) {
         constexpr unsigned k = decltype(kc)::value;
-        if (cmp.b >= g.total) return;
+        if (cmp.b >= g.total) {
+            mx_wait_vm<0>();                            /* no LDS-DMA outlives the wave */
+            return;
+        }
         mx_wait_vm<2 * (kMxs422C - 1 - k) + 2 * k>();
         body(cmp, L.ring[k]);
         mxs_next(cmp, g);
@@ -1567,14 +1579,15 @@ __device__ __forceinline__ unsigned mx420_pm(unsigned gq) { return (gq & 1u) * 2
  * or launch ends) read their pixels from global memory. */
 template <class Lds, class XT>
 __device__ __forceinline__ void mx420_exact_inline(Lds &L, const uint8_t *sp, uint32_t bits, unsigned mp,
-                                                   bool simple, const MxG &g, const Mx420G &h, const XT &xt)
+                                                   bool simple, const uint8_t *ps0, const uint8_t *ps1,
+                                                   const MxG &g, const Mx420G &h, const XT &xt)
 {
     const unsigned lane = mx_lane();
     mx_wave_sync();
     const auto chroma = [&](unsigned gq, auto &&fn) __attribute__((always_inline)) {
         const unsigned pm = mx420_pm(gq);
         if (simple)
-            return fn(MxSmp4<lds_u8, unsigned>{mx_lds(L.ring[pm >> 1]) + 48u * (pm & 1u), 96u});
+            return fn(MxSmp4<lds_u8, unsigned>{mx_lds((void *)((pm >> 1) ? ps1 : ps0)) + 48u * (pm & 1u), 96u});
         unsigned m = mp + pm;
         m = m < h.tm ? m : h.tm - 1u;
         return fn(MxSmp4<uint8_t, long long>{mx420_mcu_src(g, h, m), g.pitch});
@@ -1633,22 +1646,24 @@ __device__ __forceinline__ unsigned mx420_yblock(const MxG &g, const Mx420G &h, 
 }
 
 struct alignas(16) Mxs420Lds {
-    uint8_t ring[2][kSlot];             /* [y 0..15][4 blocks x 24 B] */
+    uint8_t ring[3][kSlot];             /* [y 0..15][4 blocks x 24 B]: steps 0, 1, 2; step 3 reuses slot 0 */
     union {
         uint8_t stage[16 * kBS];
         struct {                        /* general step: MCU's right column, true rows [16][24]; read
-                                           for the A operands before the chroma column writes here */
-            uint8_t y_[kSt420C];
+                                           for the A operands before the Y column writes here */
             uint8_t qtrue[2][384];
+            uint8_t y_[kSt420C - 2 * 384];
+            mx_f4 rA[64];               /* a pair's first chroma R tile, in the chroma stage (written
+                                           at the end of the pair's first step, read before the
+                                           pair's chroma column writes there) */
         };
     };
-    mx_f4 rA[64];                       /* step 0's chroma R (not held across step 0's exact pass) */
     uint16_t task[8];
 };
-static_assert(2 * 384 <= 16 * kBS - kSt420C, "qtrue inside the chroma stage");
+static_assert(2 * 384 <= kSt420C && 64 * 16 <= 16 * kBS - kSt420C, "qtrue in the Y stage, rA in the chroma stage");
 constexpr unsigned kMxs420WPG = 4;
 struct alignas(16) MxsImg420 {
-    mx_u4 B[JX_MX_PARTS * 5][64];
+    mx_u4 B[JX_MX_PARTS * 4][64];       /* [part * 4 + which]: the two Y sets merged (as k_mxs422), chroma K steps */
     MxTab tab;
     float limc[2][16];
     uint8_t scan_t[8][8];
@@ -1701,21 +1716,34 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
                 mxs_dma<16>(img + 16u * piece, (uint8_t *)&s_img + 16u * (64u * kMxs420WPG * i + 64u * wave));
         }
     }
-    /* the pair: MCUs m0 .. m0 + 3; simple = one MCU row of one frame, no row-last MCU, in range */
-    const unsigned m0 = 4u * (blockIdx.x * kMxs420WPG + wave);
+    /* two pairs: MCUs m0 .. m0 + 3 and m0 + 4 .. m0 + 7; simple = one MCU row of one frame, no
+     * row-last MCU, in range (per pair) */
+    const unsigned m0 = 8u * (blockIdx.x * kMxs420WPG + wave);
     const uint32_t off0 = (uint32_t)((lane / 6u) * (unsigned)g.pitch + 16u * (lane % 6u));
     const uint32_t off1 = (uint32_t)(((64u + lane) / 6u) * (unsigned)g.pitch + 16u * ((64u + lane) % 6u));
+    /* the current pair's cursor; of pair 1 only its pixel pointer is kept until its steps (SGPRs) */
     Mx420Chunk cc;
-    bool simple = false;
-    if (m0 < h.tm) {
-        mx420_at(cc, g, h, m0);
-        simple = m0 + 4u <= h.tm && cc.mx + 4u < h.mpr && g.lin_store;
-    }
+    bool simple[2] = {false, false};
+    const uint8_t *src1 = g.rgb;
 #pragma unroll
-    for (unsigned k = 0; k < 2; k++) {
-        if (simple) {
-            mxs_dma<16>(cc.src + 96u * k + off0, L.ring[k]);
-            if (lane < 32) mxs_dma<16>(cc.src + 96u * k + off1, L.ring[k] + 1024u);
+    for (unsigned pp = 0; pp < 2; pp++) {
+        const unsigned mp = m0 + 4u * pp;
+        if (mp < h.tm) {
+            mx420_at(cc, g, h, mp);
+            simple[pp] = mp + 4u <= h.tm && cc.mx + 4u < h.mpr && g.lin_store;
+            if (pp == 1) src1 = cc.src;
+        }
+    }
+    if (m0 < h.tm) mx420_at(cc, g, h, m0);
+    /* steps 0, 1 (pair 0) and 2 (pair 1's first) into slots 0..2 now; step 3 into slot 0 after
+     * pair 0 is done (mx420_dma3) */
+#pragma unroll
+    for (unsigned k = 0; k < 3; k++) {
+        const unsigned pp = k >> 1, ks = k & 1u;
+        const uint8_t *src = pp ? src1 : cc.src;
+        if (simple[pp]) {
+            mxs_dma<16>(src + 96u * ks + off0, L.ring[k]);
+            if (lane < 32) mxs_dma<16>(src + 96u * ks + off1, L.ring[k] + 1024u);
         } else {
             mxs_dma<4>(g.rgb, L.ring[k]);                   /* padding: filled at compute time */
             mxs_dma<4>(g.rgb, L.ring[k]);
@@ -1736,10 +1764,13 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
     const uint32_t rc = kSt420C + kBS * (4u * (lane >> 5) + mx420_pm((lane >> 3) & 3u)) + (lane & 7u) * 16u;
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
 
-    mx_wait_vm<4>();                                    /* the image (older than the pixel DMA) */
+    mx_wait_vm<6>();                                    /* the image (older than the pixel DMA) */
     __builtin_amdgcn_s_barrier();
     mx_wave_sync();
-    if (m0 >= h.tm) return;
+    if (m0 >= h.tm) {
+        mx_wait_vm<0>();                                /* no LDS-DMA outlives the wave */
+        return;
+    }
     uint32_t za[8];
     {
         const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * (4u * (j >> 3) + gq);
@@ -1747,13 +1778,17 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
 #pragma unroll
         for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
     }
-    /* the B operands; reloaded after step 0's exact pass, so that their registers are free during it */
+    /* the B operands; reloaded after an exact pass, so that their registers are free during it */
     mx_u4 B[kParts][5];
     const auto load_b = [&](unsigned l) __attribute__((always_inline)) {
 #pragma unroll
-        for (int p = 0; p < kParts; p++)
+        for (int p = 0; p < kParts; p++) {
+            const mx_u4 by = s_img.B[4 * p][l], zero = {};
+            B[p][0] = (l & 15u) < 8 ? by : zero;
+            B[p][1] = (l & 15u) < 8 ? zero : by;
 #pragma unroll
-            for (int w = 0; w < 5; w++) B[p][w] = s_img.B[5 * p + w][l];
+            for (int w = 2; w < 5; w++) B[p][w] = s_img.B[4 * p + w - 1][l];
+        }
     };
     load_b(lane);
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
@@ -1762,15 +1797,28 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
 
     const auto step = [&](auto kc) __attribute__((always_inline)) {
         constexpr unsigned k = decltype(kc)::value;
-        constexpr bool second = k == 1;
-        const unsigned ms = m0 + 2u * k;                /* the step's first MCU */
+        constexpr unsigned pp = k >> 1, slot = k == 3 ? 0u : k;
+        constexpr bool second = (k & 1u) != 0;
+        const unsigned mp = m0 + 4u * pp;               /* the pair's first MCU */
+        const unsigned ms = mp + 2u * (k & 1u);         /* the step's first MCU */
+        if (mp >= h.tm) {
+            mx_wait_vm<0>();
+            return;
+        }
+        /* the step's DMA has landed: younger are 4 / 2 + 1 / 1 + 2 + 2 / 1 operations */
         if (k == 0)
-            mx_wait_vm<2>();                            /* younger: step 1's DMA */
+            mx_wait_vm<4>();
+        else if (k == 1)
+            mx_wait_vm<3>();
+        else if (k == 2)
+            mx_wait_vm<5>();
         else
-            mx_wait_vm<1>();                            /* younger: step 0's Y store */
-        uint8_t *const sp = L.ring[k];
-        if (!simple) mx420_issue_general(g, h, ms, sp);     /* register path; waits vmcnt(0) */
-        const uint32_t qmask = simple ? 0u : mx420_true_rows(L, g, h, ms);
+            mx_wait_vm<1>();
+        const bool simp = simple[pp];
+        if (k == 2) mx420_at(cc, g, h, mp);             /* pair 1's cursor */
+        uint8_t *const sp = L.ring[slot];
+        if (!simp) mx420_issue_general(g, h, ms, sp);      /* register path; waits vmcnt(0) */
+        const uint32_t qmask = simp ? 0u : mx420_true_rows(L, g, h, ms);
         mx_wave_sync();
         const mx_f4 z = {};
         uint32_t fl = 0;
@@ -1796,8 +1844,6 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
             c2 = *(const mx_u2 *)p2;
         }
         __builtin_amdgcn_sched_barrier(0);
-        /* every A operand before the first product; all operands stay live until the products are
-         * done (mx_keep_ops after the Y column's fence) */
         const mx_h8 Al0 = mx_aop(y00, s0, s1, s2), Ah0 = mx_aop(y01, s0, s1, s2);
         const mx_h8 Al1 = mx_aop(y10, s0, s1, s2), Ah1 = mx_aop(y11, s0, s1, s2);
         __builtin_amdgcn_sched_barrier(0);
@@ -1818,8 +1864,6 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        /* the Y products are done before anything writes a register again: a chained product may
-         * wait in the matrix pipe and read its operands late (profiles/r04_mfma_valu_war.txt) */
         mx_fence_all(accY);
         mx_keep(midY);
         mx_keep_ops(Al1, Ah1);
@@ -1841,7 +1885,6 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        /* the same for the chroma products */
         mx_fence_all(accC);
         mx_keep(midC);
         mx_keep_ops(C1, C2);
@@ -1870,15 +1913,15 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
             {   /* clamped MCUs past the launch's end: no tasks */
                 if (ms + (gq >> 1) >= h.tm) fl &= ~0xffu;
-                if (m0 + mx420_pm(gq) >= h.tm) fl &= ~0xff00u;
+                if (mp + mx420_pm(gq) >= h.tm) fl &= ~0xff00u;
             }
-            mx420_exact_inline(L, sp, fl, m0, simple, g, h, xt);
-            if (!second) load_b(mx_lane());
+            mx420_exact_inline(L, sp, fl, mp, simp, L.ring[pp ? 2 : 0], L.ring[pp ? 0 : 1], g, h, xt);
+            if (k < 3) load_b(mx_lane());
         }
         /* stores: the Y store; on the second step also the pair's chroma */
-        if (simple) {
+        if (simp) {
             const mx_u4 vy = *(const mx_u4 *)(L.stage + ro);
-            __builtin_nontemporal_store(vy, (mx_u4 *)((const uint8_t *)(cc.ydst + 256u * k) + soy));
+            __builtin_nontemporal_store(vy, (mx_u4 *)((const uint8_t *)(cc.ydst + 256u * (k & 1u)) + soy));
             if (second) {
                 const mx_u4 vc = *(const mx_u4 *)(L.stage + rc);
                 __builtin_nontemporal_store(vc, (mx_u4 *)((const uint8_t *)cc.cdst + soc));
@@ -1896,7 +1939,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
                         vy, (mx_u4 *)(g.out + (long long)f * g.ofstride + (long long)bi * 64 + (l & 7u) * 8));
             }
             if (second) {
-                const unsigned pm = (l >> 3) & 3u, mm = m0 + pm;
+                const unsigned pm = (l >> 3) & 3u, mm = mp + pm;
                 const unsigned mc = mm < h.tm ? mm : h.tm - 1u;
                 unsigned f, mi, my, mx;
                 mx420_mcu(h, mc, f, mi, my, mx);
@@ -1909,9 +1952,39 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
             }
         }
         mx_wave_sync();
+        if (k == 1) {
+            /* pair 0 is done with slot 0 (its chroma exact pass read it): step 3's pixels into it,
+             * from inline asm so that the compiler does not drain vmcnt before step 2's LDS reads
+             * (it does after a builtin LDS-DMA, not knowing which bytes it writes).  The asm sets
+             * M0, which the compiler treats as reserved: no instruction of the kernel after this
+             * point reads M0 (the builtin LDS-DMAs are all in the prologue; checked in the ISA by
+             * tests/test_isa.py). */
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+            const uint32_t l0 = (uint32_t)(uintptr_t)mx_lds(L.ring[0]);
+            if (m0 + 4u < h.tm && simple[1]) {
+                const uint8_t *src = src1 + 96u + off0;
+                asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(l0)
+                             : "memory", "m0");
+                const uint8_t *srcb = src1 + 96u + off1;
+                const uint32_t l1 = l0 + 1024u;
+                if (lane < 32)
+                    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(srcb), "s"(l1)
+                                 : "memory", "m0");
+            } else {
+                asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g.rgb), "s"(l0)
+                             : "memory", "m0");
+                asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g.rgb), "s"(l0)
+                             : "memory", "m0");
+            }
+#pragma clang diagnostic pop
+        }
     };
     step(std::integral_constant<unsigned, 0>{});
     step(std::integral_constant<unsigned, 1>{});
+    step(std::integral_constant<unsigned, 2>{});
+    step(std::integral_constant<unsigned, 3>{});
 }
 
 int mx_rc(hipError_t e) { return e == hipSuccess ? JPGX_OK : JPGX_EHIP; }
@@ -2119,7 +2192,15 @@ int mx420_tables_for_current_device()
             std::vector<MxsImg420> img(2 * (JX_MAXQ + 1));
             memset(img.data(), 0, img.size() * sizeof(MxsImg420));
             for (size_t i = 0; i < img.size(); i++) {
-                memcpy(img[i].B, ops, sizeof img[i].B);
+                for (int p = 0; p < JX_MX_PARTS; p++)
+                    for (unsigned l = 0; l < 64; l++) {
+                        const bool set0 = (l & 15u) < 8;   /* the Y sets' zero halves (as k_mxs422) */
+                        const uint16_t *keep = ops[p][set0 ? 0 : 1][l], *zero = ops[p][set0 ? 1 : 0][l];
+                        for (int e = 0; e < 8; e++)
+                            if (zero[e]) rc = JPGX_EARG;
+                        memcpy(&img[i].B[4 * p][l], keep, 16);
+                        for (int w = 2; w < 5; w++) memcpy(&img[i].B[4 * p + w - 1][l], ops[p][w][l], 16);
+                    }
                 mx_layout_tab(img[i].tab, tab[i], [](unsigned tt, unsigned jp) { return tt < 2 ? (jp & 7u) : 8u + jp; });
                 for (unsigned jp = 0; jp < 16; jp++) {
                     img[i].limc[0][jp] = mx_limc(img[i].tab, 1, jp);
@@ -2144,7 +2225,7 @@ extern "C" int jx_launch_mx420(const jx_xform_args *xa, void *stream)
     const int rc = mx420_tables_for_current_device();
     if (rc) return rc;
     const size_t mcus = (size_t)xa->g.nb / 4 * (size_t)xa->g.nframes;
-    const size_t waves = (mcus + 3) / 4;
+    const size_t waves = (mcus + 7) / 8;
     hipLaunchKernelGGL(k_mxs420, dim3((unsigned)((waves + kMxs420WPG - 1) / kMxs420WPG)), dim3(64 * kMxs420WPG), 0,
                        (hipStream_t)stream, *xa);
     return mx_rc(hipGetLastError());

@@ -46,6 +46,40 @@ def test_mfma_operand_rule(tmp_path):
         assert int(re.search(r"\.private_segment_fixed_size:\s+(\d+)", meta).group(1)) == 0, n
         assert int(re.search(r"\.sgpr_spill_count:\s+(\d+)", meta).group(1)) == 0, n
         assert int(m.group(2)) == 0, n
+    # k_mxs420 issues its fourth step's LDS-DMA from inline asm that sets M0, a register the
+    # compiler treats as reserved: every compiler-emitted reader of M0 (a builtin LDS-DMA, or an
+    # instruction naming m0 as a source) must follow its own M0 write in the same basic block, with
+    # no inline asm in between
+    for n in ("k_mxs", "k_mxs422", "k_mxs420"):
+        assert _m0_readers_unsafe(text, n) == [], n
+
+
+def _m0_readers_unsafe(text, kernel):
+    m = re.search(r"^(_Z[^\s:]*\d%sE[^\s:]*):" % kernel, text, re.M)
+    body = text[m.end():text.find(".Lfunc_end", m.end())].splitlines()
+    bad, m0_set, in_asm = [], False, False
+    for ln in body:
+        t = ln.strip()
+        if t.startswith(";;#ASMSTART"):
+            in_asm, m0_set = True, False
+            continue
+        if t.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if in_asm or not t or t.startswith(";") or t.startswith("."):
+            if re.match(r"^\.LBB\w+:", t):
+                m0_set = False                 # a new basic block: M0 unknown again
+            continue
+        ops = t.split(None, 1)
+        op, rest = ops[0], (ops[1] if len(ops) > 1 else "")
+        dst = rest.split(",")[0].strip()
+        if dst == "m0" and op.startswith("s_"):
+            m0_set = True
+            continue
+        reads_m0 = "_lds_" in op or op.endswith("_lds") or re.search(r"\bm0\b", rest) is not None
+        if reads_m0 and not m0_set:
+            bad.append(t)
+    return bad
 
 
 def test_mfma_operand_rule_catches_a_violation(tmp_path):
@@ -221,3 +255,24 @@ def test_no_packed_fp32_rule_rejects_recorded_failing_builds():
     if seen == 0:
         import pytest
         pytest.skip("no variant ISA in this checkout")
+
+
+def test_m0_rule_catches_a_reader_after_asm():
+    fake = """_ZN12_GLOBAL__N_18k_fakeE13jx_xform_args:
+\ts_mov_b32 m0, s4
+\tglobal_load_lds_dwordx4 v[2:3], off
+\t;;#ASMSTART
+\ts_mov_b32 m0, s9
+\tglobal_load_lds_dwordx4 v[4:5], off
+\t;;#ASMEND
+\tglobal_load_lds_dwordx4 v[6:7], off
+\ts_add_i32 m0, s4, 0x400
+\tglobal_load_lds_dwordx4 v[6:7], off
+.LBB0_1:
+\tglobal_load_lds_dword v[8:9], off
+\tv_readlane_b32 s2, v1, m0
+.Lfunc_end0:
+"""
+    bad = _m0_readers_unsafe(fake, "k_fake")
+    assert bad == ["global_load_lds_dwordx4 v[6:7], off", "global_load_lds_dword v[8:9], off",
+                   "v_readlane_b32 s2, v1, m0"], bad
