@@ -278,10 +278,13 @@ def main():
     ap.add_argument("--input-sets", type=int, default=2,
                     help="copies of the input batch read by consecutive steps in turn (1 = the "
                          "same input every step, which the Infinity Cache partly holds)")
-    ap.add_argument("--settle-ms", type=float, default=200.0,
+    ap.add_argument("--settle-ms", type=float, default=1000.0,
                     help="after the W warmup steps, keep stepping (untimed) until this much time "
                          "has passed, so the timed steps see the GPU's loaded steady state and not "
-                         "its ramp out of idle (about 20 ms of load; profiles/r02_ramp.json); 0 = off")
+                         "its ramp out of idle (about 20 ms of load; profiles/r02_ramp.json) -- and "
+                         "a rocprofv3 summary of the same command averages mostly steady-state "
+                         "launches (with 200 ms the ramp's ~150 slow launches raised the mean by "
+                         "~3 %%); 0 = off")
     ap.add_argument("--frames-per-gpu", type=int, default=8)
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
