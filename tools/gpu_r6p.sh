@@ -12,4 +12,4 @@ timeout -k 10 400 python tools/diag_rate.py ${N:-100} 0 1 2 > "$OUT/rate_product
 grep -v amdgpu.ids "$OUT/rate_product.txt"
 timeout -k 10 300 python tools/diag_golden.py 8 > "$OUT/golden_product.txt" 2>&1 || exit $?
 grep -E "^q" "$OUT/golden_product.txt" | sort | uniq -c | head -4
-ROUNDS=2 bash tools/gpu_r5_price.sh "$1" "r5a" "r5a" "r5a" || exit $?
+ROUNDS=3 bash tools/gpu_r5_price.sh "$1" "r5b" || exit $?
