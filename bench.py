@@ -221,6 +221,25 @@ def check_output(d_out, plan, W, H, q, subsample, world, device, jpgx):
             "against": "tests/golden/big_golden.json batch64_4k_q90 (frame 0, all stripes)"}
 
 
+def repeat_check(step, d_out, launches, world, device):
+    """After the golden check: `launches` more launches (alternating input sets, identical
+    content), each compared on the GPU with the checked output -- a wrong-output fault that
+    comes and goes from launch to launch would show here on every bench run.
+    Counts are summed over ranks."""
+    import torch
+    import torch.distributed as dist
+    ref = d_out.clone()
+    wrong = torch.zeros((), dtype=torch.int64, device=d_out.device)
+    for _ in range(launches):
+        step()
+        wrong += torch.ne(d_out, ref).any().to(torch.int64)
+    n = torch.tensor([launches, int(wrong.item())], dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(n)
+    del ref
+    return {"repeat_launches": int(n[0]), "repeat_launches_differing": int(n[1])}
+
+
 ALT_LIB = os.path.join(REPO, "jpeg-encoder-and-decoder_amd", "lib", "libjpgx_alt.so")
 
 
@@ -290,6 +309,9 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--quality", type=int, default=90)
     ap.add_argument("--sample-ratio", type=int, default=0)
+    ap.add_argument("--verify-launches", type=int, default=256,
+                    help="after the timed region and the golden check, this many more launches "
+                         "compared with the checked output on the GPU (0 = off)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel", choices=["xform", "mx"], default=None,
@@ -413,6 +435,13 @@ def main():
     achieved = bytes_per_px * px_rank_step / (xform_ms * 1e-3) / 1e9
 
     check = check_output(d_out, plan, W, H, q, args.subsample, world, cdev, jpgx)
+    if args.verify_launches > 0:
+        rep = repeat_check(step, d_out, args.verify_launches, world, cdev)
+        if check is None:          # no committed golden at this config: self-consistency only
+            check = {"frames_checked": 0, "ok": True,
+                     "against": "the last timed launch's output (no committed golden at this config)"}
+        check.update(rep)
+        check["ok"] = check["ok"] and rep["repeat_launches_differing"] == 0
     if rank == 0:
         t_ratio, t_src = measured_traffic(kname) if not args.subsample else (None, None)
         cpu = None

@@ -28,6 +28,8 @@ def test_bench_single_gpu_line():
     d = _line(r.stdout)
     assert KEYS <= d.keys() and d["n_gpus"] == 1
     assert d["output_check"]["ok"] and d["output_check"]["frames_checked"] == 8
+    assert d["output_check"]["repeat_launches"] == 256
+    assert d["output_check"]["repeat_launches_differing"] == 0
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel"] == "k_mxs"
 
@@ -44,6 +46,7 @@ def test_bench_two_ranks_rehearsal():
     assert d["n_gpus"] == 2 and d["config"]["global_batch_frames"] == 4
     assert d["cpu_baseline"] is None
     assert d["output_check"]["ok"] and "all stripes" in d["output_check"]["against"]
+    assert d["output_check"]["repeat_launches"] == 2 * 256        # summed over the ranks
 
 
 def test_bench_refuses_more_gpus_than_the_node_has():

@@ -113,3 +113,19 @@ def test_bench_output_check_single_rank():
     res = bench.check_output(d_out, plan, 3840, 2160, 90, False, 1, None, jpgx)
     assert not res["ok"] and res["frames_wrong"] == [1001]
     assert bench.check_output(d_out, plan, 1920, 1080, 90, False, 1, None, jpgx) is None
+
+
+def test_bench_repeat_check_counts_differing_launches():
+    """bench.py's repeated-launch check: every launch after the checked one is compared with it."""
+    import torch
+
+    import bench
+    d_out = torch.arange(64, dtype=torch.int16).view(1, 1, 64).clone()
+    calls = [0]
+
+    def step():
+        calls[0] += 1
+        d_out[0, 0, 5] = 5 if calls[0] not in (3, 7) else -1      # launches 3 and 7 differ
+
+    res = bench.repeat_check(step, d_out, 10, 1, torch.device("cpu"))
+    assert res == {"repeat_launches": 10, "repeat_launches_differing": 2} and calls[0] == 10
