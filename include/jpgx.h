@@ -153,6 +153,16 @@ size_t jpgx_entropy_workspace_size(size_t nb_y, size_t nb_c);
 int jpgx_entropy_stats_gpu(const int16_t *d_coef, size_t nb_y, size_t nb_c, const int32_t *carry,
                            int32_t *d_dc, uint32_t *d_hist, void *d_workspace,
                            size_t workspace_bytes, void *stream);
+/* The same over a batch of nframes independent images of one size in one set of launches (what
+ * jpgx_blocks_gpu writes for a frame batch: frame f's coefficients at d_coef + f *
+ * coef_frame_stride int16 elements, a multiple of 64 and >= (nb_y + 2 nb_c) 64): d_dc
+ * [nframes][nb_y + 2 nb_c], d_hist [nframes][4][257]; every frame starts its recurrence at the
+ * image start (carry must be NULL unless nframes == 1).  Per-image launches leave the chip mostly
+ * idle at 4K.  Workspace: jpgx_entropy_workspace_size_batch() bytes. */
+size_t jpgx_entropy_workspace_size_batch(size_t nb_y, size_t nb_c, size_t nframes);
+int jpgx_entropy_stats_gpu_batch(const int16_t *d_coef, size_t coef_frame_stride, size_t nframes, size_t nb_y,
+                                 size_t nb_c, const int32_t *carry, int32_t *d_dc, uint32_t *d_hist,
+                                 void *d_workspace, size_t workspace_bytes, void *stream);
 
 /* Synthetic frames, generated directly in device memory (SURVEY.md 8c generator G: byte k
  * of the buffer = splitmix64(seed + (k+1)*0x9E3779B97F4A7C15) >> 56). */

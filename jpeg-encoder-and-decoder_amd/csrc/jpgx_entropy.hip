@@ -11,10 +11,29 @@
  *
  * The recurrence is sequential; it is an alternating prefix sum:
  *     d_l = (-1)^l (P_l - c),  P_l = sum_{k<=l} (-1)^k v_k,  c = the DC carried in
- * so three launches per image: (A) per 256-block chunk, AC symbols into the histogram and the
- * chunk's sum of (-1)^k v_k; (B) one workgroup scans the chunk sums per channel; (C) per chunk,
- * the in-chunk scan, d_l, the DC classes.  Integer work, bound by reading the coefficients
- * once (A) plus their DC words (C).
+ * so three launches per image, the first two over chunks of 256 blocks of one channel (4 waves,
+ * one workgroup):
+ *   (A) k_ent_ac: every block's AC symbols into the histogram, the chunk's sum of (-1)^k v_k,
+ *       and the DC words compacted (2 bytes per block) into the workspace.  A wave takes 8
+ *       blocks per load (lane l: 16 bytes = coefficients 8 (l & 7) .. + 7 of block l >> 3, so
+ *       one load instruction reads 1 KiB contiguous), all 8 loads of its 64 blocks issued first.
+ *       A nonzero AC coefficient at zig-zag position i whose previous nonzero is at p (the DC
+ *       position 0 if none) is the reference's symbol ((i - p - 1) & 15) | class after
+ *       (i - p - 1) >> 4 ZRLs; a block ends in EOB iff its coefficient 63 is zero (huffman.c:
+ *       193-221).  p comes from an exclusive max-scan of the lanes' highest nonzero positions
+ *       over the block's 8 lanes.  The reference's `run | size` keeps every symbol in 1..31,
+ *       so each thread counts into its own LDS column of 32 words (no two lanes of a wave share a
+ *       bank; 16-bit counters packed two per word measured 4 % slower, profiles/r05_entropy.txt)
+ *       and the workgroup sums the columns once at its end into per-chunk counts (plain stores).
+ *   (B) k_ent_dc: the sum of the channel's earlier chunk sums (at most a few hundred, read from
+ *       L2), the in-chunk scan over the compacted DC words, d_l, and the DC classes per chunk.
+ *   (C) k_ent_hist: one workgroup per count row sums it over the luma / chroma chunks and writes
+ *       the histogram -- every entry, so no memset and no global atomics (a few thousand
+ *       device-scope atomics on the same few words cost more than the whole coefficient read).
+ * HBM traffic: the coefficients once (128 B per block) plus 2 + 2 + 4 bytes per block of DC.
+ * A call takes a batch of frames (jpgx_entropy_stats_gpu_batch): the chunks of every frame in one
+ * grid, each frame's recurrence starting from its own carry-in -- one frame per launch leaves the
+ * chip mostly idle (49.8 MB of 4K coefficients is ~10 us of HBM time against ~3 launches).
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -23,7 +42,9 @@
 
 namespace {
 
-constexpr int kChunk = 256;     /* blocks per workgroup (one thread per block) */
+constexpr int kChunk = 256;     /* blocks per workgroup: 4 waves x 8 loads x 8 blocks */
+constexpr int kSyms = 32;       /* AC symbols (zeros | class) 1..31; 0 = no symbol    */
+constexpr int kRows = 66;       /* per-chunk count rows: AC 0..31 (row 0: EOB), ZRL 32, DC class 33..65 */
 
 __device__ __forceinline__ int dc_class(int v)   /* huffman.c:226-235 get_class */
 {
@@ -32,137 +53,297 @@ __device__ __forceinline__ int dc_class(int v)   /* huffman.c:226-235 get_class 
 }
 
 struct Chunks {
-    const int16_t *coef;        /* Y [nb_y][64] | Cb [nb_c][64] | Cr [nb_c][64]          */
-    int32_t *dc;                /* [nb_y + 2 nb_c]                                       */
-    uint32_t *hist;             /* [4][257]                                              */
-    long long *part;            /* [nchunks] chunk sums of (-1)^k v_k (k local to channel) */
-    unsigned nb[3];             /* blocks per channel                                    */
-    unsigned first[3];          /* first chunk of each channel                           */
-    unsigned off[3];            /* first block of each channel in coef / dc              */
-    int carry[3];               /* DC carried in per channel (0 at the image start)      */
+    const int16_t *coef;        /* frame f: Y [nb_y][64] | Cb [nb_c][64] | Cr [nb_c][64] at f fstride */
+    int32_t *dc;                /* frame f: [nb_y + 2 nb_c] at f (nb_y + 2 nb_c)                 */
+    uint32_t *hist;             /* [nframes][4][257]                                             */
+    long long *part;            /* [nchunks] chunk sums of (-1)^k v_k (k local to channel)        */
+    uint32_t *cnt;              /* [kRows][nchunks] per-chunk counts                             */
+    int16_t *dcv;               /* [nframes][nb_y + 2 nb_c] the DC words, compacted              */
+    unsigned long long fstride; /* coefficient blocks from one frame to the next                 */
+    unsigned nchunks, nchf;     /* chunks in all, per frame                                      */
+    unsigned ndcg;              /* DC workgroups per frame (k_ent_dc)                            */
+    unsigned nbf;               /* nb_y + 2 nb_c                                                 */
+    unsigned nb[3];             /* blocks per channel                                            */
+    unsigned first[3];          /* first chunk of each channel within a frame                    */
+    unsigned off[3];            /* first block of each channel within a frame                    */
+    int carry[3];               /* DC carried in per channel (0 at the image start)              */
 };
 
-__device__ __forceinline__ void chunk_of(const Chunks &c, unsigned chunk, int &ch, unsigned &k0)
+/* chunk -> frame f, channel ch, first block k0 of the chunk in the channel */
+__device__ __forceinline__ void chunk_of(const Chunks &c, unsigned chunk, unsigned &f, int &ch, unsigned &k0)
 {
-    ch = chunk >= c.first[2] ? 2 : (chunk >= c.first[1] ? 1 : 0);
-    k0 = (chunk - c.first[ch]) * kChunk;
+    f = chunk / c.nchf;
+    const unsigned l = chunk - f * c.nchf;
+    ch = l >= c.first[2] ? 2 : (l >= c.first[1] ? 1 : 0);
+    k0 = (l - c.first[ch]) * kChunk;
 }
 
-__global__ __launch_bounds__(kChunk) void k_stats_ac(const Chunks c)
+__global__ __launch_bounds__(kChunk) void k_ent_ac(const Chunks c)
 {
-    __shared__ uint32_t h[256];
+    __shared__ uint32_t cnt[kSyms][kChunk];          /* [symbol][thread] */
+    __shared__ uint32_t red[kChunk / 32][kSyms];
     __shared__ long long wsum[kChunk / 64];
+    __shared__ uint32_t wez[kChunk / 64][2];
+    unsigned f, k0;
     int ch;
-    unsigned k0;
-    chunk_of(c, blockIdx.x, ch, k0);
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const unsigned k = k0 + threadIdx.x;
+    chunk_of(c, blockIdx.x, f, ch, k0);
+    const unsigned t = threadIdx.x, lane = t & 63u, wave = t >> 6, s = lane & 7u;
+#pragma unroll
+    for (int b = 0; b < kSyms; b++) cnt[b][t] = 0;   /* own column: no barrier before use */
+    const unsigned n = min(c.nb[ch] - k0, (unsigned)kChunk);
+    const int16_t *z = c.coef + (f * c.fstride + c.off[ch] + k0) * 64;
+    uint4 q[8];
+#pragma unroll
+    for (int it = 0; it < 8; it++) {                  /* unconditional: all 8 in flight at once */
+        const unsigned blk = 64u * wave + 8u * (unsigned)it + (lane >> 3);
+        q[it] = *(const uint4 *)(z + (size_t)(blk < n ? blk : 0u) * 64 + 8u * s);
+    }
+    uint32_t eob = 0, zrl = 0;
     long long w = 0;
-    if (k < c.nb[ch]) {
-        const int16_t *z = c.coef + ((size_t)c.off[ch] + k) * 64;
-        int zz[64];
-        for (int i = 0; i < 64; i += 8) {            /* 16-byte loads */
-            const uint4 q = *(const uint4 *)(z + i);
-            const uint32_t u[4] = {q.x, q.y, q.z, q.w};
-            for (int j = 0; j < 4; j++) {
-                zz[i + 2 * j] = (int16_t)(u[j] & 0xffffu);
-                zz[i + 2 * j + 1] = (int16_t)(u[j] >> 16);
-            }
+#pragma unroll
+    for (int it = 0; it < 8; it++) {
+        const unsigned blk = 64u * wave + 8u * (unsigned)it + (lane >> 3);
+        const uint32_t live = blk < n ? ~0u : 0u;       /* a dead block reads as zeros */
+        const uint32_t u[4] = {q[it].x & live, q[it].y & live, q[it].z & live, q[it].w & live};
+        int v[8];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            v[2 * j] = (int)(int16_t)(u[j] & 0xffffu);
+            v[2 * j + 1] = (int)u[j] >> 16;
         }
-        w = (k & 1) ? -(long long)zz[0] : (long long)zz[0];
-        int last = 0;                                 /* huffman.c:193-199 */
-        for (int i = 63; i > 0; i--)
-            if (zz[i] != 0) {
-                last = i;
-                break;
-            }
-        int zeros = 0;
-        for (int i = 1; i < 64; i++) {                /* :202-221 */
-            if (i == last + 1) {
-                atomicAdd(&h[0x00], 1u);              /* EOB */
-                break;
-            }
-            if (zz[i] == 0) {
-                if (++zeros == 16) {
-                    atomicAdd(&h[0xF0], 1u);          /* ZRL */
-                    zeros = 0;
-                }
-            } else {
-                atomicAdd(&h[zeros | dc_class(zz[i])], 1u);
-                zeros = 0;
+        const int i0 = 8 * (int)s;
+        bool nz[8];                                   /* a nonzero AC coefficient */
+#pragma unroll
+        for (int k = 0; k < 8; k++) nz[k] = v[k] != 0;
+        nz[0] = nz[0] && s > 0;                       /* the DC coefficient is no AC symbol */
+        int hi = -1, lo = 64;                         /* highest / lowest nonzero AC position */
+#pragma unroll
+        for (int k = 0; k < 8; k++) hi = nz[k] ? i0 + k : hi;
+#pragma unroll
+        for (int k = 7; k >= 0; k--) lo = nz[k] ? i0 + k : lo;
+        int x = max(hi, 0);                           /* max-scan over the block's 8 lanes */
+#pragma unroll
+        for (int d = 1; d < 8; d <<= 1) {
+            const int y = __shfl_up(x, d, 8);
+            if (s >= (unsigned)d) x = max(x, y);
+        }
+        int prev = __shfl_up(x, 1, 8);
+        if (s == 0) prev = 0;                         /* the DC position */
+        /* ZRLs: only the lane's first nonzero can follow 16 or more zeros (gaps inside a lane
+         * are < 8) */
+        if (hi >= 0) zrl += (uint32_t)((lo - prev - 1) >> 4);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int i = i0 + k;
+            /* class = frexp exponent of the exact float (0 for 0), huffman.c:226-235 */
+            const int cls = __builtin_amdgcn_frexp_expf((float)v[k]);
+            const int sym = ((i - prev - 1) & 15) | cls;
+            atomicAdd(&cnt[nz[k] ? sym : 0][t], 1u);
+            prev = nz[k] ? i : prev;
+        }
+        if (blk < n) {
+            eob += (s == 7 && v[7] == 0) ? 1u : 0u;
+            if (s == 0) {
+                c.dcv[f * c.nbf + c.off[ch] + k0 + blk] = (int16_t)v[0];
+                w += ((k0 + blk) & 1u) ? -(long long)v[0] : (long long)v[0];
             }
         }
     }
-    /* chunk sum of (-1)^k v_k */
-    for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = w;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        w += __shfl_xor(w, o, 64);
+        eob += __shfl_xor(eob, o, 64);
+        zrl += __shfl_xor(zrl, o, 64);
+    }
+    if (lane == 0) {
+        wsum[wave] = w;
+        wez[wave][0] = eob;
+        wez[wave][1] = zrl;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        long long s = 0;
-        for (int i = 0; i < kChunk / 64; i++) s += wsum[i];
-        c.part[blockIdx.x] = s;
+    {   /* column sums: lanes of a wave read 64 distinct banks (row r, rotated by the symbol) */
+        const unsigned b = t & 31u, r = t >> 5;
+        uint32_t sum = 0;
+#pragma unroll
+        for (unsigned j = 0; j < 32; j++) sum += cnt[b][32u * r + ((j + b) & 31u)];
+        red[r][b] = sum;
     }
-    const uint32_t n = h[threadIdx.x];
-    if (n) atomicAdd(&c.hist[(ch == 0 ? 1 : 3) * 257 + threadIdx.x], n);
-}
-
-/* exclusive scan of the chunk sums, per channel; one workgroup */
-__global__ __launch_bounds__(kChunk) void k_stats_scan(const Chunks c, unsigned nchunks)
-{
-    __shared__ long long sh[kChunk];
-    if (threadIdx.x < 4) c.hist[threadIdx.x * 257 + 256] = 1u;   /* reserved code point */
-    for (int ch = 0; ch < 3; ch++) {
-        const unsigned a = c.first[ch], b = ch < 2 ? c.first[ch + 1] : nchunks;
-        long long run = 0;
-        for (unsigned base = a; base < b; base += kChunk) {
-            const unsigned i = base + threadIdx.x;
-            const long long v = i < b ? c.part[i] : 0;
-            sh[threadIdx.x] = v;
-            __syncthreads();
-            for (int o = 1; o < kChunk; o <<= 1) {    /* Hillis-Steele, inclusive */
-                const long long t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
-                __syncthreads();
-                sh[threadIdx.x] += t;
-                __syncthreads();
-            }
-            if (i < b) c.part[i] = run + sh[threadIdx.x] - v;     /* exclusive */
-            run += sh[kChunk - 1];
-            __syncthreads();
+    __syncthreads();
+    if (t < (unsigned)kSyms) {
+        uint32_t tot = 0;                             /* symbol t; row 0 counts EOB */
+        if (t == 0) {
+#pragma unroll
+            for (int i = 0; i < kChunk / 64; i++) tot += wez[i][0];
+        } else {
+#pragma unroll
+            for (int r = 0; r < kChunk / 32; r++) tot += red[r][t];
         }
+        c.cnt[(size_t)t * c.nchunks + blockIdx.x] = tot;
+    } else if (t == (unsigned)kSyms) {
+        uint32_t zr = 0;
+        long long ws = 0;
+#pragma unroll
+        for (int i = 0; i < kChunk / 64; i++) zr += wez[i][1], ws += wsum[i];
+        c.cnt[(size_t)kSyms * c.nchunks + blockIdx.x] = zr;     /* ZRL */
+        c.part[blockIdx.x] = ws;
     }
 }
 
-__global__ __launch_bounds__(kChunk) void k_stats_dc(const Chunks c)
+/* DC pass over kDcChunks consecutive chunks of one channel (8 blocks per thread): the channel's
+ * earlier chunk sums, the scan, d_l and the classes; its class counts go to column blockIdx.x of
+ * the DC count rows (frame f's DC workgroups are f dc_groups() .. + dc_groups() - 1, luma first). */
+constexpr int kDcChunks = 8;
+__global__ __launch_bounds__(kChunk) void k_ent_dc(const Chunks c)
 {
-    __shared__ uint32_t h[33];                        /* classes 0..32 of an int */
-    __shared__ long long wtot[kChunk / 64];
-    int ch;
-    unsigned k0;
-    chunk_of(c, blockIdx.x, ch, k0);
-    if (threadIdx.x < 33) h[threadIdx.x] = 0;
-    const unsigned k = k0 + threadIdx.x;
-    const bool live = k < c.nb[ch];
-    const long long v = live ? (long long)c.coef[((size_t)c.off[ch] + k) * 64] : 0;
-    long long p = (k & 1) ? -v : v;                   /* inclusive scan over the chunk */
-    const unsigned lane = threadIdx.x & 63;
+    __shared__ uint32_t cnt[16][kChunk];              /* [class / 2][thread], 16-bit halves: classes 0..31 */
+    __shared__ uint32_t red[kChunk / 16][32];
+    __shared__ uint32_t top[kChunk / 64];             /* class 32 (d = INT_MIN) per wave */
+    __shared__ long long wtot[kChunk / 64], wbase[kChunk / 64];
+    /* workgroup g: chunks kDcChunks g' .. of channel ch of frame f (g' counts per channel) */
+    const unsigned per[3] = {(c.first[1] - c.first[0] + kDcChunks - 1) / kDcChunks,
+                             (c.first[2] - c.first[1] + kDcChunks - 1) / kDcChunks,
+                             (c.nchf - c.first[2] + kDcChunks - 1) / kDcChunks};
+    const unsigned pf = per[0] + per[1] + per[2];
+    const unsigned f = blockIdx.x / pf;
+    unsigned l = blockIdx.x - f * pf;
+    const int ch = l >= per[0] + per[1] ? 2 : (l >= per[0] ? 1 : 0);
+    l -= ch == 0 ? 0u : (ch == 1 ? per[0] : per[0] + per[1]);
+    const unsigned chunk0 = f * c.nchf + c.first[ch] + kDcChunks * l;      /* first chunk */
+    const unsigned b0 = kDcChunks * kChunk * l;                           /* first block */
+    const unsigned t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+#pragma unroll
+    for (int b = 0; b < 16; b++) cnt[b][t] = 0;      /* own column: no barrier before use */
+    const unsigned k = b0 + 8u * t;                   /* this thread's 8 blocks */
+    const size_t at = (size_t)f * c.nbf + c.off[ch] + k;
+    long long v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = k + i < c.nb[ch] ? (long long)c.dcv[at + i] : 0;
+    long long e = 0;                                  /* the channel's earlier chunks */
+    {
+        const unsigned i0 = f * c.nchf + c.first[ch] + t;
+        long long pp[4];                              /* up to 1024 earlier chunks, loads together */
+#pragma unroll
+        for (int r = 0; r < 4; r++) pp[r] = i0 + r * kChunk < chunk0 ? c.part[i0 + r * kChunk] : 0;
+        for (unsigned i = i0 + 4 * kChunk; i < chunk0; i += kChunk) e += c.part[i];
+#pragma unroll
+        for (int r = 0; r < 4; r++) e += pp[r];
+    }
+    long long run = 0;                                /* k is even: (-1)^(k+i) = (-1)^i */
+#pragma unroll
+    for (int i = 0; i < 8; i++) run += (i & 1) ? -v[i] : v[i];
+    long long p = run;                                /* inclusive scan of the thread totals */
+#pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const long long t = __shfl_up(p, o, 64);
-        if (lane >= (unsigned)o) p += t;
+        const long long y = __shfl_up(p, o, 64);
+        if (lane >= (unsigned)o) p += y;
+        e += __shfl_xor(e, o, 64);
     }
-    if (lane == 63) wtot[threadIdx.x >> 6] = p;
+    if (lane == 63) wtot[wave] = p;
+    if (lane == 0) wbase[wave] = e;
     __syncthreads();
-    for (unsigned wv = 0; wv < (threadIdx.x >> 6); wv++) p += wtot[wv];
-    if (live) {
-        const long long P = c.part[blockIdx.x] + p;
-        const long long d = (k & 1) ? -(P - c.carry[ch]) : (P - c.carry[ch]);
-        const int di = (int)d;                        /* the reference's int */
-        c.dc[c.off[ch] + k] = di;
-        atomicAdd(&h[dc_class(di)], 1u);
+    p -= run;                                         /* exclusive */
+#pragma unroll
+    for (unsigned wv = 0; wv < kChunk / 64; wv++) {
+        p += wbase[wv];
+        if (wv < wave) p += wtot[wv];
+    }
+    uint32_t n32 = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        p += (i & 1) ? -v[i] : v[i];
+        if (k + i < c.nb[ch]) {
+            const long long d = (i & 1) ? -(p - c.carry[ch]) : (p - c.carry[ch]);
+            const int di = (int)d;                    /* the reference's int */
+            c.dc[at + i] = di;
+            const int cl = dc_class(di);
+            if (cl < 32) atomicAdd(&cnt[cl >> 1][t], 1u << ((cl & 1) << 4));
+            else n32++;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) n32 += __shfl_xor(n32, o, 64);
+    if (lane == 0) top[wave] = n32;
+    __syncthreads();
+    {   /* column sums: word b (classes 2b, 2b + 1) of 16 columns; 64 distinct banks per wave */
+        const unsigned b = t & 15u, r = t >> 4;
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (unsigned j = 0; j < 16; j++) {
+            const uint32_t x = cnt[b][16u * r + ((j + b) & 15u)];
+            lo += x & 0xffffu, hi += x >> 16;
+        }
+        red[r][2 * b] = lo;
+        red[r][2 * b + 1] = hi;
     }
     __syncthreads();
-    if (threadIdx.x < 33 && h[threadIdx.x])
-        atomicAdd(&c.hist[(ch == 0 ? 0 : 2) * 257 + threadIdx.x], h[threadIdx.x]);
+    if (t <= 32) {
+        uint32_t tot = 0;
+        if (t < 32) {
+#pragma unroll
+            for (int r = 0; r < kChunk / 16; r++) tot += red[r][t];
+        } else {
+#pragma unroll
+            for (int r = 0; r < kChunk / 64; r++) tot += top[r];
+        }
+        c.cnt[(size_t)(kSyms + 1 + t) * c.nchunks + blockIdx.x] = tot;
+    }
+}
+
+/* the DC workgroups of one frame */
+unsigned dc_groups(const Chunks &c)
+{
+    return (c.first[1] - c.first[0] + kDcChunks - 1) / kDcChunks + (c.first[2] - c.first[1] + kDcChunks - 1) / kDcChunks +
+           (c.nchf - c.first[2] + kDcChunks - 1) / kDcChunks;
+}
+
+/* the histograms from the per-chunk count rows: workgroup (r, f) sums row r over frame f's luma
+ * chunks and over its chroma chunks; workgroup (0, f) also writes every entry no row maps to (0,
+ * and the reserved freq[256] = 1 of initialize_huffman, huffman.c:55) */
+__global__ __launch_bounds__(kChunk) void k_ent_hist(const Chunks c)
+{
+    __shared__ uint32_t part[2][kChunk / 64];
+    const unsigned r = blockIdx.x, f = blockIdx.y, t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    const bool dcrow = r > (unsigned)kSyms;
+    const unsigned ny = dcrow ? (c.first[1] + kDcChunks - 1) / kDcChunks : c.first[1];   /* luma columns */
+    const unsigned ncol = dcrow ? c.ndcg : c.nchf;                                  /* columns per frame */
+    const uint32_t *row = c.cnt + (size_t)r * c.nchunks + (size_t)f * ncol;
+    uint32_t *hist = c.hist + (size_t)f * 4 * 257;
+    uint32_t sy = 0, sc = 0;
+    for (unsigned i0 = t; i0 < ncol; i0 += 8 * kChunk) {     /* eight loads in flight */
+        uint32_t x[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) x[r] = i0 + r * kChunk < ncol ? row[i0 + r * kChunk] : 0u;
+#pragma unroll
+        for (int r = 0; r < 8; r++) (i0 + r * kChunk < ny ? sy : sc) += x[r];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        sy += __shfl_xor(sy, o, 64);
+        sc += __shfl_xor(sc, o, 64);
+    }
+    if (lane == 0) part[0][wave] = sy, part[1][wave] = sc;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t y = 0, ch = 0;
+#pragma unroll
+        for (int w = 0; w < kChunk / 64; w++) y += part[0][w], ch += part[1][w];
+        if (r <= (unsigned)kSyms) {                   /* AC: symbol r, or ZRL */
+            const unsigned e = r < (unsigned)kSyms ? r : 0xF0u;
+            hist[1 * 257 + e] = y;
+            hist[3 * 257 + e] = ch;
+        } else {                                      /* DC class r - 33 */
+            hist[0 * 257 + r - kSyms - 1] = y;
+            hist[2 * 257 + r - kSyms - 1] = ch;
+        }
+    }
+    if (r == 0) {
+        for (unsigned e = t; e < 4u * 257u; e += kChunk) {
+            const unsigned k = e / 257u, i = e - 257u * k;
+            const bool ac = k & 1u;
+            const bool mapped = ac ? (i < (unsigned)kSyms || i == 0xF0u) : i <= 32u;
+            if (!mapped) hist[e] = i == 256u ? 1u : 0u;
+        }
+    }
 }
 
 int hip_rc2(hipError_t e) { return e == hipSuccess ? JPGX_OK : JPGX_EHIP; }
@@ -172,30 +353,50 @@ size_t nchunks_of(size_t nb_y, size_t nb_c)
     return (nb_y + kChunk - 1) / kChunk + 2 * ((nb_c + kChunk - 1) / kChunk);
 }
 
+size_t round8(size_t x) { return (x + 7) / 8 * 8; }
+
 }  // namespace
 
 extern "C" {
 
-size_t jpgx_entropy_workspace_size(size_t nb_y, size_t nb_c)
+size_t jpgx_entropy_workspace_size_batch(size_t nb_y, size_t nb_c, size_t nframes)
 {
-    return nchunks_of(nb_y, nb_c) * sizeof(long long);
+    const size_t nch = nchunks_of(nb_y, nb_c) * nframes;
+    return nch * sizeof(long long) + round8(kRows * nch * sizeof(uint32_t)) +
+           round8(nframes * (nb_y + 2 * nb_c) * sizeof(int16_t));
 }
 
-int jpgx_entropy_stats_gpu(const int16_t *d_coef, size_t nb_y, size_t nb_c, const int32_t *carry,
-                           int32_t *d_dc, uint32_t *d_hist, void *d_workspace,
-                           size_t workspace_bytes, void *stream)
+size_t jpgx_entropy_workspace_size(size_t nb_y, size_t nb_c)
 {
-    if (!d_coef || !d_dc || !d_hist || ((uintptr_t)d_coef & 15) || nb_y == 0 ||
-        nb_y + 2 * nb_c >= (1ull << 31))
+    return jpgx_entropy_workspace_size_batch(nb_y, nb_c, 1);
+}
+
+int jpgx_entropy_stats_gpu_batch(const int16_t *d_coef, size_t coef_frame_stride, size_t nframes, size_t nb_y,
+                                 size_t nb_c, const int32_t *carry, int32_t *d_dc, uint32_t *d_hist,
+                                 void *d_workspace, size_t workspace_bytes, void *stream)
+{
+    const size_t nbf = nb_y + 2 * nb_c;
+    if (!d_coef || !d_dc || !d_hist || ((uintptr_t)d_coef & 15) || nb_y == 0 || nframes == 0 ||
+        coef_frame_stride < nbf * 64 || coef_frame_stride % 64 || nbf >= (1ull << 31) ||
+        nframes * nbf >= (1ull << 31) || (carry && nframes != 1))
         return JPGX_EARG;
-    const size_t nch = nchunks_of(nb_y, nb_c);
-    if (!d_workspace || workspace_bytes < nch * sizeof(long long) || ((uintptr_t)d_workspace & 7))
+    const size_t nchf = nchunks_of(nb_y, nb_c), nch = nchf * nframes;
+    if (nch >= (1ull << 31))
+        return JPGX_EARG;
+    if (!d_workspace || workspace_bytes < jpgx_entropy_workspace_size_batch(nb_y, nb_c, nframes) ||
+        ((uintptr_t)d_workspace & 7))
         return JPGX_EWORKSPACE;
     Chunks c;
     c.coef = d_coef;
     c.dc = d_dc;
     c.hist = d_hist;
     c.part = (long long *)d_workspace;
+    c.cnt = (uint32_t *)((char *)d_workspace + nch * sizeof(long long));
+    c.dcv = (int16_t *)((char *)c.cnt + round8(kRows * nch * sizeof(uint32_t)));
+    c.fstride = coef_frame_stride / 64;
+    c.nchunks = (unsigned)nch;
+    c.nchf = (unsigned)nchf;
+    c.nbf = (unsigned)nbf;
     c.nb[0] = (unsigned)nb_y;
     c.nb[1] = c.nb[2] = (unsigned)nb_c;
     c.first[0] = 0;
@@ -206,12 +407,19 @@ int jpgx_entropy_stats_gpu(const int16_t *d_coef, size_t nb_y, size_t nb_c, cons
     c.off[2] = (unsigned)(nb_y + nb_c);
     for (int k = 0; k < 3; k++) c.carry[k] = carry ? carry[k] : 0;
     hipStream_t s = (hipStream_t)stream;
-    int rc = hip_rc2(hipMemsetAsync(d_hist, 0, 4 * 257 * sizeof(uint32_t), s));
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_stats_ac, dim3((unsigned)nch), dim3(kChunk), 0, s, c);
-    hipLaunchKernelGGL(k_stats_scan, dim3(1), dim3(kChunk), 0, s, c, (unsigned)nch);
-    hipLaunchKernelGGL(k_stats_dc, dim3((unsigned)nch), dim3(kChunk), 0, s, c);
+    hipLaunchKernelGGL(k_ent_ac, dim3((unsigned)nch), dim3(kChunk), 0, s, c);
+    c.ndcg = dc_groups(c);
+    hipLaunchKernelGGL(k_ent_dc, dim3(c.ndcg * (unsigned)nframes), dim3(kChunk), 0, s, c);
+    hipLaunchKernelGGL(k_ent_hist, dim3(kRows, (unsigned)nframes), dim3(kChunk), 0, s, c);
     return hip_rc2(hipGetLastError());
+}
+
+int jpgx_entropy_stats_gpu(const int16_t *d_coef, size_t nb_y, size_t nb_c, const int32_t *carry,
+                           int32_t *d_dc, uint32_t *d_hist, void *d_workspace,
+                           size_t workspace_bytes, void *stream)
+{
+    return jpgx_entropy_stats_gpu_batch(d_coef, (nb_y + 2 * nb_c) * 64, 1, nb_y, nb_c, carry, d_dc, d_hist,
+                                        d_workspace, workspace_bytes, stream);
 }
 
 }  /* extern "C" */

@@ -39,7 +39,8 @@ EXPORTS = [
     "jpgx_gen_splitmix_gpu",
     "jpgx_gen_tie_gpu", "jpgx_blocks", "jpgx_blocks_multi", "jpgx_stripe",
     "jpgx_device_count", "jpgx_version", "jpgx_chroma_blocks", "jpgx_entropy_workspace_size",
-    "jpgx_entropy_stats_gpu", "jpgx_host_create", "jpgx_host_destroy", "jpgx_host_blocks",
+    "jpgx_entropy_stats_gpu", "jpgx_entropy_workspace_size_batch", "jpgx_entropy_stats_gpu_batch",
+    "jpgx_host_create", "jpgx_host_destroy", "jpgx_host_blocks",
     "jpgx_host_register", "jpgx_host_unregister", "jpgx_host_release",
 ]
 COMPAT_EXPORTS = [
@@ -109,6 +110,9 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.jpgx_entropy_workspace_size.argtypes = [sz, sz]
     L.jpgx_entropy_workspace_size.restype = sz
     L.jpgx_entropy_stats_gpu.argtypes = [vp, sz, sz, vp, vp, vp, vp, sz, vp]
+    L.jpgx_entropy_workspace_size_batch.argtypes = [sz, sz, sz]
+    L.jpgx_entropy_workspace_size_batch.restype = sz
+    L.jpgx_entropy_stats_gpu_batch.argtypes = [vp, sz, sz, sz, sz, vp, vp, vp, vp, sz, vp]
     L.jpgx_version.restype = ctypes.c_char_p
     L.jpgx_host_create.argtypes = [ctypes.POINTER(vp), i, vp, i]
     L.jpgx_host_destroy.argtypes = [vp]
@@ -268,6 +272,23 @@ def entropy_stats_gpu(d_coef, nb_y: int, nb_c: int, carry=None, stream=None):
                                       ctypes.cast(cy, ctypes.c_void_p) if cy is not None else None,
                                       dc.data_ptr(), hist.data_ptr(), ws.data_ptr(), ws.numel(),
                                       _stream_ptr(stream)), "jpgx_entropy_stats_gpu")
+    return dc, hist
+
+
+def entropy_stats_gpu_batch(d_coef, nb_y: int, nb_c: int, stream=None):
+    """The same over a frame batch d_coef [nframes][>= nb_y + 2 nb_c][64] (int16, contiguous
+    frames): (dc int32 [nframes][nb_y + 2 nb_c], hist uint32 [nframes][4][257]), every frame from
+    the image start."""
+    import torch
+    dev = d_coef.device
+    nf = d_coef.shape[0]
+    dc = torch.empty((nf, nb_y + 2 * nb_c), dtype=torch.int32, device=dev)
+    hist = torch.empty((nf, 4, 257), dtype=torch.int32, device=dev)
+    ws = torch.empty(max(int(lib.jpgx_entropy_workspace_size_batch(nb_y, nb_c, nf)), 8),
+                     dtype=torch.uint8, device=dev)
+    _check(lib.jpgx_entropy_stats_gpu_batch(d_coef.data_ptr(), d_coef[0].numel(), nf, nb_y, nb_c, None,
+                                            dc.data_ptr(), hist.data_ptr(), ws.data_ptr(), ws.numel(),
+                                            _stream_ptr(stream)), "jpgx_entropy_stats_gpu_batch")
     return dc, hist
 
 

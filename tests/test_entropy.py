@@ -137,3 +137,96 @@ def test_gpu_stats_subsampled_layout(cuda, sr):
     rdc, rhist = O.entropy_stats(out.cpu().numpy(), nb, nbc)
     assert np.array_equal(dc.cpu().numpy(), rdc)
     assert np.array_equal(hist.cpu().numpy(), rhist)
+
+
+def _gap_rule_hist(coef):
+    """k_ent_ac's rule restated (csrc/jpgx_entropy.hip): lane s of a block holds coefficients
+    8s..8s+7; p = the highest nonzero AC position of the lanes below (exclusive max-scan, 0 = the
+    DC position); a nonzero AC coefficient at i is symbol ((i - p - 1) & 15) | class (class = the
+    frexp exponent of the coefficient as a float); ZRLs come only from a lane's first nonzero,
+    (i - p - 1) >> 4 of them (gaps inside a lane are < 8); EOB iff coefficient 63 is zero.
+    Returns the AC histogram [257]."""
+    z = np.asarray(coef, np.int64).reshape(-1, 64)
+    h = np.zeros(257, np.int64)
+    pos = np.arange(64)
+    nz = (z != 0) & (pos > 0)
+    hi = np.where(nz, pos, 0).reshape(-1, 8, 8).max(axis=2)                  # per lane
+    excl = np.concatenate([np.zeros((z.shape[0], 1), np.int64),
+                           np.maximum.accumulate(hi, axis=1)[:, :-1]], axis=1)
+    for s in range(8):
+        prev = excl[:, s].copy()
+        lane = nz[:, 8 * s:8 * s + 8]
+        first = 8 * s + np.argmax(lane, axis=1)                      # the lane's first nonzero
+        anynz = lane.any(axis=1)
+        h[0xF0] += int(((first - prev - 1) >> 4)[anynz].sum())
+        for k in range(8):
+            i = 8 * s + k
+            m = nz[:, i]
+            gap = i - prev - 1
+            cls = np.frexp(z[:, i].astype(np.float32))[1].astype(np.int64)   # 0 for 0
+            sym = (gap & 15) | cls
+            np.add.at(h, sym[m], 1)
+            prev = np.where(m, i, prev)
+    h[0] += int((z[:, 63] == 0).sum())
+    return h
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse", "long_runs", "extremes"])
+def test_device_gap_rule_matches_oracle(kind):
+    """The histogram rule the GPU kernel uses, against the oracle's sequential huffman.c loop."""
+    rng = np.random.default_rng({"dense": 1, "sparse": 2, "long_runs": 3, "extremes": 4}[kind])
+    nb = 3000
+    if kind == "dense":
+        c = rng.integers(-300, 301, (3, nb, 64))
+    elif kind == "sparse":
+        c = rng.integers(-40, 41, (3, nb, 64)) * (rng.random((3, nb, 64)) < 0.08)
+    elif kind == "long_runs":                     # runs of 16+, 32+ zeros, all-zero AC blocks
+        c = np.zeros((3, nb, 64), np.int64)
+        for b in range(nb):
+            for i in rng.choice(64, rng.integers(0, 4), replace=False):
+                c[0, b, i] = c[1, b, (i * 7) % 64] = c[2, b, 63 - i] = rng.integers(1, 9) * rng.choice([-1, 1])
+    else:                                         # int16 extremes: classes up to 16
+        c = rng.choice(np.array([0, 1, -1, 32767, -32768, 2048, -2047]), (3, nb, 64))
+    c = c.astype(np.int16)
+    _, hist = O.entropy_stats(c)
+    for ch, row in ((0, 1), (1, 3)):
+        blocks = c[0] if ch == 0 else c[1:].reshape(-1, 64)
+        want = hist[row].astype(np.int64)
+        got = _gap_rule_hist(blocks)
+        got[256] = want[256]                      # the reserved count
+        assert np.array_equal(got, want), (kind, ch)
+
+
+@pytest.mark.gpu
+def test_gpu_stats_batch_equals_per_frame(cuda):
+    """The batch call (one set of launches over frames with a padded frame stride) equals one
+    call per frame, and the oracle on frame 1."""
+    import torch
+    W, H, F = 640, 480, 3
+    nb = (H // 8) * (W // 8)
+    out = torch.zeros((F, 3 * nb + 5, 64), dtype=torch.int16, device=cuda)    # padded frames
+    for f in range(F):
+        out[f, :3 * nb] = jpgx.encode_blocks(torch.from_numpy(O.gen_splitmix(40 + f, W, H)).to(cuda),
+                                             50 + 20 * f).reshape(3 * nb, 64)
+    dcb, hb = jpgx.entropy_stats_gpu_batch(out, nb, nb)
+    for f in range(F):
+        dc, h = jpgx.entropy_stats_gpu(out[f, :3 * nb].contiguous(), nb, nb)
+        assert torch.equal(dcb[f], dc) and torch.equal(hb[f], h), f
+    rdc, rh = O.entropy_stats(out[1, :3 * nb].cpu().numpy(), nb, nb)
+    assert np.array_equal(dcb[1].cpu().numpy(), rdc) and np.array_equal(hb[1].cpu().numpy(), rh)
+
+
+def test_batch_entry_point_rejects_bad_arguments():
+    """Argument checks of jpgx_entropy_stats_gpu_batch that need no device."""
+    import ctypes
+    L = jpgx.lib
+    nb = 100
+    ws = ctypes.create_string_buffer(int(L.jpgx_entropy_workspace_size_batch(nb, nb, 2)) + 16)
+    p16 = ctypes.addressof(ws) + (-ctypes.addressof(ws)) % 16
+    args = lambda stride, nf, carry: L.jpgx_entropy_stats_gpu_batch(      # noqa: E731
+        p16, stride, nf, nb, nb, carry, p16, p16, p16, len(ws.raw) - 16, None)
+    carry = (ctypes.c_int32 * 3)(1, 2, 3)
+    assert args(3 * nb * 64 - 64, 2, None) == jpgx.EARG                # stride below a frame
+    assert args(3 * nb * 64 + 8, 2, None) == jpgx.EARG                 # not whole blocks
+    assert args(3 * nb * 64, 0, None) == jpgx.EARG                     # no frames
+    assert args(3 * nb * 64, 2, ctypes.cast(carry, ctypes.c_void_p)) == jpgx.EARG   # carry with a batch
