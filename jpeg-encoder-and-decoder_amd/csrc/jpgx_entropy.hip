@@ -62,6 +62,7 @@ struct Chunks {
     unsigned long long fstride; /* coefficient blocks from one frame to the next                 */
     unsigned nchunks, nchf;     /* chunks in all, per frame                                      */
     unsigned ndcg;              /* DC workgroups per frame (k_ent_dc)                            */
+    bool vec;                   /* k_ent_dc's 16-byte DC loads / stores are aligned              */
     unsigned nbf;               /* nb_y + 2 nb_c                                                 */
     unsigned nb[3];             /* blocks per channel                                            */
     unsigned first[3];          /* first chunk of each channel within a frame                    */
@@ -198,7 +199,8 @@ __global__ __launch_bounds__(kChunk) void k_ent_dc(const Chunks c)
     __shared__ uint32_t cnt[16][kChunk];              /* [class / 2][thread], 16-bit halves: classes 0..31 */
     __shared__ uint32_t red[kChunk / 16][32];
     __shared__ uint32_t top[kChunk / 64];             /* class 32 (d = INT_MIN) per wave */
-    __shared__ long long wtot[kChunk / 64], wbase[kChunk / 64];
+    __shared__ int wtot[kChunk / 64];
+    __shared__ long long wbase[kChunk / 64];
     /* workgroup g: chunks kDcChunks g' .. of channel ch of frame f (g' counts per channel) */
     const unsigned per[3] = {(c.first[1] - c.first[0] + kDcChunks - 1) / kDcChunks,
                              (c.first[2] - c.first[1] + kDcChunks - 1) / kDcChunks,
@@ -215,9 +217,17 @@ __global__ __launch_bounds__(kChunk) void k_ent_dc(const Chunks c)
     for (int b = 0; b < 16; b++) cnt[b][t] = 0;      /* own column: no barrier before use */
     const unsigned k = b0 + 8u * t;                   /* this thread's 8 blocks */
     const size_t at = (size_t)f * c.nbf + c.off[ch] + k;
-    long long v[8];
+    const bool vec = c.vec && k + 8u <= c.nb[ch];    /* 16-byte loads / stores */
+    int v[8];
+    if (vec) {
+        const uint4 q = *(const uint4 *)(c.dcv + at);
+        const uint32_t u[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = k + i < c.nb[ch] ? (long long)c.dcv[at + i] : 0;
+        for (int j = 0; j < 4; j++) v[2 * j] = (int)(int16_t)(u[j] & 0xffffu), v[2 * j + 1] = (int)u[j] >> 16;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = k + i < c.nb[ch] ? (int)c.dcv[at + i] : 0;
+    }
     long long e = 0;                                  /* the channel's earlier chunks */
     {
         const unsigned i0 = f * c.nchf + c.first[ch] + t;
@@ -228,37 +238,45 @@ __global__ __launch_bounds__(kChunk) void k_ent_dc(const Chunks c)
 #pragma unroll
         for (int r = 0; r < 4; r++) e += pp[r];
     }
-    long long run = 0;                                /* k is even: (-1)^(k+i) = (-1)^i */
+    int run = 0;                                      /* k is even: (-1)^(k+i) = (-1)^i */
 #pragma unroll
     for (int i = 0; i < 8; i++) run += (i & 1) ? -v[i] : v[i];
-    long long p = run;                                /* inclusive scan of the thread totals */
-#pragma unroll
+    int p32 = run;                                    /* inclusive scan of the thread totals: */
+#pragma unroll                                        /* |.| <= 2048 * 32768, 32-bit          */
     for (int o = 1; o < 64; o <<= 1) {
-        const long long y = __shfl_up(p, o, 64);
-        if (lane >= (unsigned)o) p += y;
+        const int y = __shfl_up(p32, o, 64);
+        if (lane >= (unsigned)o) p32 += y;
         e += __shfl_xor(e, o, 64);
     }
-    if (lane == 63) wtot[wave] = p;
+    if (lane == 63) wtot[wave] = p32;
     if (lane == 0) wbase[wave] = e;
     __syncthreads();
-    p -= run;                                         /* exclusive */
+    long long p = p32 - run;                          /* exclusive */
 #pragma unroll
     for (unsigned wv = 0; wv < kChunk / 64; wv++) {
         p += wbase[wv];
         if (wv < wave) p += wtot[wv];
     }
     uint32_t n32 = 0;
+    int dv[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         p += (i & 1) ? -v[i] : v[i];
+        const long long d = (i & 1) ? -(p - c.carry[ch]) : (p - c.carry[ch]);
+        dv[i] = (int)d;                               /* the reference's int */
         if (k + i < c.nb[ch]) {
-            const long long d = (i & 1) ? -(p - c.carry[ch]) : (p - c.carry[ch]);
-            const int di = (int)d;                    /* the reference's int */
-            c.dc[at + i] = di;
-            const int cl = dc_class(di);
+            const int cl = dc_class(dv[i]);
             if (cl < 32) atomicAdd(&cnt[cl >> 1][t], 1u << ((cl & 1) << 4));
             else n32++;
         }
+    }
+    if (vec) {
+        *(int4 *)(c.dc + at) = make_int4(dv[0], dv[1], dv[2], dv[3]);
+        *(int4 *)(c.dc + at + 4) = make_int4(dv[4], dv[5], dv[6], dv[7]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            if (k + i < c.nb[ch]) c.dc[at + i] = dv[i];
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) n32 += __shfl_xor(n32, o, 64);
@@ -409,6 +427,8 @@ int jpgx_entropy_stats_gpu_batch(const int16_t *d_coef, size_t coef_frame_stride
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(k_ent_ac, dim3((unsigned)nch), dim3(kChunk), 0, s, c);
     c.ndcg = dc_groups(c);
+    c.vec = nbf % 8 == 0 && nb_y % 8 == 0 && nb_c % 8 == 0 && ((uintptr_t)c.dcv & 15) == 0 &&
+            ((uintptr_t)d_dc & 15) == 0;
     hipLaunchKernelGGL(k_ent_dc, dim3(c.ndcg * (unsigned)nframes), dim3(kChunk), 0, s, c);
     hipLaunchKernelGGL(k_ent_hist, dim3(kRows, (unsigned)nframes), dim3(kChunk), 0, s, c);
     return hip_rc2(hipGetLastError());
