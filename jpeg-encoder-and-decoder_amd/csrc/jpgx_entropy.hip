@@ -11,12 +11,12 @@
  *
  * The recurrence is sequential; it is an alternating prefix sum:
  *     d_l = (-1)^l (P_l - c),  P_l = sum_{k<=l} (-1)^k v_k,  c = the DC carried in
- * so three launches per image, the first two over chunks of 256 blocks of one channel (4 waves,
+ * so three launches per image, (A) over chunks of 512 blocks of one channel (4 waves,
  * one workgroup):
  *   (A) k_ent_ac: every block's AC symbols into the histogram, the chunk's sum of (-1)^k v_k,
  *       and the DC words compacted (2 bytes per block) into the workspace.  A wave takes 8
  *       blocks per load (lane l: 16 bytes = coefficients 8 (l & 7) .. + 7 of block l >> 3, so
- *       one load instruction reads 1 KiB contiguous), all 8 loads of its 64 blocks issued first.
+ *       one load instruction reads 1 KiB contiguous), all 16 loads of its 128 blocks issued first.
  *       A nonzero AC coefficient at zig-zag position i whose previous nonzero is at p (the DC
  *       position 0 if none) is the reference's symbol ((i - p - 1) & 15) | class after
  *       (i - p - 1) >> 4 ZRLs; a block ends in EOB iff its coefficient 63 is zero (huffman.c:
@@ -42,7 +42,12 @@
 
 namespace {
 
-constexpr int kChunk = 256;     /* blocks per workgroup: 4 waves x 8 loads x 8 blocks */
+#ifndef JX_ENT_LOADS
+#define JX_ENT_LOADS 16
+#endif
+constexpr int kChunk = 256;     /* threads per workgroup (4 waves)                     */
+constexpr int kLoads = JX_ENT_LOADS;   /* k_ent_ac: 8-block loads per wave, all issued first (16 vs 8: 4 % faster, profiles/r05_entropy.txt) */
+constexpr int kCB = 32 * kLoads;       /* blocks per chunk: 4 waves x kLoads x 8 blocks       */
 constexpr int kSyms = 32;       /* AC symbols (zeros | class) 1..31; 0 = no symbol    */
 constexpr int kRows = 66;       /* per-chunk count rows: AC 0..31 (row 0: EOB), ZRL 32, DC class 33..65 */
 
@@ -76,7 +81,7 @@ __device__ __forceinline__ void chunk_of(const Chunks &c, unsigned chunk, unsign
     f = chunk / c.nchf;
     const unsigned l = chunk - f * c.nchf;
     ch = l >= c.first[2] ? 2 : (l >= c.first[1] ? 1 : 0);
-    k0 = (l - c.first[ch]) * kChunk;
+    k0 = (l - c.first[ch]) * kCB;
 }
 
 __global__ __launch_bounds__(kChunk) void k_ent_ac(const Chunks c)
@@ -91,19 +96,19 @@ __global__ __launch_bounds__(kChunk) void k_ent_ac(const Chunks c)
     const unsigned t = threadIdx.x, lane = t & 63u, wave = t >> 6, s = lane & 7u;
 #pragma unroll
     for (int b = 0; b < kSyms; b++) cnt[b][t] = 0;   /* own column: no barrier before use */
-    const unsigned n = min(c.nb[ch] - k0, (unsigned)kChunk);
+    const unsigned n = min(c.nb[ch] - k0, (unsigned)kCB);
     const int16_t *z = c.coef + (f * c.fstride + c.off[ch] + k0) * 64;
-    uint4 q[8];
+    uint4 q[kLoads];
 #pragma unroll
-    for (int it = 0; it < 8; it++) {                  /* unconditional: all 8 in flight at once */
-        const unsigned blk = 64u * wave + 8u * (unsigned)it + (lane >> 3);
+    for (int it = 0; it < kLoads; it++) {             /* unconditional: all in flight at once */
+        const unsigned blk = 8u * kLoads * wave + 8u * (unsigned)it + (lane >> 3);
         q[it] = *(const uint4 *)(z + (size_t)(blk < n ? blk : 0u) * 64 + 8u * s);
     }
     uint32_t eob = 0, zrl = 0;
     long long w = 0;
 #pragma unroll
-    for (int it = 0; it < 8; it++) {
-        const unsigned blk = 64u * wave + 8u * (unsigned)it + (lane >> 3);
+    for (int it = 0; it < kLoads; it++) {
+        const unsigned blk = 8u * kLoads * wave + 8u * (unsigned)it + (lane >> 3);
         const uint32_t live = blk < n ? ~0u : 0u;       /* a dead block reads as zeros */
         const uint32_t u[4] = {q[it].x & live, q[it].y & live, q[it].z & live, q[it].w & live};
         int v[8];
@@ -193,7 +198,7 @@ __global__ __launch_bounds__(kChunk) void k_ent_ac(const Chunks c)
 /* DC pass over kDcChunks consecutive chunks of one channel (8 blocks per thread): the channel's
  * earlier chunk sums, the scan, d_l and the classes; its class counts go to column blockIdx.x of
  * the DC count rows (frame f's DC workgroups are f dc_groups() .. + dc_groups() - 1, luma first). */
-constexpr int kDcChunks = 8;
+constexpr int kDcChunks = 2048 / kCB;   /* 2,048 blocks per DC workgroup */
 __global__ __launch_bounds__(kChunk) void k_ent_dc(const Chunks c)
 {
     __shared__ uint32_t cnt[16][kChunk];              /* [class / 2][thread], 16-bit halves: classes 0..31 */
@@ -211,7 +216,7 @@ __global__ __launch_bounds__(kChunk) void k_ent_dc(const Chunks c)
     const int ch = l >= per[0] + per[1] ? 2 : (l >= per[0] ? 1 : 0);
     l -= ch == 0 ? 0u : (ch == 1 ? per[0] : per[0] + per[1]);
     const unsigned chunk0 = f * c.nchf + c.first[ch] + kDcChunks * l;      /* first chunk */
-    const unsigned b0 = kDcChunks * kChunk * l;                           /* first block */
+    const unsigned b0 = kDcChunks * kCB * l;                              /* first block */
     const unsigned t = threadIdx.x, lane = t & 63u, wave = t >> 6;
 #pragma unroll
     for (int b = 0; b < 16; b++) cnt[b][t] = 0;      /* own column: no barrier before use */
@@ -368,7 +373,7 @@ int hip_rc2(hipError_t e) { return e == hipSuccess ? JPGX_OK : JPGX_EHIP; }
 
 size_t nchunks_of(size_t nb_y, size_t nb_c)
 {
-    return (nb_y + kChunk - 1) / kChunk + 2 * ((nb_c + kChunk - 1) / kChunk);
+    return (nb_y + kCB - 1) / kCB + 2 * ((nb_c + kCB - 1) / kCB);
 }
 
 size_t round8(size_t x) { return (x + 7) / 8 * 8; }
@@ -418,8 +423,8 @@ int jpgx_entropy_stats_gpu_batch(const int16_t *d_coef, size_t coef_frame_stride
     c.nb[0] = (unsigned)nb_y;
     c.nb[1] = c.nb[2] = (unsigned)nb_c;
     c.first[0] = 0;
-    c.first[1] = (unsigned)((nb_y + kChunk - 1) / kChunk);
-    c.first[2] = c.first[1] + (unsigned)((nb_c + kChunk - 1) / kChunk);
+    c.first[1] = (unsigned)((nb_y + kCB - 1) / kCB);
+    c.first[2] = c.first[1] + (unsigned)((nb_c + kCB - 1) / kCB);
     c.off[0] = 0;
     c.off[1] = (unsigned)nb_y;
     c.off[2] = (unsigned)(nb_y + nb_c);
