@@ -199,6 +199,7 @@ __global__ __launch_bounds__(kChunk) void k_ent_ac(const Chunks c)
  * earlier chunk sums, the scan, d_l and the classes; its class counts go to column blockIdx.x of
  * the DC count rows (frame f's DC workgroups are f dc_groups() .. + dc_groups() - 1, luma first). */
 constexpr int kDcChunks = 2048 / kCB;   /* 2,048 blocks per DC workgroup */
+static_assert(kCB <= 2048 && 2048 % kCB == 0, "JX_ENT_LOADS: a power of two up to 64 (DC workgroups tile whole chunks)");
 __global__ __launch_bounds__(kChunk) void k_ent_dc(const Chunks c)
 {
     __shared__ uint32_t cnt[16][kChunk];              /* [class / 2][thread], 16-bit halves: classes 0..31 */
@@ -401,7 +402,7 @@ int jpgx_entropy_stats_gpu_batch(const int16_t *d_coef, size_t coef_frame_stride
     const size_t nbf = nb_y + 2 * nb_c;
     if (!d_coef || !d_dc || !d_hist || ((uintptr_t)d_coef & 15) || nb_y == 0 || nframes == 0 ||
         coef_frame_stride < nbf * 64 || coef_frame_stride % 64 || nbf >= (1ull << 31) ||
-        nframes * nbf >= (1ull << 31) || (carry && nframes != 1))
+        nframes * nbf >= (1ull << 31) || nframes > 65535 || (carry && nframes != 1))
         return JPGX_EARG;
     const size_t nchf = nchunks_of(nb_y, nb_c), nch = nchf * nframes;
     if (nch >= (1ull << 31))

@@ -84,6 +84,31 @@ __host__ __device__ constexpr unsigned mx_pos(unsigned c, unsigned jb)
 {
     return c == 0 ? jb : (c == 1 ? 12u + jb : (jb < 4 ? 8u + jb : 16u + jb));
 }
+/* k_mxs's stage (round 6): 128-B blocks with no padding, the eight 16-byte pieces of the block in
+ * slot s XOR-swizzled by mxs_h(s).  A ds_write_b16 of the column pass puts, per 32-lane half, the
+ * coefficients (v, u = 0..7) of four blocks -- slots {s, s + 1, s + 12, s + 13} (+ 4 or 8 for the
+ * other columns), whose swizzles are {0, 5, 2, 7} -- on the 32 banks: every one of the 24 writes of
+ * a step is at most 2-way (the minimum: rows v = 1..6 use three or four pieces in one dword
+ * position, 12-16 dwords for the 8 banks of that position), 36 extra bank cycles per step against
+ * 60 (with three-way writes) for the 144-B padded slots of rounds 2-5; the 16-byte stage reads
+ * (ro, rcb, rr: piece l & 7 of block l >> 3) stay conflict-free (the padded slots: 12 extra cycles).
+ * A lane's three blocks (s, s + 4, s + 8) share one swizzle, so one set of addresses serves them. */
+constexpr unsigned kBSs = 128;
+__host__ __device__ constexpr unsigned mxs_h(unsigned s)
+{
+    return ((s & 1u) ? 5u : 0u) ^ (s >= 12u ? 2u : 0u);
+}
+__host__ __device__ constexpr unsigned mxs_piece(unsigned s, unsigned p)
+{
+    return kBSs * s + 16u * (p ^ mxs_h(s));
+}
+__host__ __device__ constexpr unsigned mxs_coef(unsigned s, unsigned z)
+{
+    return mxs_piece(s, z >> 3) + 2u * (z & 7u);
+}
+static_assert(mxs_h(0) == mxs_h(4) && mxs_h(0) == mxs_h(8) && mxs_h(1) == mxs_h(9) && mxs_h(12) == mxs_h(16) &&
+                  mxs_h(12) == mxs_h(20) && mxs_h(13) == mxs_h(21),
+              "a lane's three column blocks share a swizzle");
 /* per-lane scales / band limits, shared by the workgroup: table t, half h (pairs 2h, 2h + 1 in
  * jx_pk_k order), profile j = lane & 15 -- a column's read of one (t, h) by the wave touches 16
  * consecutive 16-byte entries, every bank once.  4:4:4 (compacted to MxsTab below): t = Wy|b, Ly|b
@@ -501,7 +526,7 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
         const unsigned jb = mx_col_block(k, sl);
         int val;
         const bool ok = mx_exact_one(MxSmp1{mx_lds((void *)slot) + 24u * jb, 192u}, ch, u, v, xt, val);
-        return mx_put_one(L.stage, kBS * mx_pos(ch, jb) + 2u * xt.scan(u, v), ok, val);
+        return mx_put_one(L.stage, mxs_coef(mx_pos(ch, jb), xt.scan(u, v)), ok, val);
     });
     for (;;) {
         const uint64_t act = __ballot(bits != 0);
@@ -522,8 +547,8 @@ __device__ __forceinline__ void mx_exact_inline(Lds &L, const uint8_t *slot, uin
         const unsigned jb = mx_col_block(k, sl);
         const int val = mx_exact_coef<true>(MxSmp1{mx_lds((void *)slot) + 24u * jb, 192u}, ch, u, v, x, xt);
         if (live && x == 7)
-            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + kBS * mx_pos(ch, jb) +
-                                                           2u * xt.scan(u, v)) = (int16_t)val;
+            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + mxs_coef(mx_pos(ch, jb), xt.scan(u, v))) =
+                (int16_t)val;
         mx_wave_sync();
     }
 }
@@ -744,7 +769,7 @@ constexpr unsigned kMxsC = 3;           /* steps per wave = LDS input slots */
 constexpr unsigned kMxsWPG = 4;         /* waves per workgroup (one LDS image) */
 struct alignas(16) MxsLds {
     uint8_t ring[kMxsC][kSlot];         /* pixels, [y][24 jb + k]                       */
-    uint8_t stage[24 * kBS];            /* zig-zag stage (mx_pos)                       */
+    uint8_t stage[24 * kBSs];           /* zig-zag stage (mx_pos, mxs_coef)             */
     uint16_t task[8];                   /* inline exact batch                           */
 };
 static_assert(sizeof(MxsLds) % 16 == 0, "16-byte aligned LDS regions");
@@ -894,14 +919,17 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
 
     /* lane constants */
     const unsigned m = lane & 15u, q = lane >> 4;
-    const uint32_t aoff = 192u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 0u);
+    /* lanes 48..63 (the bias / zero rows k = 24..31) use no pixel byte: they read lanes 32..47's
+     * addresses, an LDS broadcast (round 6: their own addresses made every A read 2-way in the
+     * upper half of the wave) */
+    const uint32_t aoff = 192u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 2u);
     const uint32_t s0 = q < 3 ? kSelLo : kSelOne;
     const uint32_t s1 = q < 3 ? kSelHi : kSelZero;
     const uint32_t s2 = q < 3 ? kSelLo : kSelZero;
     const uint32_t so0 = lane * 16u, so1 = so0 + g.nb * 128u, so2 = so1 + g.nb * 128u;
-    const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
-    const uint32_t rr = ro + ((lane >> 3) < 4 ? 8u : 16u) * kBS;
-    const uint32_t rcb = 12u * kBS + ro;
+    const uint32_t ro = mxs_piece(lane >> 3, lane & 7u);
+    const uint32_t rr = mxs_piece((lane >> 3) + ((lane >> 3) < 4 ? 8u : 16u), lane & 7u);
+    const uint32_t rcb = mxs_piece(12u + (lane >> 3), lane & 7u);
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
     const MxExLds xt{s_img.ex, s_img.scan_t};
 
@@ -917,10 +945,14 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
      * global load: its wait would drain the pixel DMA too) */
     uint32_t za[8];
     {
-        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * mx_pos(j >> 3, gq);
+        const unsigned s = mx_pos(j >> 3, gq);
+        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBSs * s, hs = mxs_h(s);
         const mx_u2 sc = *(const mx_u2 *)&s_img.scan_t[u][0];
 #pragma unroll
-        for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
+        for (int v = 0; v < 8; v++) {
+            const uint32_t z = (v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu;
+            za[v] = base + 16u * ((z >> 3) ^ hs) + 2u * (z & 7u);
+        }
     }
     /* the B operands; reloaded after an exact pass, so that their registers are free during it */
     mx_u4 B[kParts][3];
@@ -990,7 +1022,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
         __builtin_amdgcn_sched_barrier(0);
         cr[1][3] = mx_mma(A11, B[1][2], z);
         __builtin_amdgcn_sched_barrier(0);
-        mx_column_t<4 * kBS>(acc[1], w0, limc0, tb, 0, j, za, fl, 1, &cr[1][3]);
+        mx_column_t<4 * kBSs>(acc[1], w0, limc0, tb, 0, j, za, fl, 1, &cr[1][3]);
         __builtin_amdgcn_sched_barrier(0);
         const uint8_t *const ob = (const uint8_t *)S.dst;
         /* the launch's last step: flags of its clamped copies are dropped (never stored) */
@@ -1006,7 +1038,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
             const unsigned l = mx_lane();
             const unsigned bl = S.b + (l >> 3), b = bl < g.total ? bl : g.total - 1u;
             const unsigned f = b / g.nb, bi = b - f * g.nb;
-            const mx_u4 val = *(const mx_u4 *)(L.stage + kBS * mx_pos((unsigned)c, l >> 3) + (l & 7u) * 16u);
+            const mx_u4 val = *(const mx_u4 *)(L.stage + mxs_piece(mx_pos((unsigned)c, l >> 3), l & 7u));
             if (bl < g.total)
                 __builtin_nontemporal_store(
                     val, (mx_u4 *)(g.out + (long long)f * g.ofstride + ((long long)c * g.nb + bi) * 64 + (l & 7u) * 8));
@@ -1025,7 +1057,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
         for (int i = 0; i < 4; i++)                    /* scalar adds (no packed fp32, mx_unpack8) */
             acc[2][i] = mx_f4{cr[0][i].x + cr[1][i].x, cr[0][i].y + cr[1][i].y, cr[0][i].z + cr[1][i].z,
                               cr[0][i].w + cr[1][i].w};
-        mx_column_t<8 * kBS, true>(acc[2], w0, limc2, tb, 2, j, za, fl, 2);
+        mx_column_t<8 * kBSs, true>(acc[2], w0, limc2, tb, 2, j, za, fl, 2);
         mx_wave_sync();
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
             clamp(fl);
@@ -1267,7 +1299,7 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
 
     /* lane constants */
     const unsigned m = lane & 15u, q = lane >> 4;
-    const uint32_t aoff = 192u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 0u);
+    const uint32_t aoff = 192u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 2u);
     const uint32_t s0 = q < 3 ? kSelLo : kSelOne;
     const uint32_t s1 = q < 3 ? kSelHi : kSelZero;
     const uint32_t s2 = q < 3 ? kSelLo : kSelZero;
@@ -1752,7 +1784,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
 
     /* lane constants */
     const unsigned m = lane & 15u, q = lane >> 4;
-    const uint32_t aoff = 96u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 0u);
+    const uint32_t aoff = 96u * (m & 3u) + 24u * (m >> 2) + 8u * (q < 3 ? q : 2u);
     const uint32_t s0 = q < 3 ? kSelLo : kSelOne;
     const uint32_t s1 = q < 3 ? kSelHi : kSelZero;
     const uint32_t s2 = q < 3 ? kSelLo : kSelZero;

@@ -276,17 +276,24 @@ def entropy_stats_gpu(d_coef, nb_y: int, nb_c: int, carry=None, stream=None):
 
 
 def entropy_stats_gpu_batch(d_coef, nb_y: int, nb_c: int, stream=None):
-    """The same over a frame batch d_coef [nframes][>= nb_y + 2 nb_c][64] (int16, contiguous
-    frames): (dc int32 [nframes][nb_y + 2 nb_c], hist uint32 [nframes][4][257]), every frame from
-    the image start."""
+    """The same over a frame batch d_coef [nframes][>= nb_y + 2 nb_c][64] (int16; each frame
+    contiguous, frames d_coef.stride(0) elements apart, e.g. a slice of a padded batch):
+    (dc int32 [nframes][nb_y + 2 nb_c], hist uint32 [nframes][4][257]), every frame from the image
+    start."""
     import torch
+    if d_coef.dtype != torch.int16 or d_coef.dim() < 2:
+        raise ValueError("entropy_stats_gpu_batch: d_coef must be an int16 [nframes][...] tensor")
+    if not d_coef[0].is_contiguous() or d_coef[0].numel() < (nb_y + 2 * nb_c) * 64:
+        raise ValueError("entropy_stats_gpu_batch: each frame must be contiguous and hold nb_y + 2 nb_c blocks")
+    if d_coef.data_ptr() % 16 or d_coef.stride(0) % 64:
+        raise ValueError("entropy_stats_gpu_batch: 16-byte aligned frames, a stride of whole blocks")
     dev = d_coef.device
     nf = d_coef.shape[0]
     dc = torch.empty((nf, nb_y + 2 * nb_c), dtype=torch.int32, device=dev)
     hist = torch.empty((nf, 4, 257), dtype=torch.int32, device=dev)
     ws = torch.empty(max(int(lib.jpgx_entropy_workspace_size_batch(nb_y, nb_c, nf)), 8),
                      dtype=torch.uint8, device=dev)
-    _check(lib.jpgx_entropy_stats_gpu_batch(d_coef.data_ptr(), d_coef[0].numel(), nf, nb_y, nb_c, None,
+    _check(lib.jpgx_entropy_stats_gpu_batch(d_coef.data_ptr(), d_coef.stride(0), nf, nb_y, nb_c, None,
                                             dc.data_ptr(), hist.data_ptr(), ws.data_ptr(), ws.numel(),
                                             _stream_ptr(stream)), "jpgx_entropy_stats_gpu_batch")
     return dc, hist

@@ -35,7 +35,7 @@ def batch():
 
 @pytest.fixture(params=["xform", "mx"])
 def kernel(request, monkeypatch):
-    """k_mx (the product library) and k_xform (the test-only libjpgx_alt.so)"""
+    """k_mxs (the product library's 4:4:4 kernel) and k_xform (the test-only libjpgx_alt.so)"""
     if request.param == "xform":
         monkeypatch.setattr(jpgx, "lib", jpgx.alt_library())
     return request.param
@@ -96,8 +96,8 @@ def test_batch64_as_eight_rank_stripes(batch, cuda, kernel):
 
 
 def test_batch64_single_launch(batch, cuda, kernel):
-    """The same 64 frames as ONE launch on one GPU (no stripes): 2025 tiles per frame, about
-    40 tiles per persistent wave."""
+    """The same 64 frames as ONE launch on one GPU (no stripes): 1,036,800 steps of 8 blocks,
+    three steps per short-lived k_mxs wave (345,600 waves, steps crossing frame ends)."""
     import torch
     W, H, q = batch["W"], batch["H"], batch["quality"]
     out = _run_rank(bench.rank_plan(W, H, FPG * NGPU, 1, 0, jpgx), W, H, q, cuda)
@@ -110,7 +110,8 @@ def test_batch64_single_launch(batch, cuda, kernel):
 
 def test_batch_force_exact_multi_tile(batch, cuda, kernel):
     """FLAG_FORCE_EXACT over 8 frames in one launch: every coefficient through the in-kernel
-    exact fp64 pass, with queues that overflow and drain mid-run on every tile."""
+    exact fp64 pass (k_mxs: every step's 192 coefficients in 8-lane batches, inline before the
+    step's stores; k_xform: its per-tile queues overflowing and draining on every tile)."""
     import torch
     W, H, q = batch["W"], batch["H"], batch["quality"]
     plan = bench.rank_plan(W, H, FPG, 1, 0, jpgx)

@@ -230,3 +230,55 @@ def test_batch_entry_point_rejects_bad_arguments():
     assert args(3 * nb * 64 + 8, 2, None) == jpgx.EARG                 # not whole blocks
     assert args(3 * nb * 64, 0, None) == jpgx.EARG                     # no frames
     assert args(3 * nb * 64, 2, ctypes.cast(carry, ctypes.c_void_p)) == jpgx.EARG   # carry with a batch
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sr", [0, 1, 2])
+def test_gpu_stats_batch_sliced_and_subsampled(cuda, sr):
+    """A sliced view of a padded batch (frames nb_y + 2 nb_c + 5 blocks apart, the first
+    nb_y + 2 nb_c of each used: the frame stride is the tensor's, not the slice's size) and
+    subsampled layouts (nb_c = nb_y / 2, nb_y / 4: different DC workgroup counts per channel)
+    equal one call per frame and the oracle."""
+    import torch
+    W, H, F = 256, 192, 3
+    fl = jpgx.FLAG_SUBSAMPLE if sr else 0
+    nb = (H // 8) * (W // 8)
+    nbc = jpgx.chroma_blocks(W, 0, H // 8, sr, fl)
+    per = nb + 2 * nbc
+    pad = torch.zeros((F, per + 5, 64), dtype=torch.int16, device=cuda)
+    for f in range(F):
+        pad[f, :per] = jpgx.encode_blocks(torch.from_numpy(O.gen_splitmix(60 + f, W, H)).to(cuda),
+                                          60 + 10 * f, sr, flags=fl).reshape(per, 64)
+    view = pad[:, :per]
+    assert not view.is_contiguous() and view.stride(0) == (per + 5) * 64
+    dcb, hb = jpgx.entropy_stats_gpu_batch(view, nb, nbc)
+    for f in range(F):
+        dc, h = jpgx.entropy_stats_gpu(pad[f, :per].contiguous(), nb, nbc)
+        assert torch.equal(dcb[f], dc) and torch.equal(hb[f], h), f
+        rdc, rh = O.entropy_stats(pad[f, :per].cpu().numpy(), nb, nbc)
+        assert np.array_equal(dcb[f].cpu().numpy(), rdc) and np.array_equal(hb[f].cpu().numpy(), rh)
+
+
+def test_batch_binding_rejects_bad_layouts():
+    """The Python binding refuses what the C entry point cannot see (no device needed: CPU
+    tensors stand in, the checks run before any call)."""
+    import torch
+    nb = 16
+    with pytest.raises(ValueError):
+        jpgx.entropy_stats_gpu_batch(torch.zeros((2, 3 * nb, 64), dtype=torch.int32), nb, nb)
+    with pytest.raises(ValueError):                       # frames not contiguous
+        jpgx.entropy_stats_gpu_batch(torch.zeros((2, 64, 3 * nb), dtype=torch.int16).transpose(1, 2), nb, nb)
+    with pytest.raises(ValueError):                       # frame shorter than nb_y + 2 nb_c blocks
+        jpgx.entropy_stats_gpu_batch(torch.zeros((2, 3 * nb - 1, 64), dtype=torch.int16), nb, nb)
+
+
+def test_batch_entry_point_rejects_too_many_frames():
+    """nframes > 65535 (the histogram launch's grid.y) is refused up front, before any launch."""
+    import ctypes
+    L = jpgx.lib
+    nb = 1
+    need = int(L.jpgx_entropy_workspace_size_batch(nb, nb, 65536))
+    ws = ctypes.create_string_buffer(need + 16)
+    p16 = ctypes.addressof(ws) + (-ctypes.addressof(ws)) % 16
+    assert L.jpgx_entropy_stats_gpu_batch(p16, 3 * 64, 65536, nb, nb, None, p16, p16, p16, need,
+                                          None) == jpgx.EARG

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True, params=["xform", "mx"])
 def kernel(request, monkeypatch):
-    """Every parity test runs on both 4:4:4 kernels: k_mx (colour + row DCT on the matrix
+    """Every parity test runs on both 4:4:4 kernels: k_mxs (colour + row DCT on the matrix
     cores, csrc/jpgx_mx.hip: the product library's kernel) and k_xform (all-VALU), which only
     the test-only cross-check library libjpgx_alt.so dispatches."""
     if request.param == "xform":

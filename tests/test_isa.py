@@ -35,7 +35,7 @@ def test_mfma_operand_rule(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "mfma_war_check.py"), "--no-pk", str(asm)]
                        + names, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
-    assert r.stdout.count(" 0 packed-fp32 VALU instruction(s)") == len(names), r.stdout
+    assert r.stdout.count(" 0 packed VALU instruction(s)") == len(names), r.stdout
     # and no scratch, no VGPR / SGPR spills
     text = asm.read_text()
     for n in ("k_mxs", "k_mxs422", "k_mxs420"):
@@ -225,7 +225,7 @@ def test_no_packed_fp32_rule(tmp_path):
         return subprocess.run([sys.executable, tool, "--no-pk", str(s), "k_mx"], capture_output=True, text=True)
 
     bad = run(_BGL_EXCERPT)
-    assert bad.returncode == 1 and " 5 packed-fp32 VALU instruction(s)" in bad.stdout, bad.stdout
+    assert bad.returncode == 1 and " 5 packed VALU instruction(s)" in bad.stdout, bad.stdout
     scalar = run(_BGL_EXCERPT[:5] + ["\tv_add_f32_e32 v46, v58, v62", "\tv_add_f32_e32 v47, v59, v63",
                                      "\tv_fmac_f32_e32 v52, 0x3f5906bd, v46", "\ts_endpgm"])
     assert scalar.returncode == 0, scalar.stdout
@@ -237,24 +237,38 @@ def test_no_packed_fp32_rule(tmp_path):
 
 
 def test_no_packed_fp32_rule_rejects_recorded_failing_builds():
-    """every recorded failing build of the MFMA kernels (round-4b variants, built by
-    tools/build_variants.sh from tools/probes/jpgx_mx_r5_knobs.patch) fails --no-pk, whatever the
-    other rules said of it: bgl / bglpad (B from global memory), w1 (one-wave workgroups), and the
-    compact-table exact pass without its lgkmcnt(0) (ucc); the round-4b product too -- it passed by
-    timing.  Checked on the ISA files that exist in this checkout (build/variants, gitignored)."""
+    """every recorded failing build of the MFMA kernels fails --no-pk, whatever the other rules said
+    of it.  Committed excerpts (tests/isa_fixtures/: k_mxs of the round-4b variants bgl -- B from
+    global memory --, w1 -- one-wave workgroups -- and ucc -- the compact-table exact pass without
+    its lgkmcnt(0) --, from 40 lines before the first MFMA to 200 after the first packed op) always
+    run; the whole variant ISA (build/variants, gitignored, tools/build_variants.sh over
+    tools/probes/jpgx_mx_r5_knobs.patch) is checked too where this checkout has it."""
     tool = os.path.join(REPO, "tools", "mfma_war_check.py")
+    fix = os.path.join(REPO, "tests", "isa_fixtures")
+    for name in ("bgl", "w1", "ucc"):
+        f = os.path.join(fix, name + "_k_mxs.isa")
+        r = subprocess.run([sys.executable, tool, "--no-pk", f, "k_mxs"], capture_output=True, text=True)
+        assert r.returncode == 1 and "16 MFMAs" in r.stdout and "packed VALU" in r.stdout, (name, r.stdout)
     vdir = os.path.join(PKG, "build", "variants")
-    seen = 0
     for name in ("bgl", "bglpad", "w1", "ucc", "dump3"):
         f = os.path.join(vdir, name + ".s")
-        if not os.path.exists(f):
-            continue
-        seen += 1
-        r = subprocess.run([sys.executable, tool, "--no-pk", f, "k_mxs"], capture_output=True, text=True)
-        assert r.returncode == 1 and "packed-fp32" in r.stdout, (name, r.stdout)
-    if seen == 0:
-        import pytest
-        pytest.skip("no variant ISA in this checkout")
+        if os.path.exists(f):
+            r = subprocess.run([sys.executable, tool, "--no-pk", f, "k_mxs"], capture_output=True, text=True)
+            assert r.returncode == 1 and "packed VALU" in r.stdout, (name, r.stdout)
+
+
+def test_no_packed_rule_covers_16bit_packed_forms(tmp_path):
+    """the 16-bit packed VALU forms were never probed after MFMAs, so --no-pk refuses
+    them too; only v_pk_mov_b32 (a move, used by the compiler to pair registers) passes"""
+    tool = os.path.join(REPO, "tools", "mfma_war_check.py")
+    s = tmp_path / "fake.s"
+    mfma = "\tv_mfma_f32_16x16x32_f16 v[8:11], v[0:3], v[4:7], 0"
+    for op in ("v_pk_add_f16 v20, v21, v22", "v_pk_fma_f16 v20, v21, v22, v23", "v_pk_mul_lo_u16 v20, v21, v22",
+               "v_pk_add_u16 v20, v21, v22", "v_pk_mul_f32 v[20:21], v[22:23], v[24:25]"):
+        s.write_text("\n".join(["_ZN12_GLOBAL__N_14k_mxE13jx_xform_args:", mfma, "\t" + op, "\ts_endpgm",
+                                ".Lfunc_end0:", ""]))
+        r = subprocess.run([sys.executable, tool, "--no-pk", str(s), "k_mx"], capture_output=True, text=True)
+        assert r.returncode == 1 and " 1 packed VALU" in r.stdout, (op, r.stdout)
 
 
 def test_m0_rule_catches_a_reader_after_asm():
