@@ -23,7 +23,7 @@
  *   with the colour conversion and row DCT on the matrix cores.
  *
  * Compiled with FP contraction off; the fast path uses explicit fmaf.  Variants of k_xform
- * measured slower are kept out of this file: tools/probes/k_xform_variants.patch.
+ * measured slower are kept out of this file: tools/probes/k_xform_variants.patch (git history: 63924df).
  */
 #include <hip/hip_runtime.h>
 #include <math.h>

@@ -242,7 +242,7 @@ def test_no_packed_fp32_rule_rejects_recorded_failing_builds():
     global memory --, w1 -- one-wave workgroups -- and ucc -- the compact-table exact pass without
     its lgkmcnt(0) --, from 40 lines before the first MFMA to 200 after the first packed op) always
     run; the whole variant ISA (build/variants, gitignored, tools/build_variants.sh over
-    tools/probes/jpgx_mx_r5_knobs.patch) is checked too where this checkout has it."""
+    tools/probes/jpgx_mx_r5_knobs.patch (git history: 63924df)) is checked too where this checkout has it."""
     tool = os.path.join(REPO, "tools", "mfma_war_check.py")
     fix = os.path.join(REPO, "tests", "isa_fixtures")
     for name in ("bgl", "w1", "ucc"):

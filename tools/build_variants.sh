@@ -14,11 +14,13 @@ while [ $# -ge 2 ]; do
       $flags -c "$PKG/csrc/jpgx_kernels.hip" -o "$obj"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-slp-vectorize -I"$ROOT/include" \
       $flags -c "${MX_SRC:-$PKG/csrc/jpgx_mx.hip}" -o "$PKG/build/variants/${name}_mx.o"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-slp-vectorize -I"$ROOT/include" \
+      $flags -c "$PKG/csrc/jpgx_entropy.hip" -o "$PKG/build/variants/${name}_ent.o"
   g++ -O2 -fPIC -std=c++17 -ffp-contract=off -I"$ROOT/include" $flags \
       -c "$PKG/csrc/jpgx_plan.cpp" -o "$PKG/build/variants/${name}_plan.o"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libjpgx_$name.so" "$obj" "$PKG/build/variants/${name}_mx.o" \
       "$PKG/build/variants/${name}_plan.o" "$PKG"/build/jpgx_block.o "$PKG"/build/jpgx_jpgdata.o \
-      "$PKG"/build/jpgx_jfif.o "$PKG"/build/jpgx_entropy.o "$PKG"/build/jpgx_host.o -lpthread
+      "$PKG"/build/jpgx_jfif.o "$PKG/build/variants/${name}_ent.o" "$PKG"/build/jpgx_host.o -lpthread
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -I"$ROOT/include" \
       $flags --cuda-device-only -S "${MX_SRC:-$PKG/csrc/jpgx_mx.hip}" -o "$PKG/build/variants/$name.s"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -I"$ROOT/include" \
