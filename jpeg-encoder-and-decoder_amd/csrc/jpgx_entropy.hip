@@ -38,6 +38,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "jpgx_internal.h"
 
 namespace {
@@ -84,6 +86,169 @@ __device__ __forceinline__ void chunk_of(const Chunks &c, unsigned chunk, unsign
     k0 = (l - c.first[ch]) * kCB;
 }
 
+#ifndef JX_ENT_LANEBLK
+#define JX_ENT_LANEBLK 1
+#endif
+#if JX_ENT_LANEBLK
+/*
+ * Round 6: one lane per block.  The wave's 16 loads stay the coalesced 1-KiB loads (lane l: 16 bytes
+ * of block l >> 3); each half of them (64 blocks) goes through a per-wave LDS tile so that lane b
+ * then holds all 64 coefficients of block b, and walks them in zig-zag order with the previous
+ * nonzero position in a register -- no cross-lane max-scan.  A lane walks its two blocks (one per
+ * half) side by side (two independent chains).  Per coefficient: its class (frexp of the float, 0
+ * for 0), the run since the previous nonzero, and ONE LDS add into a count bin:
+ *   nonzero:  bin ((run & 15) | class), the reference's symbol (huffman.c:199-218, `run | size`);
+ *   zero:     bin 32 + (run & 15) -- a zero whose run is 15 mod 16 completes a group of 16 zeros, so
+ *             bin 47 counts the ZRLs (huffman.c:199-204: (run >> 4) ZRLs before a symbol), except
+ *             for the groups in the block's trailing zeros (no ZRL: EOB, :219-221), floor((63 - L)
+ *             / 16) for the last nonzero position L, subtracted per block.
+ * Count columns are per lane & 31 and shared by the workgroup's waves (an LDS add is atomic across
+ * waves, and lanes l, l + 32 are serviced in different LDS cycles), so the counters take 6 KiB and
+ * four workgroups fit a CU.  The round-5 form (8 lanes per block, an 8-lane max-scan through
+ * ds_bpermute, 8 SGPR masks per load that the compiler spilled into VGPR lanes, per-thread columns
+ * of 32 KiB) issued ~1.6x the VALU per coefficient: JX_ENT_LANEBLK=0.
+ */
+constexpr int kBins = 48;                        /* AC symbols 0..31, zero coefficients 32 + (run & 15) */
+typedef uint32_t ent_u4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) ent_u4 ent_l4;
+typedef __attribute__((address_space(3))) uint32_t ent_l32;
+
+/* the transposition tile: block b (0..63) in 128 bytes at 128 b, its 16-byte pieces XOR-swizzled by
+ * (b >> 1) & 7 -- the piece writes (8 contiguous lanes = one block) and the per-lane block reads (a
+ * ds_read_b128 16-lane group: 16 distinct (b & 1, (b >> 1) & 7)) hit distinct banks */
+__device__ __forceinline__ unsigned ent_tile(unsigned b, unsigned piece)
+{
+    return 128u * b + 16u * (piece ^ ((b >> 1) & 7u));
+}
+
+/* the 8 loads qh (64 blocks) through the tile into u: lane b's block b */
+__device__ __forceinline__ void ent_transpose(const uint4 (&qh)[8], uint8_t *tile, unsigned lane, uint32_t (&u)[32])
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     /* earlier tile reads first */
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const uint32_t x = qh[r].x, y = qh[r].y, zz = qh[r].z, ww = qh[r].w;
+        *(ent_l4 *)(tile + ent_tile(8u * r + (lane >> 3), lane & 7u)) = ent_u4{x, y, zz, ww};
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     /* other lanes' writes first */
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const ent_u4 x = *(const ent_l4 *)(tile + ent_tile(lane, (unsigned)r));
+        u[4 * r] = x.x, u[4 * r + 1] = x.y, u[4 * r + 2] = x.z, u[4 * r + 3] = x.w;
+    }
+}
+
+/* coefficient k of a block: its count bin (above) and the previous-nonzero update */
+__device__ __forceinline__ void ent_coef(const uint32_t (&u)[32], int k, uint32_t &prev, uint32_t colb)
+{
+    const uint32_t word = u[k >> 1];
+    const int v = (k & 1) ? (int)word >> 16 : (int)(int16_t)(word & 0xffffu);
+    /* class = frexp exponent of the exact float (0 for 0), huffman.c:226-235 */
+    const uint32_t cls = (uint32_t)__builtin_amdgcn_frexp_expf((float)v);
+    const uint32_t run = (uint32_t)(k - 1) - prev;
+    const bool nz = cls != 0;
+    const uint32_t bin = (run & 15u) | (nz ? cls : 32u);
+    __hip_atomic_fetch_add((ent_l32 *)(uintptr_t)(colb + bin * 128u), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+    prev = nz ? (uint32_t)k : prev;
+}
+
+/* a block's end: EOB, DC word and chunk sum (live blocks), the trailing-zero ZRL correction (every
+ * block: a dead block reads as zeros and fed bin 47 too) */
+__device__ __forceinline__ void ent_block_end(const uint32_t (&u)[32], uint32_t prev, unsigned blk, unsigned n,
+                                              uint32_t &eob, uint32_t &zcor, long long &w, const Chunks &c,
+                                              unsigned f, int ch, unsigned k0)
+{
+    zcor += (63u - prev) >> 4;
+    if (blk < n) {
+        eob += (u[31] >> 16) == 0 ? 1u : 0u;          /* huffman.c:219-221 */
+        const int v0 = (int)(int16_t)(u[0] & 0xffffu);
+        c.dcv[f * c.nbf + c.off[ch] + k0 + blk] = (int16_t)v0;
+        w += ((k0 + blk) & 1u) ? -(long long)v0 : (long long)v0;
+    }
+}
+
+__global__ __launch_bounds__(kChunk, 4) void k_ent_ac(const Chunks c)
+{
+    __shared__ uint32_t cnt[kBins][32];              /* [bin][lane & 31], shared by the 4 waves */
+    __shared__ __attribute__((aligned(16))) uint8_t tile[kChunk / 64][64 * 128];
+    __shared__ long long wsum[kChunk / 64];
+    __shared__ uint32_t wez[kChunk / 64][2];
+    unsigned f, k0;
+    int ch;
+    chunk_of(c, blockIdx.x, f, ch, k0);
+    const unsigned t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    for (unsigned i = t; i < (unsigned)kBins * 32u; i += kChunk) (&cnt[0][0])[i] = 0;
+    const unsigned n = min(c.nb[ch] - k0, (unsigned)kCB);
+    const int16_t *z = c.coef + (f * c.fstride + c.off[ch] + k0) * 64;
+    static_assert(kLoads == 16, "two halves of 64 blocks per wave");
+    uint4 qa[8], qb[8];                               /* all 16 loads in flight at once */
+#pragma unroll
+    for (int it = 0; it < 8; it++) {
+        const unsigned blk = 8u * kLoads * wave + 8u * (unsigned)it + (lane >> 3);
+        qa[it] = *(const uint4 *)(z + (size_t)(blk < n ? blk : 0u) * 64 + 8u * (lane & 7u));
+    }
+#pragma unroll
+    for (int it = 0; it < 8; it++) {
+        const unsigned blk = 8u * kLoads * wave + 64u + 8u * (unsigned)it + (lane >> 3);
+        qb[it] = *(const uint4 *)(z + (size_t)(blk < n ? blk : 0u) * 64 + 8u * (lane & 7u));
+    }
+    const unsigned ba = 8u * kLoads * wave + lane, bb = ba + 64u;      /* this lane's two blocks */
+    uint32_t ua[32], ub[32];
+    ent_transpose(qa, tile[wave], lane, ua);
+    ent_transpose(qb, tile[wave], lane, ub);
+    if (n < (unsigned)kCB) {                          /* the channel's last chunk: dead blocks read as zeros */
+        const uint32_t la = ba < n ? ~0u : 0u, lb = bb < n ? ~0u : 0u;
+#pragma unroll
+        for (int i = 0; i < 32; i++) ua[i] &= la, ub[i] &= lb;
+    }
+    __syncthreads();                                  /* the counters are zeroed */
+    const uint32_t colb = (uint32_t)(uintptr_t)(ent_l32 *)&cnt[0][lane & 31u];
+    uint32_t pa = 0, pb = 0;                          /* previous nonzero: the DC position */
+#pragma unroll
+    for (int k = 1; k < 64; k++) {
+        ent_coef(ua, k, pa, colb);
+        ent_coef(ub, k, pb, colb);
+    }
+    uint32_t eob = 0, zcor = 0;
+    long long w = 0;
+    ent_block_end(ua, pa, ba, n, eob, zcor, w, c, f, ch, k0);
+    ent_block_end(ub, pb, bb, n, eob, zcor, w, c, f, ch, k0);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        w += __shfl_xor(w, o, 64);
+        eob += __shfl_xor(eob, o, 64);
+        zcor += __shfl_xor(zcor, o, 64);
+    }
+    if (lane == 0) {
+        wsum[wave] = w;
+        wez[wave][0] = eob;
+        wez[wave][1] = zcor;
+    }
+    __syncthreads();
+    if (t <= (unsigned)kSyms) {                       /* symbol t (row 0: EOB), t == 32: ZRL */
+        uint32_t tot = 0;
+        if (t == 0) {
+#pragma unroll
+            for (int i = 0; i < kChunk / 64; i++) tot += wez[i][0];
+        } else {
+            const unsigned bin = t < (unsigned)kSyms ? t : 47u;
+#pragma unroll
+            for (unsigned j = 0; j < 32; j++) tot += cnt[bin][(j + t) & 31u];     /* rotated: distinct banks */
+            if (t == (unsigned)kSyms) {
+#pragma unroll
+                for (int i = 0; i < kChunk / 64; i++) tot -= wez[i][1];
+            }
+        }
+        c.cnt[(size_t)t * c.nchunks + blockIdx.x] = tot;
+    } else if (t == (unsigned)kSyms + 1) {
+        long long ws = 0;
+#pragma unroll
+        for (int i = 0; i < kChunk / 64; i++) ws += wsum[i];
+        c.part[blockIdx.x] = ws;
+    }
+}
+#else
 __global__ __launch_bounds__(kChunk) void k_ent_ac(const Chunks c)
 {
     __shared__ uint32_t cnt[kSyms][kChunk];          /* [symbol][thread] */
@@ -194,6 +359,8 @@ __global__ __launch_bounds__(kChunk) void k_ent_ac(const Chunks c)
         c.part[blockIdx.x] = ws;
     }
 }
+
+#endif
 
 /* DC pass over kDcChunks consecutive chunks of one channel (8 blocks per thread): the channel's
  * earlier chunk sums, the scan, d_l and the classes; its class counts go to column blockIdx.x of

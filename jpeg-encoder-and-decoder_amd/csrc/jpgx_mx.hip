@@ -41,8 +41,8 @@
  *           F = ((1/4 a(u)) a(v)) s, round(F / Q).
  *   Output  channel c's 8 blocks x 128 B leave as one 1-KiB nontemporal store.
  * The round-3 persistent kernels (k_mx, k_mx422, k_mx420) and the timing / diagnostic build knobs
- * (round-4b A/Bs and the round-5 fault probes) live in tools/probes/jpgx_mx_r5_knobs.patch:
- * `patch -p1 < tools/probes/jpgx_mx_r5_knobs.patch` at the repository root restores them.
+ * (round-4b A/Bs and the round-5 fault probes) live in tools/probes/jpgx_mx_r5_knobs.patch, removed from
+ * the tree in round 6: `git show 63924df:tools/probes/jpgx_mx_r5_knobs.patch | patch -p1` at that commit restores them.
  */
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -74,12 +74,11 @@ constexpr int kParts = JX_MX_PARTS;     /* f16 parts of B: hi (exact products) +
 constexpr unsigned kSlot = 1536;        /* one step's pixels: [y][8 blocks x 24 B]           */
 constexpr int kWPE = 4;                 /* waves per SIMD the register allocation targets    */
 
-/* LDS stage: 128 B per block in zig-zag order, 16 B of padding between blocks (kBS).  k_mxs's
- * block (c, jb) sits at slot mx_pos(c, jb): Y 0..7, Cr 0..3 at 8..11, Cb at 12..19, Cr 4..7 at
- * 20..23 -- so that a lane's three columns, (c = j / 8, gq), (c = j / 8, 4 + gq) and (Cr,
- * 4 (j / 8) + gq), lie at one lane address plus 0, 4 and 8 slots (one set of address registers
- * with immediate offsets). */
-constexpr unsigned kBS = 144;
+/* LDS stage: 128 B per block in zig-zag order (rounds 2-5 padded each block to 144 B; round 6
+ * XOR-swizzles the 16-byte pieces instead, mxs_coef / mx2_coef below).  k_mxs's block (c, jb) sits in
+ * slot mx_pos(c, jb): Y 0..7, Cr 0..3 at 8..11, Cb at 12..19, Cr 4..7 at 20..23 -- so that a lane's
+ * three columns, (c = j / 8, gq), (c = j / 8, 4 + gq) and (Cr, 4 (j / 8) + gq), lie at one lane
+ * address plus 4 and 8 slots (one set of address registers with immediate offsets). */
 __host__ __device__ constexpr unsigned mx_pos(unsigned c, unsigned jb)
 {
     return c == 0 ? jb : (c == 1 ? 12u + jb : (jb < 4 ? 8u + jb : 16u + jb));
@@ -109,6 +108,42 @@ __host__ __device__ constexpr unsigned mxs_coef(unsigned s, unsigned z)
 static_assert(mxs_h(0) == mxs_h(4) && mxs_h(0) == mxs_h(8) && mxs_h(1) == mxs_h(9) && mxs_h(12) == mxs_h(16) &&
                   mxs_h(12) == mxs_h(20) && mxs_h(13) == mxs_h(21),
               "a lane's three column blocks share a swizzle");
+/* The 4:2:x kernels' stage (round 6): 16 unpadded 128-B blocks, Y in slots 0..7 and chroma in 8..15
+ * (a lane's chroma column 8 slots after its Y column), pieces XOR-swizzled by mx2_h(s).  A column
+ * write's 32-lane half covers slots {s, s + 1, s + 4, s + 5} (swizzles {0, 5, 2, 7}, the minimum 2-way
+ * of the 4:4:4 stage above) and the 16-byte stage reads stay conflict-free. */
+constexpr unsigned kBS2 = 128;
+__host__ __device__ constexpr unsigned mx2_h(unsigned s)
+{
+    return ((s & 1u) ? 5u : 0u) ^ ((s & 4u) ? 2u : 0u);
+}
+__host__ __device__ constexpr unsigned mx2_piece(unsigned s, unsigned p)
+{
+    return kBS2 * s + 16u * (p ^ mx2_h(s));
+}
+__host__ __device__ constexpr unsigned mx2_coef(unsigned s, unsigned z)
+{
+    return mx2_piece(s, z >> 3) + 2u * (z & 7u);
+}
+static_assert(mx2_h(0) == mx2_h(8) && mx2_h(5) == mx2_h(13), "a lane's Y and chroma columns share a swizzle");
+/* the stage reads of the stores (lane l: piece l & 7 of block l >> 3) in closed form -- a few bit
+ * operations, so that the per-step re-derivation the register allocator chooses stays cheap:
+ * 16 mx?_h(s) for s = l >> 3 is (l & 8) * 10 (bits 0 and 2 of the piece) ^ (l & 32) (bit 1) */
+__host__ __device__ constexpr unsigned mx_ro(unsigned l) { return (l << 4) ^ ((l & 8u) * 10u); }
+__host__ __device__ constexpr unsigned mx2_ro(unsigned l) { return mx_ro(l) ^ (l & 32u); }
+__host__ __device__ constexpr bool mx_ro_ok()
+{
+    for (unsigned l = 0; l < 64; l++) {
+        const unsigned s = l >> 3, p = l & 7u;
+        if (mx_ro(l) != mxs_piece(s, p) || mx_ro(l) + 1536u - (mx_ro(l) & 32u) + (~mx_ro(l) & 32u) != mxs_piece(12u + s, p))
+            return false;
+        if ((mx_ro(l) ^ (l & 32u)) + 1024u + ((l & 32u) << 5) != mxs_piece(s + (s < 4 ? 8u : 16u), p))
+            return false;
+        if (mx2_ro(l) != mx2_piece(s, p) || mx2_ro(l) + 1024u != mx2_piece(8u + s, p)) return false;
+    }
+    return true;
+}
+static_assert(mx_ro_ok(), "closed forms of the stage read addresses");
 /* per-lane scales / band limits, shared by the workgroup: table t, half h (pairs 2h, 2h + 1 in
  * jx_pk_k order), profile j = lane & 15 -- a column's read of one (t, h) by the wave touches 16
  * consecutive 16-byte entries, every bank once.  4:4:4 (compacted to MxsTab below): t = Wy|b, Ly|b
@@ -927,9 +962,9 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
     const uint32_t s1 = q < 3 ? kSelHi : kSelZero;
     const uint32_t s2 = q < 3 ? kSelLo : kSelZero;
     const uint32_t so0 = lane * 16u, so1 = so0 + g.nb * 128u, so2 = so1 + g.nb * 128u;
-    const uint32_t ro = mxs_piece(lane >> 3, lane & 7u);
-    const uint32_t rr = mxs_piece((lane >> 3) + ((lane >> 3) < 4 ? 8u : 16u), lane & 7u);
-    const uint32_t rcb = mxs_piece(12u + (lane >> 3), lane & 7u);
+    const uint32_t ro = mx_ro(lane);                          /* mxs_piece(lane >> 3, lane & 7) */
+    const uint32_t rr = (ro ^ (lane & 32u)) + 1024u + ((lane & 32u) << 5);   /* Cr: slots 8..11, 20..23 */
+    const uint32_t rcb = (ro ^ 32u) + 1536u;                  /* Cb: slots 12..19 */
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
     const MxExLds xt{s_img.ex, s_img.scan_t};
 
@@ -1124,7 +1159,7 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
  *           cpuref_chroma_sample, dct_coef): X = (ls(2X) + ls(2X+1)) * 0.5, ls = the level-shifted
  *           chroma in preprocess.c's operation order.
  */
-constexpr unsigned kSt422C = 8 * kBS;         /* chroma (c, cb) at kSt422C + kBS (4 c + cb) */
+constexpr unsigned kSt422C = 8 * kBS2;        /* chroma (c, cb) in slot 8 + 4 c + cb (mx2_coef) */
 
 /* Y block of a lane's columns (lane (gq, j): set j / 8); also the chroma column's stage slot */
 __device__ __forceinline__ unsigned mx422_yblock(unsigned sl)
@@ -1159,7 +1194,7 @@ __device__ __forceinline__ void mx422_exact_inline(Lds &L, const uint8_t *sp, ui
             ok = mx_exact_one(MxSmp1{mx_lds((void *)sp) + 24u * slot, 192u}, 0u, u, v, xt, val);
         else
             ok = mx_exact_one(mx422_smp(L, sp, qmask, sl >> 4), 1u + (jj >> 3), u, v, xt, val);
-        return mx_put_one(L.stage, (k ? kSt422C : 0u) + kBS * slot + 2u * xt.scan(u, v), ok, val);
+        return mx_put_one(L.stage, mx2_coef(slot + (k ? 8u : 0u), xt.scan(u, v)), ok, val);
     });
     for (;;) {
         const uint64_t act = __ballot(bits != 0);
@@ -1184,8 +1219,8 @@ __device__ __forceinline__ void mx422_exact_inline(Lds &L, const uint8_t *sp, ui
         else
             val = mx_exact_coef<true>(mx422_smp(L, sp, qmask, sl >> 4), 1u + (jj >> 3), u, v, x, xt);
         if (live && x == 7)
-            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + (k ? kSt422C : 0u) + kBS * slot +
-                                                           2u * xt.scan(u, v)) = (int16_t)val;
+            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + mx2_coef(slot + (k ? 8u : 0u), xt.scan(u, v))) =
+                (int16_t)val;
         mx_wave_sync();
     }
 }
@@ -1230,7 +1265,7 @@ constexpr unsigned kMxs422C = 3;
 constexpr unsigned kMxs422WPG = 4;
 struct alignas(16) Mxs422Lds {
     uint8_t ring[kMxs422C][kSlot];
-    uint8_t stage[16 * kBS];
+    uint8_t stage[16 * kBS2];
     uint8_t qtrue[4][192];
     uint16_t task[8];
 };
@@ -1319,10 +1354,14 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
     }
     uint32_t za[8];
     {
-        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * ((j >> 3) * 4u + gq);
+        const unsigned s = (j >> 3) * 4u + gq;
+        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS2 * s, hs = mx2_h(s);
         const mx_u2 sc = *(const mx_u2 *)&s_img.scan_t[u][0];
 #pragma unroll
-        for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
+        for (int v = 0; v < 8; v++) {
+            const uint32_t zz = (v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu;
+            za[v] = base + 16u * ((zz >> 3) ^ hs) + 2u * (zz & 7u);
+        }
     }
     /* the B operands; reloaded after an exact pass, so that their registers are free during it */
     mx_u4 B[kParts][4];
@@ -1428,9 +1467,8 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
             /* the store's lane offsets, re-derived here (no VGPRs held across the step for them) */
             const unsigned l = mx_lane();
             const uint32_t soy = l * 16u, soc = (l & 31u) * 16u + (l >> 5) * (g.nb / 2u) * 128u;
-            const uint32_t ro = (l >> 3) * kBS + (l & 7u) * 16u;
-            const mx_u4 vy = *(const mx_u4 *)(L.stage + ro);
-            const mx_u4 vc = *(const mx_u4 *)(L.stage + kSt422C + ro);
+            const mx_u4 vy = *(const mx_u4 *)(L.stage + mx2_ro(l));
+            const mx_u4 vc = *(const mx_u4 *)(L.stage + mx2_ro(l) + kSt422C);
             __builtin_nontemporal_store(vy, (mx_u4 *)((const uint8_t *)S.dst + soy));
             __builtin_nontemporal_store(vc, (mx_u4 *)((const uint8_t *)S.cdst + soc));
         } else {
@@ -1439,9 +1477,8 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
             const unsigned yb = by < g.total ? by : g.total - 1u, cbk = bc < g.total ? bc : g.total - 1u;
             const unsigned fy = yb / g.nb, biy = yb - fy * g.nb;
             const unsigned fc = cbk / g.nb, bic = cbk - fc * g.nb;
-            const uint32_t rl = (l >> 3) * kBS + (l & 7u) * 16u;
-            const mx_u4 vy = *(const mx_u4 *)(L.stage + rl);
-            const mx_u4 vc = *(const mx_u4 *)(L.stage + kSt422C + rl);
+            const mx_u4 vy = *(const mx_u4 *)(L.stage + mx2_ro(l));
+            const mx_u4 vc = *(const mx_u4 *)(L.stage + mx2_ro(l) + kSt422C);
             if (by < g.total)
                 __builtin_nontemporal_store(
                     vy, (mx_u4 *)(g.out + (long long)fy * g.ofstride + (long long)biy * 64 + (l & 7u) * 8));
@@ -1491,7 +1528,7 @@ __global__ __launch_bounds__(64 * kMxs422WPG, kWPE) void k_mxs422(const jx_xform
  *   Exact   inline: Y tasks from the slot; chroma tasks read their MCU's pixels from global
  *           memory, in the oracle's order: ((ls(p00) + ls(p01)) + (ls(p10) + ls(p11))) * 0.25.
  */
-constexpr unsigned kSt420C = 8 * kBS;         /* chroma (c, lane group gq) at kSt420C + kBS (4 c + gq) */
+constexpr unsigned kSt420C = 8 * kBS2;        /* chroma (c, lane group gq) in slot 8 + 4 c + gq (mx2_coef) */
 
 /* MCU geometry of the launch */
 struct Mx420G {
@@ -1635,7 +1672,7 @@ __device__ __forceinline__ void mx420_exact_inline(Lds &L, const uint8_t *sp, ui
             ok = chroma(gq, [&](const auto &smp) __attribute__((always_inline)) {
                 return mx_exact_one(smp, 1u + (jj >> 3), u, v, xt, val);
             });
-        return mx_put_one(L.stage, (k ? kSt420C : 0u) + kBS * slot + 2u * xt.scan(u, v), ok, val);
+        return mx_put_one(L.stage, mx2_coef(slot + (k ? 8u : 0u), xt.scan(u, v)), ok, val);
     });
     for (;;) {
         const uint64_t act = __ballot(bits != 0);
@@ -1662,8 +1699,8 @@ __device__ __forceinline__ void mx420_exact_inline(Lds &L, const uint8_t *sp, ui
                 return mx_exact_coef<true>(smp, 1u + (jj >> 3), u, v, x, xt);
             });
         if (live && x == 7)
-            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + (k ? kSt420C : 0u) + kBS * slot +
-                                                           2u * xt.scan(u, v)) = (int16_t)val;
+            *(__attribute__((address_space(3))) int16_t *)(mx_lds(L.stage) + mx2_coef(slot + (k ? 8u : 0u), xt.scan(u, v))) =
+                (int16_t)val;
         mx_wave_sync();
     }
 }
@@ -1680,7 +1717,7 @@ __device__ __forceinline__ unsigned mx420_yblock(const MxG &g, const Mx420G &h, 
 struct alignas(16) Mxs420Lds {
     uint8_t ring[3][kSlot];             /* [y 0..15][4 blocks x 24 B]: steps 0, 1, 2; step 3 reuses slot 0 */
     union {
-        uint8_t stage[16 * kBS];
+        uint8_t stage[16 * kBS2];
         struct {                        /* general step: MCU's right column, true rows [16][24]; read
                                            for the A operands before the Y column writes here */
             uint8_t qtrue[2][384];
@@ -1692,7 +1729,7 @@ struct alignas(16) Mxs420Lds {
     };
     uint16_t task[8];
 };
-static_assert(2 * 384 <= kSt420C && 64 * 16 <= 16 * kBS - kSt420C, "qtrue in the Y stage, rA in the chroma stage");
+static_assert(2 * 384 <= kSt420C && 64 * 16 <= 16 * kBS2 - kSt420C, "qtrue in the Y stage, rA in the chroma stage");
 constexpr unsigned kMxs420WPG = 4;
 struct alignas(16) MxsImg420 {
     mx_u4 B[JX_MX_PARTS * 4][64];       /* [part * 4 + which]: the two Y sets merged (as k_mxs422), chroma K steps */
@@ -1792,8 +1829,8 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
     const uint32_t cof1 = cof0 + (q < 2 ? 32u : 80u);
     const uint32_t soy = (lane & 31u) * 16u + (lane >> 5) * g.bpr * 128u;
     const uint32_t soc = (lane & 31u) * 16u + (lane >> 5) * h.nmcu * 128u;
-    const uint32_t ro = (lane >> 3) * kBS + (lane & 7u) * 16u;
-    const uint32_t rc = kSt420C + kBS * (4u * (lane >> 5) + mx420_pm((lane >> 3) & 3u)) + (lane & 7u) * 16u;
+    const uint32_t ro = mx2_ro(lane);                         /* mx2_piece(lane >> 3, lane & 7) */
+    const uint32_t rc = mx2_piece(8u + 4u * (lane >> 5) + mx420_pm((lane >> 3) & 3u), lane & 7u);
     const unsigned gq = lane >> 4, j = lane & 15u, u = j & 7u;
 
     mx_wait_vm<6>();                                    /* the image (older than the pixel DMA) */
@@ -1805,10 +1842,14 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
     }
     uint32_t za[8];
     {
-        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS * (4u * (j >> 3) + gq);
+        const unsigned s = 4u * (j >> 3) + gq;
+        const uint32_t base = (uint32_t)(uintptr_t)mx_lds(L.stage) + kBS2 * s, hs = mx2_h(s);
         const mx_u2 sc = *(const mx_u2 *)&s_img.scan_t[u][0];
 #pragma unroll
-        for (int v = 0; v < 8; v++) za[v] = base + 2u * ((v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu);
+        for (int v = 0; v < 8; v++) {
+            const uint32_t zz = (v < 4 ? sc.x : sc.y) >> (8 * (v & 3)) & 0xffu;
+            za[v] = base + 16u * ((zz >> 3) ^ hs) + 2u * (zz & 7u);
+        }
     }
     /* the B operands; reloaded after an exact pass, so that their registers are free during it */
     mx_u4 B[kParts][5];
@@ -1965,7 +2006,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
                 const unsigned mc = mm < h.tm ? mm : h.tm - 1u;
                 const unsigned yb = mx420_yblock(g, h, mc - (jb >> 1), l >> 5, jb);
                 const unsigned f = yb / g.nb, bi = yb - f * g.nb;
-                const mx_u4 vy = *(const mx_u4 *)(L.stage + (l >> 3) * kBS + (l & 7u) * 16u);
+                const mx_u4 vy = *(const mx_u4 *)(L.stage + mx2_ro(l));
                 if (mm < h.tm)
                     __builtin_nontemporal_store(
                         vy, (mx_u4 *)(g.out + (long long)f * g.ofstride + (long long)bi * 64 + (l & 7u) * 8));
@@ -1975,8 +2016,7 @@ __global__ __launch_bounds__(64 * kMxs420WPG, kWPE) void k_mxs420(const jx_xform
                 const unsigned mc = mm < h.tm ? mm : h.tm - 1u;
                 unsigned f, mi, my, mx;
                 mx420_mcu(h, mc, f, mi, my, mx);
-                const mx_u4 vc = *(const mx_u4 *)(L.stage + kSt420C + kBS * (4u * (l >> 5) + mx420_pm(pm)) +
-                                                   (l & 7u) * 16u);
+                const mx_u4 vc = *(const mx_u4 *)(L.stage + mx2_piece(8u + 4u * (l >> 5) + mx420_pm(pm), l & 7u));
                 if (mm < h.tm)
                     __builtin_nontemporal_store(
                         vc, (mx_u4 *)(g.out + (long long)f * g.ofstride +

@@ -140,34 +140,29 @@ def test_gpu_stats_subsampled_layout(cuda, sr):
 
 
 def _gap_rule_hist(coef):
-    """k_ent_ac's rule restated (csrc/jpgx_entropy.hip): lane s of a block holds coefficients
-    8s..8s+7; p = the highest nonzero AC position of the lanes below (exclusive max-scan, 0 = the
-    DC position); a nonzero AC coefficient at i is symbol ((i - p - 1) & 15) | class (class = the
-    frexp exponent of the coefficient as a float); ZRLs come only from a lane's first nonzero,
-    (i - p - 1) >> 4 of them (gaps inside a lane are < 8); EOB iff coefficient 63 is zero.
+    """k_ent_ac's rule restated (csrc/jpgx_entropy.hip, round 6): a lane walks its block's 63 AC
+    coefficients with the previous nonzero position p (0 = the DC position); coefficient i has run
+    r = i - p - 1 and adds one count to bin ((r & 15) | class) when nonzero (class = the frexp
+    exponent of the coefficient as a float) or to bin 32 + (r & 15) when zero; a zero with r & 15 == 15
+    completes a group of 16 zeros, so ZRL = bin 47 minus the groups in the trailing zeros,
+    sum over blocks of (63 - L) >> 4 (L = the last nonzero position); EOB iff coefficient 63 is zero.
     Returns the AC histogram [257]."""
     z = np.asarray(coef, np.int64).reshape(-1, 64)
+    nb = z.shape[0]
+    bins = np.zeros(48, np.int64)
+    prev = np.zeros(nb, np.int64)
+    for i in range(1, 64):
+        v = z[:, i]
+        cls = np.frexp(v.astype(np.float32))[1].astype(np.int64)      # 0 for 0
+        r = i - 1 - prev
+        nz = cls != 0
+        b = np.where(nz, (r & 15) | cls, 32 | (r & 15))
+        np.add.at(bins, b, 1)
+        prev = np.where(nz, i, prev)
     h = np.zeros(257, np.int64)
-    pos = np.arange(64)
-    nz = (z != 0) & (pos > 0)
-    hi = np.where(nz, pos, 0).reshape(-1, 8, 8).max(axis=2)                  # per lane
-    excl = np.concatenate([np.zeros((z.shape[0], 1), np.int64),
-                           np.maximum.accumulate(hi, axis=1)[:, :-1]], axis=1)
-    for s in range(8):
-        prev = excl[:, s].copy()
-        lane = nz[:, 8 * s:8 * s + 8]
-        first = 8 * s + np.argmax(lane, axis=1)                      # the lane's first nonzero
-        anynz = lane.any(axis=1)
-        h[0xF0] += int(((first - prev - 1) >> 4)[anynz].sum())
-        for k in range(8):
-            i = 8 * s + k
-            m = nz[:, i]
-            gap = i - prev - 1
-            cls = np.frexp(z[:, i].astype(np.float32))[1].astype(np.int64)   # 0 for 0
-            sym = (gap & 15) | cls
-            np.add.at(h, sym[m], 1)
-            prev = np.where(m, i, prev)
-    h[0] += int((z[:, 63] == 0).sum())
+    h[1:32] = bins[1:32]
+    h[0xF0] = bins[47] - int(((63 - prev) >> 4).sum())
+    h[0] = int((z[:, 63] == 0).sum())
     return h
 
 

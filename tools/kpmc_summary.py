@@ -11,7 +11,7 @@ STEPS = 8 * 480 * 270 // 8
 
 
 def main(d, kernel="k_mxs"):
-    for f in sorted(glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True)):
+    for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
         tag = os.path.relpath(f, d).split(os.sep)[0]
         for k, v in sorted(counters(f, kernel).items()):
             print(f"{tag:50s} {k:28s} per launch {mean(v):14.1f}  per step {mean(v) / STEPS:9.2f}  n={len(v)}")
