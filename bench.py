@@ -304,6 +304,10 @@ def main():
                          "a rocprofv3 summary of the same command averages mostly steady-state "
                          "launches (with 200 ms the ramp's ~150 slow launches raised the mean by "
                          "~3 %%); 0 = off")
+    ap.add_argument("--kernel-timing", choices=["events", "span"], default="span",
+                    help="roofline.kernel_ms from the span of the K launches / K (queue gaps "
+                         "included; default) or from per-launch kernel begin/end events "
+                         "(jpgx_blocks_gpu_timed, the interval rocprofv3 reports; slows the loop)")
     ap.add_argument("--frames-per-gpu", type=int, default=8)
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
@@ -383,10 +387,19 @@ def main():
     torch.cuda.synchronize()
     nstep = [0]
 
-    def step(ev_mid=None):
+    def step(ev_mid=None, kev=None):
         jpgx.blocks_gpu(fr, params, rgb_ptrs[nstep[0] % len(rgb_ptrs)], d_out, d_ws,
-                        event_between=ev_mid)
+                        event_between=ev_mid, kernel_events=kev)
         nstep[0] += 1
+
+    # per-launch kernel events (jpgx_blocks_gpu_timed: hipExtLaunchKernel sets them to the kernel's
+    # own begin / end, the interval rocprofv3's kernel trace reports); recorded once so that their
+    # handles exist
+    kevs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for _ in range(args.steps if args.kernel_timing == "events" else 0)]
+    for a, b in kevs:
+        a.record()
+        b.record()
 
     # W warmup steps, each timed on its own (reported as the cold start), then untimed steps
     # until --settle-ms have passed: after idle the GPU's power management takes ~20 ms of load
@@ -407,11 +420,15 @@ def main():
         settle_steps += 10
         torch.cuda.synchronize()
     cold_ms = [a.elapsed_time(b) for a, b in cold]
-    # Kernel timing inside the timed region: HIP events on the launch stream around the whole
-    # loop of K back-to-back launches (the exact pass runs inside the kernel, so one launch per
-    # step); their span / K is the average launch duration, queue gaps included (the launches
-    # are asynchronous, so the queue never drains between them).  The wall clock around the
-    # same loop, bracketed by barrier + synchronize, gives the step time and `value`.
+    # Kernel timing inside the timed region (one launch per step: the exact pass runs inside the
+    # kernel).  --kernel-timing span (default): HIP events on the launch stream around the K
+    # back-to-back launches; span / K is `kernel_ms` (the queue gaps between launches included).
+    # --kernel-timing events: every launch goes through jpgx_blocks_gpu_timed, whose
+    # hipExtLaunchKernel sets a pair of HIP events to that kernel's own begin and end (the interval
+    # a rocprofv3 kernel trace reports) and `kernel_ms` is their mean -- but those launches cost the
+    # wall clock ~5 us each (round 6: 118.5 vs 112.3-113.8 us per step, kernel 110.2 vs span 110.6-
+    # 112.2 us), so it is not the default.  The wall clock around the loop, bracketed by barrier +
+    # synchronize, gives the step time and `value` either way.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
@@ -420,14 +437,16 @@ def main():
     t0 = time.perf_counter()
     ev0.record()
     for i in range(args.steps):
-        step()
+        step(kev=kevs[i] if args.kernel_timing == "events" else None)
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, world, cdev)
 
-    xform_ms = ev0.elapsed_time(ev1) / args.steps
+    span_ms = ev0.elapsed_time(ev1) / args.steps
+    launch_ms = [a.elapsed_time(b) for a, b in kevs] if args.kernel_timing == "events" else None
+    xform_ms = sum(launch_ms) / len(launch_ms) if launch_ms else span_ms
     px_rank_step = B * (r1 - r0) * 8 * W
     px_total = B * W * H * args.steps                 # all ranks
     value = px_total / elapsed / 1e6
@@ -465,7 +484,8 @@ def main():
                        "sample_ratio": args.sample_ratio, "parallelism": f"stripes{N}",
                        "collectives": ("none" if N == 1 else
                                        f"{backend}: barrier, max-time, output check"),
-                       "kernel_timing": "HIP events around the K launches on their stream",
+                       "kernel_timing": ("per-launch kernel begin/end HIP events (hipExtLaunchKernel)"
+                                         if launch_ms else "HIP events around the K launches on their stream"),
                        "input_sets": args.input_sets},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -474,6 +494,9 @@ def main():
                          "traffic_source": t_src,
                          "kernel": kname if not args.subsample else sub_kernel_name(args.sample_ratio),
                          "kernel_ms": round(xform_ms, 4),
+                         "kernel_ms_min_max": ([round(min(launch_ms), 4), round(max(launch_ms), 4)]
+                                               if launch_ms else None),
+                         "span_ms_per_launch": round(span_ms, 4),
                          "bytes_per_launch": bytes_per_px * px_rank_step},
             "cpu_baseline": cpu,
             "output_check": check,

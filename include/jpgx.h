@@ -140,6 +140,16 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
                        int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream,
                        void *event_between);
 
+/* Same as jpgx_blocks_gpu, and times the transform kernel itself: the 4:4:4 / true-4:2:x kernels
+ * are launched through hipExtLaunchKernel with hipEvent_t ev_start / ev_stop (both required,
+ * created by the caller), so hipEventElapsedTime(ev_start, ev_stop) is the kernel's execution
+ * interval -- the one a rocprofv3 kernel trace reports, without the queue gap before the dispatch
+ * that events recorded around the call include (bench.py's roofline).  The test-only library
+ * records them around its kernels instead. */
+int jpgx_blocks_gpu_timed(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
+                          int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream,
+                          void *ev_start, void *ev_stop);
+
 /* Entropy-stage statistics on the device: over one image's coefficients
  * d_coef = Y [nb_y][64] | Cb [nb_c][64] | Cr [nb_c][64] (what jpgx_blocks_gpu writes; nb_c =
  * nb_y unless JPGX_FLAG_SUBSAMPLE), the reference's in-place DC recurrence (src/dpcm.c:6-21)

@@ -11,20 +11,16 @@
  *
  * The recurrence is sequential; it is an alternating prefix sum:
  *     d_l = (-1)^l (P_l - c),  P_l = sum_{k<=l} (-1)^k v_k,  c = the DC carried in
- * so three launches per image, (A) over chunks of 512 blocks of one channel (4 waves,
- * one workgroup):
- *   (A) k_ent_ac: every block's AC symbols into the histogram, the chunk's sum of (-1)^k v_k,
- *       and the DC words compacted (2 bytes per block) into the workspace.  A wave takes 8
- *       blocks per load (lane l: 16 bytes = coefficients 8 (l & 7) .. + 7 of block l >> 3, so
- *       one load instruction reads 1 KiB contiguous), all 16 loads of its 128 blocks issued first.
- *       A nonzero AC coefficient at zig-zag position i whose previous nonzero is at p (the DC
- *       position 0 if none) is the reference's symbol ((i - p - 1) & 15) | class after
- *       (i - p - 1) >> 4 ZRLs; a block ends in EOB iff its coefficient 63 is zero (huffman.c:
- *       193-221).  p comes from an exclusive max-scan of the lanes' highest nonzero positions
- *       over the block's 8 lanes.  The reference's `run | size` keeps every symbol in 1..31,
- *       so each thread counts into its own LDS column of 32 words (no two lanes of a wave share a
- *       bank; 16-bit counters packed two per word measured 4 % slower, profiles/r05_entropy.txt)
- *       and the workgroup sums the columns once at its end into per-chunk counts (plain stores).
+ * so three launches per image, (A) over chunks of 512 blocks of one channel (4 waves, one
+ * workgroup):
+ *   (A) k_ent_ac: every block's AC symbols into count bins, the chunk's sum of (-1)^k v_k, and the
+ *       DC words compacted (2 bytes per block) into the workspace.  A wave's 16 coalesced 1-KiB
+ *       loads (128 blocks) pass through an LDS tile so that each lane walks two whole blocks in
+ *       zig-zag order (round 6, below): a nonzero AC coefficient at position i after the previous
+ *       nonzero p (the DC position 0 if none) is the reference's symbol ((i - p - 1) & 15) | class
+ *       after (i - p - 1) >> 4 ZRLs; a block ends in EOB iff its coefficient 63 is zero
+ *       (huffman.c:193-221).  The workgroup sums its count columns at its end into per-chunk
+ *       counts (plain stores).
  *   (B) k_ent_dc: the sum of the channel's earlier chunk sums (at most a few hundred, read from
  *       L2), the in-chunk scan over the compacted DC words, d_l, and the DC classes per chunk.
  *   (C) k_ent_hist: one workgroup per count row sums it over the luma / chroma chunks and writes
@@ -38,18 +34,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <type_traits>
 
 #include "jpgx_internal.h"
 
 namespace {
 
-#ifndef JX_ENT_LOADS
-#define JX_ENT_LOADS 16
-#endif
-constexpr int kChunk = 256;     /* threads per workgroup (4 waves)                     */
-constexpr int kLoads = JX_ENT_LOADS;   /* k_ent_ac: 8-block loads per wave, all issued first (16 vs 8: 4 % faster, profiles/r05_entropy.txt) */
-constexpr int kCB = 32 * kLoads;       /* blocks per chunk: 4 waves x kLoads x 8 blocks       */
+constexpr int kChunk = 256;            /* threads per workgroup (4 waves)                           */
+constexpr int kLoads = 16;             /* k_ent_ac: 8-block loads per wave, all issued first        */
+constexpr int kAcW = 4;                /* k_ent_ac: waves per workgroup (8: slower, r06_entropy)  */
+constexpr int kAcT = 64 * kAcW;
+constexpr int kCB = 8 * kAcW * kLoads; /* blocks per chunk: kAcW waves x kLoads x 8 blocks     */
 constexpr int kSyms = 32;       /* AC symbols (zeros | class) 1..31; 0 = no symbol    */
 constexpr int kRows = 66;       /* per-chunk count rows: AC 0..31 (row 0: EOB), ZRL 32, DC class 33..65 */
 
@@ -86,10 +80,6 @@ __device__ __forceinline__ void chunk_of(const Chunks &c, unsigned chunk, unsign
     k0 = (l - c.first[ch]) * kCB;
 }
 
-#ifndef JX_ENT_LANEBLK
-#define JX_ENT_LANEBLK 1
-#endif
-#if JX_ENT_LANEBLK
 /*
  * Round 6: one lane per block.  The wave's 16 loads stay the coalesced 1-KiB loads (lane l: 16 bytes
  * of block l >> 3); each half of them (64 blocks) goes through a per-wave LDS tile so that lane b
@@ -106,7 +96,8 @@ __device__ __forceinline__ void chunk_of(const Chunks &c, unsigned chunk, unsign
  * waves, and lanes l, l + 32 are serviced in different LDS cycles), so the counters take 6 KiB and
  * four workgroups fit a CU.  The round-5 form (8 lanes per block, an 8-lane max-scan through
  * ds_bpermute, 8 SGPR masks per load that the compiler spilled into VGPR lanes, per-thread columns
- * of 32 KiB) issued ~1.6x the VALU per coefficient: JX_ENT_LANEBLK=0.
+ * of 32 KiB; in the git history at 63924df) issued ~1.8x the VALU per coefficient and ran 111 us
+ * per 8 x 4K batch against 78.5 (profiles/r06_entropy.txt).
  */
 constexpr int kBins = 48;                        /* AC symbols 0..31, zero coefficients 32 + (run & 15) */
 typedef uint32_t ent_u4 __attribute__((ext_vector_type(4)));
@@ -168,17 +159,17 @@ __device__ __forceinline__ void ent_block_end(const uint32_t (&u)[32], uint32_t 
     }
 }
 
-__global__ __launch_bounds__(kChunk, 4) void k_ent_ac(const Chunks c)
+__global__ __launch_bounds__(kAcT, 16 / kAcW) void k_ent_ac(const Chunks c)
 {
     __shared__ uint32_t cnt[kBins][32];              /* [bin][lane & 31], shared by the 4 waves */
-    __shared__ __attribute__((aligned(16))) uint8_t tile[kChunk / 64][64 * 128];
-    __shared__ long long wsum[kChunk / 64];
-    __shared__ uint32_t wez[kChunk / 64][2];
+    __shared__ __attribute__((aligned(16))) uint8_t tile[kAcW][64 * 128];
+    __shared__ long long wsum[kAcW];
+    __shared__ uint32_t wez[kAcW][2];
     unsigned f, k0;
     int ch;
     chunk_of(c, blockIdx.x, f, ch, k0);
     const unsigned t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    for (unsigned i = t; i < (unsigned)kBins * 32u; i += kChunk) (&cnt[0][0])[i] = 0;
+    for (unsigned i = t; i < (unsigned)kBins * 32u; i += kAcT) (&cnt[0][0])[i] = 0;
     const unsigned n = min(c.nb[ch] - k0, (unsigned)kCB);
     const int16_t *z = c.coef + (f * c.fstride + c.off[ch] + k0) * 64;
     static_assert(kLoads == 16, "two halves of 64 blocks per wave");
@@ -194,6 +185,9 @@ __global__ __launch_bounds__(kChunk, 4) void k_ent_ac(const Chunks c)
         qb[it] = *(const uint4 *)(z + (size_t)(blk < n ? blk : 0u) * 64 + 8u * (lane & 7u));
     }
     const unsigned ba = 8u * kLoads * wave + lane, bb = ba + 64u;      /* this lane's two blocks */
+    uint32_t eob = 0, zcor = 0;
+    long long w = 0;
+    const uint32_t colb = (uint32_t)(uintptr_t)(ent_l32 *)&cnt[0][lane & 31u];
     uint32_t ua[32], ub[32];
     ent_transpose(qa, tile[wave], lane, ua);
     ent_transpose(qb, tile[wave], lane, ub);
@@ -203,15 +197,12 @@ __global__ __launch_bounds__(kChunk, 4) void k_ent_ac(const Chunks c)
         for (int i = 0; i < 32; i++) ua[i] &= la, ub[i] &= lb;
     }
     __syncthreads();                                  /* the counters are zeroed */
-    const uint32_t colb = (uint32_t)(uintptr_t)(ent_l32 *)&cnt[0][lane & 31u];
     uint32_t pa = 0, pb = 0;                          /* previous nonzero: the DC position */
 #pragma unroll
     for (int k = 1; k < 64; k++) {
         ent_coef(ua, k, pa, colb);
         ent_coef(ub, k, pb, colb);
     }
-    uint32_t eob = 0, zcor = 0;
-    long long w = 0;
     ent_block_end(ua, pa, ba, n, eob, zcor, w, c, f, ch, k0);
     ent_block_end(ub, pb, bb, n, eob, zcor, w, c, f, ch, k0);
 #pragma unroll
@@ -230,143 +221,30 @@ __global__ __launch_bounds__(kChunk, 4) void k_ent_ac(const Chunks c)
         uint32_t tot = 0;
         if (t == 0) {
 #pragma unroll
-            for (int i = 0; i < kChunk / 64; i++) tot += wez[i][0];
+            for (int i = 0; i < kAcW; i++) tot += wez[i][0];
         } else {
             const unsigned bin = t < (unsigned)kSyms ? t : 47u;
 #pragma unroll
             for (unsigned j = 0; j < 32; j++) tot += cnt[bin][(j + t) & 31u];     /* rotated: distinct banks */
             if (t == (unsigned)kSyms) {
 #pragma unroll
-                for (int i = 0; i < kChunk / 64; i++) tot -= wez[i][1];
+                for (int i = 0; i < kAcW; i++) tot -= wez[i][1];
             }
         }
         c.cnt[(size_t)t * c.nchunks + blockIdx.x] = tot;
     } else if (t == (unsigned)kSyms + 1) {
         long long ws = 0;
 #pragma unroll
-        for (int i = 0; i < kChunk / 64; i++) ws += wsum[i];
+        for (int i = 0; i < kAcW; i++) ws += wsum[i];
         c.part[blockIdx.x] = ws;
     }
 }
-#else
-__global__ __launch_bounds__(kChunk) void k_ent_ac(const Chunks c)
-{
-    __shared__ uint32_t cnt[kSyms][kChunk];          /* [symbol][thread] */
-    __shared__ uint32_t red[kChunk / 32][kSyms];
-    __shared__ long long wsum[kChunk / 64];
-    __shared__ uint32_t wez[kChunk / 64][2];
-    unsigned f, k0;
-    int ch;
-    chunk_of(c, blockIdx.x, f, ch, k0);
-    const unsigned t = threadIdx.x, lane = t & 63u, wave = t >> 6, s = lane & 7u;
-#pragma unroll
-    for (int b = 0; b < kSyms; b++) cnt[b][t] = 0;   /* own column: no barrier before use */
-    const unsigned n = min(c.nb[ch] - k0, (unsigned)kCB);
-    const int16_t *z = c.coef + (f * c.fstride + c.off[ch] + k0) * 64;
-    uint4 q[kLoads];
-#pragma unroll
-    for (int it = 0; it < kLoads; it++) {             /* unconditional: all in flight at once */
-        const unsigned blk = 8u * kLoads * wave + 8u * (unsigned)it + (lane >> 3);
-        q[it] = *(const uint4 *)(z + (size_t)(blk < n ? blk : 0u) * 64 + 8u * s);
-    }
-    uint32_t eob = 0, zrl = 0;
-    long long w = 0;
-#pragma unroll
-    for (int it = 0; it < kLoads; it++) {
-        const unsigned blk = 8u * kLoads * wave + 8u * (unsigned)it + (lane >> 3);
-        const uint32_t live = blk < n ? ~0u : 0u;       /* a dead block reads as zeros */
-        const uint32_t u[4] = {q[it].x & live, q[it].y & live, q[it].z & live, q[it].w & live};
-        int v[8];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            v[2 * j] = (int)(int16_t)(u[j] & 0xffffu);
-            v[2 * j + 1] = (int)u[j] >> 16;
-        }
-        const int i0 = 8 * (int)s;
-        bool nz[8];                                   /* a nonzero AC coefficient */
-#pragma unroll
-        for (int k = 0; k < 8; k++) nz[k] = v[k] != 0;
-        nz[0] = nz[0] && s > 0;                       /* the DC coefficient is no AC symbol */
-        int hi = -1, lo = 64;                         /* highest / lowest nonzero AC position */
-#pragma unroll
-        for (int k = 0; k < 8; k++) hi = nz[k] ? i0 + k : hi;
-#pragma unroll
-        for (int k = 7; k >= 0; k--) lo = nz[k] ? i0 + k : lo;
-        int x = max(hi, 0);                           /* max-scan over the block's 8 lanes */
-#pragma unroll
-        for (int d = 1; d < 8; d <<= 1) {
-            const int y = __shfl_up(x, d, 8);
-            if (s >= (unsigned)d) x = max(x, y);
-        }
-        int prev = __shfl_up(x, 1, 8);
-        if (s == 0) prev = 0;                         /* the DC position */
-        /* ZRLs: only the lane's first nonzero can follow 16 or more zeros (gaps inside a lane
-         * are < 8) */
-        if (hi >= 0) zrl += (uint32_t)((lo - prev - 1) >> 4);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int i = i0 + k;
-            /* class = frexp exponent of the exact float (0 for 0), huffman.c:226-235 */
-            const int cls = __builtin_amdgcn_frexp_expf((float)v[k]);
-            const int sym = ((i - prev - 1) & 15) | cls;
-            atomicAdd(&cnt[nz[k] ? sym : 0][t], 1u);
-            prev = nz[k] ? i : prev;
-        }
-        if (blk < n) {
-            eob += (s == 7 && v[7] == 0) ? 1u : 0u;
-            if (s == 0) {
-                c.dcv[f * c.nbf + c.off[ch] + k0 + blk] = (int16_t)v[0];
-                w += ((k0 + blk) & 1u) ? -(long long)v[0] : (long long)v[0];
-            }
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        w += __shfl_xor(w, o, 64);
-        eob += __shfl_xor(eob, o, 64);
-        zrl += __shfl_xor(zrl, o, 64);
-    }
-    if (lane == 0) {
-        wsum[wave] = w;
-        wez[wave][0] = eob;
-        wez[wave][1] = zrl;
-    }
-    __syncthreads();
-    {   /* column sums: lanes of a wave read 64 distinct banks (row r, rotated by the symbol) */
-        const unsigned b = t & 31u, r = t >> 5;
-        uint32_t sum = 0;
-#pragma unroll
-        for (unsigned j = 0; j < 32; j++) sum += cnt[b][32u * r + ((j + b) & 31u)];
-        red[r][b] = sum;
-    }
-    __syncthreads();
-    if (t < (unsigned)kSyms) {
-        uint32_t tot = 0;                             /* symbol t; row 0 counts EOB */
-        if (t == 0) {
-#pragma unroll
-            for (int i = 0; i < kChunk / 64; i++) tot += wez[i][0];
-        } else {
-#pragma unroll
-            for (int r = 0; r < kChunk / 32; r++) tot += red[r][t];
-        }
-        c.cnt[(size_t)t * c.nchunks + blockIdx.x] = tot;
-    } else if (t == (unsigned)kSyms) {
-        uint32_t zr = 0;
-        long long ws = 0;
-#pragma unroll
-        for (int i = 0; i < kChunk / 64; i++) zr += wez[i][1], ws += wsum[i];
-        c.cnt[(size_t)kSyms * c.nchunks + blockIdx.x] = zr;     /* ZRL */
-        c.part[blockIdx.x] = ws;
-    }
-}
-
-#endif
 
 /* DC pass over kDcChunks consecutive chunks of one channel (8 blocks per thread): the channel's
  * earlier chunk sums, the scan, d_l and the classes; its class counts go to column blockIdx.x of
  * the DC count rows (frame f's DC workgroups are f dc_groups() .. + dc_groups() - 1, luma first). */
 constexpr int kDcChunks = 2048 / kCB;   /* 2,048 blocks per DC workgroup */
-static_assert(kCB <= 2048 && 2048 % kCB == 0, "JX_ENT_LOADS: a power of two up to 64 (DC workgroups tile whole chunks)");
+static_assert(kCB <= 2048 && 2048 % kCB == 0, "DC workgroups tile whole chunks");
 __global__ __launch_bounds__(kChunk) void k_ent_dc(const Chunks c)
 {
     __shared__ uint32_t cnt[16][kChunk];              /* [class / 2][thread], 16-bit halves: classes 0..31 */
@@ -598,7 +476,7 @@ int jpgx_entropy_stats_gpu_batch(const int16_t *d_coef, size_t coef_frame_stride
     c.off[2] = (unsigned)(nb_y + nb_c);
     for (int k = 0; k < 3; k++) c.carry[k] = carry ? carry[k] : 0;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_ent_ac, dim3((unsigned)nch), dim3(kChunk), 0, s, c);
+    hipLaunchKernelGGL(k_ent_ac, dim3((unsigned)nch), dim3(kAcT), 0, s, c);
     c.ndcg = dc_groups(c);
     c.vec = nbf % 8 == 0 && nb_y % 8 == 0 && nb_c % 8 == 0 && ((uintptr_t)c.dcv & 15) == 0 &&
             ((uintptr_t)d_dc & 15) == 0;

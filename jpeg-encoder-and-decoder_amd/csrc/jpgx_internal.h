@@ -111,19 +111,19 @@ int jx_plan_tables_mx(int quality, float w[24][8], float lim[24][8], int16_t q[2
 int jx_mx_operands(uint16_t ops[3 * JX_MX_PARTS][64][8]);
 long long jx_selftest_mx(long long nblocks, unsigned long long seed, int quality,
                          long long *flagged, double *ratio);
-int jx_launch_mx(const struct jx_xform_args *xa, void *stream);
+int jx_launch_mx(const struct jx_xform_args *xa, void *stream, void *ev_start, void *ev_stop);
 /* k_mx422 (true 4:2:2 on the matrix cores): operands [part][which][lane], tables, launch */
 int jx_mx422_operands(uint16_t ops[JX_MX_PARTS][4][64][8]);
 int jx_plan_tables_mx422(int quality, float w[24][8], float lim[24][8], int16_t q[2][64]);
 long long jx_selftest_mx422(long long nblocks, unsigned long long seed, int quality,
                             long long *flagged, double *ratio);
-int jx_launch_mx422(const struct jx_xform_args *xa, void *stream);
+int jx_launch_mx422(const struct jx_xform_args *xa, void *stream, void *ev_start, void *ev_stop);
 /* k_mx420 (true 4:2:0 on the matrix cores): operands [part][which][lane], tables, launch */
 int jx_mx420_operands(uint16_t ops[JX_MX_PARTS][5][64][8]);
 int jx_plan_tables_mx420(int quality, float w[24][8], float lim[24][8], int16_t q[2][64]);
 long long jx_selftest_mx420(long long nblocks, unsigned long long seed, int quality,
                             long long *flagged, double *ratio);
-int jx_launch_mx420(const struct jx_xform_args *xa, void *stream);
+int jx_launch_mx420(const struct jx_xform_args *xa, void *stream, void *ev_start, void *ev_stop);
 #ifdef __cplusplus
 }
 #endif

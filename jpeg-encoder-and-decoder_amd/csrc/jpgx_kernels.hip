@@ -824,6 +824,10 @@ constexpr size_t kMaxPitch = (size_t)1 << 27;     /* 16 rows x pitch + 256 < 2^3
 
 }  // namespace
 
+static int blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb, int16_t *d_out,
+                      void *d_workspace, size_t workspace_bytes, void *stream, void *event_after, void *ev_start,
+                      void *ev_stop);
+
 extern "C" {
 
 int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
@@ -835,6 +839,23 @@ int jpgx_blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *
 int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
                        int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream,
                        void *event_after)
+{
+    return blocks_gpu(fr, p, d_rgb, d_out, d_workspace, workspace_bytes, stream, event_after, nullptr, nullptr);
+}
+
+int jpgx_blocks_gpu_timed(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb,
+                          int16_t *d_out, void *d_workspace, size_t workspace_bytes, void *stream,
+                          void *ev_start, void *ev_stop)
+{
+    if (!ev_start || !ev_stop) return JPGX_EARG;
+    return blocks_gpu(fr, p, d_rgb, d_out, d_workspace, workspace_bytes, stream, nullptr, ev_start, ev_stop);
+}
+
+}  /* extern "C" */
+
+static int blocks_gpu(const jpgx_frames *fr, const jpgx_params *p, const uint8_t *d_rgb, int16_t *d_out,
+                      void *d_workspace, size_t workspace_bytes, void *stream, void *event_after, void *ev_start,
+                      void *ev_stop)
 {
     if (!fr || !p) return JPGX_EARG;
     int rc = jpgx_validate(fr->width, fr->height, p);
@@ -892,7 +913,7 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     xa.luma_only = sub ? 1 : 0;
     if (!sub && !kAltDispatch) {
         /* k_mx: colour + row DCT on the matrix cores, exact pass inside (csrc/jpgx_mx.hip) */
-        rc = jx_launch_mx(&xa, stream);
+        rc = jx_launch_mx(&xa, stream, ev_start, ev_stop);
         if (rc) return rc;
         if (event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
         return rc;
@@ -903,15 +924,19 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
     const unsigned grid = (unsigned)((waves + JX_WG / 64 - 1) / (JX_WG / 64));
     if (sub && p->sample_ratio == 2 && !kAltDispatch) {
         /* true 4:2:0 in one pass on the matrix cores (k_mx420, csrc/jpgx_mx.hip) */
-        rc = jx_launch_mx420(&xa, stream);
+        rc = jx_launch_mx420(&xa, stream, ev_start, ev_stop);
         if (!rc && event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
         return rc;
     }
     if (sub && p->sample_ratio == 1 && !kAltDispatch) {
         /* true 4:2:2 in one pass on the matrix cores (k_mx422, csrc/jpgx_mx.hip) */
-        rc = jx_launch_mx422(&xa, stream);
+        rc = jx_launch_mx422(&xa, stream, ev_start, ev_stop);
         if (!rc && event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
         return rc;
+    }
+    if (ev_start) {                                   /* the test library: events around its kernels */
+        rc = hip_rc(hipEventRecord((hipEvent_t)ev_start, s));
+        if (rc) return rc;
     }
     hipLaunchKernelGGL(k_xform, dim3(grid), dim3(JX_WG), 0, s, xa);
     rc = hip_rc(hipGetLastError());
@@ -934,9 +959,12 @@ int jpgx_blocks_gpu_ev(const jpgx_frames *fr, const jpgx_params *p, const uint8_
         rc = hip_rc(hipGetLastError());
         if (rc) return rc;
     }
-    if (event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
+    if (ev_stop) rc = hip_rc(hipEventRecord((hipEvent_t)ev_stop, s));
+    if (!rc && event_after) rc = hip_rc(hipEventRecord((hipEvent_t)event_after, s));
     return rc;
 }
+
+extern "C" {
 
 int jpgx_gen_splitmix_gpu(uint8_t *d_dst, size_t nbytes, uint64_t seed, void *stream)
 {

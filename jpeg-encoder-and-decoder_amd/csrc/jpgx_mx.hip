@@ -44,6 +44,7 @@
  * (round-4b A/Bs and the round-5 fault probes) live in tools/probes/jpgx_mx_r5_knobs.patch, removed from
  * the tree in round 6: `git show 63924df:tools/probes/jpgx_mx_r5_knobs.patch | patch -p1` at that commit restores them.
  */
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -2290,41 +2291,53 @@ int mx420_tables_for_current_device()
 
 }  // namespace
 
+/* a launch on `stream`; with ev_start / ev_stop (hipEvent_t, both or neither) through
+ * hipExtLaunchKernel, whose events carry the kernel's own begin / end timestamps -- the interval a
+ * rocprofv3 kernel trace reports, without the queue gap before the dispatch (bench.py) */
+template <class K>
+void mx_launch_k(K kernel, dim3 grid, dim3 block, hipStream_t s, void *ev_start, void *ev_stop, const jx_xform_args &a)
+{
+    if (ev_start && ev_stop)
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, s, (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0, a);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, s, a);
+}
+
 /* k_mxs420 over every frame of the stripe (true 4:2:0: Y [nb][64], Cb and Cr [nb / 4][64] per
  * frame, the stripe an even number of block rows); no workspace. */
-extern "C" int jx_launch_mx420(const jx_xform_args *xa, void *stream)
+extern "C" int jx_launch_mx420(const jx_xform_args *xa, void *stream, void *ev_start, void *ev_stop)
 {
     const int rc = mx420_tables_for_current_device();
     if (rc) return rc;
     const size_t mcus = (size_t)xa->g.nb / 4 * (size_t)xa->g.nframes;
     const size_t waves = (mcus + 7) / 8;
-    hipLaunchKernelGGL(k_mxs420, dim3((unsigned)((waves + kMxs420WPG - 1) / kMxs420WPG)), dim3(64 * kMxs420WPG), 0,
-                       (hipStream_t)stream, *xa);
+    mx_launch_k(k_mxs420, dim3((unsigned)((waves + kMxs420WPG - 1) / kMxs420WPG)), dim3(64 * kMxs420WPG), (hipStream_t)stream,
+                ev_start, ev_stop, *xa);
     return mx_rc(hipGetLastError());
 }
 
 /* k_mxs422 over every frame of the stripe (true 4:2:2: Y [nb][64], Cb and Cr [nb / 2][64] per
  * frame); no workspace. */
-extern "C" int jx_launch_mx422(const jx_xform_args *xa, void *stream)
+extern "C" int jx_launch_mx422(const jx_xform_args *xa, void *stream, void *ev_start, void *ev_stop)
 {
     const int rc = mx422_tables_for_current_device();
     if (rc) return rc;
     const size_t nsteps = ((size_t)xa->g.nb * (size_t)xa->g.nframes + 7) / 8;
     const size_t waves = (nsteps + kMxs422C - 1) / kMxs422C;
-    hipLaunchKernelGGL(k_mxs422, dim3((unsigned)((waves + kMxs422WPG - 1) / kMxs422WPG)), dim3(64 * kMxs422WPG), 0,
-                       (hipStream_t)stream, *xa);
+    mx_launch_k(k_mxs422, dim3((unsigned)((waves + kMxs422WPG - 1) / kMxs422WPG)), dim3(64 * kMxs422WPG), (hipStream_t)stream,
+                ev_start, ev_stop, *xa);
     return mx_rc(hipGetLastError());
 }
 
 /* k_mxs over every frame of the stripe (4:4:4 / reference-parity output); no workspace. */
-extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream)
+extern "C" int jx_launch_mx(const jx_xform_args *xa, void *stream, void *ev_start, void *ev_stop)
 {
     const int rc = mx_tables_for_current_device();
     if (rc) return rc;
     const size_t nsteps = ((size_t)xa->g.nb * (size_t)xa->g.nframes + 7) / 8;
     const size_t waves = (nsteps + kMxsC - 1) / kMxsC;
-    hipLaunchKernelGGL(k_mxs, dim3((unsigned)((waves + kMxsWPG - 1) / kMxsWPG)), dim3(64 * kMxsWPG), 0,
-                       (hipStream_t)stream, *xa);
+    mx_launch_k(k_mxs, dim3((unsigned)((waves + kMxsWPG - 1) / kMxsWPG)), dim3(64 * kMxsWPG), (hipStream_t)stream,
+                ev_start, ev_stop, *xa);
     return mx_rc(hipGetLastError());
 }
 

@@ -36,6 +36,7 @@ _ERRNAMES = {-1: "EGEOMETRY", -2: "EQUALITY", -3: "ESAMPLE", -4: "EARG", -5: "EH
 EXPORTS = [
     "jpgx_validate", "jpgx_default_params", "jpgx_glibc_underflow", "jpgx_scale_table",
     "jpgx_guard_band", "jpgx_workspace_size", "jpgx_blocks_gpu", "jpgx_blocks_gpu_ev",
+    "jpgx_blocks_gpu_timed",
     "jpgx_gen_splitmix_gpu",
     "jpgx_gen_tie_gpu", "jpgx_blocks", "jpgx_blocks_multi", "jpgx_stripe",
     "jpgx_device_count", "jpgx_version", "jpgx_chroma_blocks", "jpgx_entropy_workspace_size",
@@ -98,6 +99,7 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.jpgx_workspace_size.restype = sz
     L.jpgx_blocks_gpu.argtypes = [Fp, P, vp, vp, vp, sz, vp]
     L.jpgx_blocks_gpu_ev.argtypes = [Fp, P, vp, vp, vp, sz, vp, vp]
+    L.jpgx_blocks_gpu_timed.argtypes = [Fp, P, vp, vp, vp, sz, vp, vp, vp]
     L.jpgx_gen_splitmix_gpu.argtypes = [vp, sz, ctypes.c_uint64, vp]
     L.jpgx_gen_tie_gpu.argtypes = [vp, i, i, vp]
     L.jpgx_blocks.argtypes = [vp, i, i, sz, P, vp, i]
@@ -225,14 +227,22 @@ def _stream_ptr(stream) -> int:
 
 
 def blocks_gpu(fr: Frames, params: Params, d_rgb, d_out, d_ws, stream=None,
-               event_between=None) -> None:
+               event_between=None, kernel_events=None) -> None:
     """Launch the hot path on device tensors (uint8 input, int16 output, uint8 workspace).
     d_rgb must point at pixel (0, 8*row_begin) of frame 0 (pass a tensor view or an int).
     event_between: a torch.cuda.Event recorded right after the transform kernel (it must have
-    been recorded once already so that its handle exists)."""
+    been recorded once already so that its handle exists).
+    kernel_events: (start, stop) torch.cuda.Events (timing-enabled, recorded once already) that
+    jpgx_blocks_gpu_timed sets to the transform kernel's own begin / end."""
     def ptr(t):
         return t if isinstance(t, int) else t.data_ptr()
     ws_bytes = d_ws.numel() if hasattr(d_ws, "numel") else workspace_size(fr)
+    if kernel_events is not None:                 # (start, stop): the kernel's own interval
+        e0, e1 = (e.cuda_event for e in kernel_events)
+        _check(lib.jpgx_blocks_gpu_timed(ctypes.byref(fr), ctypes.byref(params), ptr(d_rgb), ptr(d_out),
+                                         ptr(d_ws), ws_bytes, _stream_ptr(stream), e0, e1),
+               "jpgx_blocks_gpu_timed")
+        return
     ev = event_between.cuda_event if event_between is not None else None
     _check(lib.jpgx_blocks_gpu_ev(ctypes.byref(fr), ctypes.byref(params), ptr(d_rgb),
                                   ptr(d_out), ptr(d_ws), ws_bytes, _stream_ptr(stream), ev),

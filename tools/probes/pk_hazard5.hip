@@ -15,7 +15,13 @@
  *   an iteration earlier; 1 again
  *  (set 2) fp64 VALU (the exact pass's arithmetic): 20 v_add_f64, 21 v_fma_f64, 22 v_mul_f64,
  *   23 v_add_f64 of a DPP row_half_mirror'd value; 1 again
- * Usage: ./pk_hazard5 [blocks] [iters] [set 0 | 1 | 2]
+ *  (set 3, round 6: the cross-lane ops the MFMA kernels still issue after their products, each
+ *   checked against the partner lane's value fetched by ds_bpermute, an LDS-path reference)
+ *   30 v_permlane16_swap of an fp32 value (no MFMA, then with); 31 v_permlane32_swap fp32;
+ *   32 / 33 v_permlane16 / 32_swap of an fp64's halves + v_add_f64 (mx_xsum64); 34 DPP row_mirror
+ *   fp32 + v_add_f32; 35 DPP quad_perm [1,0,3,2] fp32 + v_add_f32; 36 DPP row_mirror of an fp64's
+ *   halves + v_add_f64; 1 again (the known-failing packed form, as the positive control)
+ * Usage: ./pk_hazard5 [blocks] [iters] [set 0 | 1 | 2 | 3]
  * Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -o tools/probes/pk_hazard5 tools/probes/pk_hazard5.hip
  */
 #include <hip/hip_runtime.h>
@@ -154,6 +160,56 @@ __global__ __launch_bounds__(256) void k_form(unsigned *bad, int iters, float kx
             const uint64_t gb = __builtin_bit_cast(uint64_t, dd), wb = __builtin_bit_cast(uint64_t, wd);
             D = f2{__uint_as_float((uint32_t)gb), __uint_as_float((uint32_t)(gb >> 32))};
             wx = __uint_as_float((uint32_t)wb), wy = __uint_as_float((uint32_t)(wb >> 32));
+        } else if (MODE >= 30 && MODE <= 36) {   /* cross-lane ops; reference: ds_bpermute of the partner */
+            const float x = A.x;
+            const double dx = (double)A.x * 3.0 + (double)A.y;
+            const uint64_t bx = __builtin_bit_cast(uint64_t, dx);
+            const unsigned r = lane >> 4;
+            uint32_t g0 = 0, g1 = 0, w0 = 0, w1 = 0;
+            if (MODE == 30 || MODE == 31) {
+                const auto pr = MODE == 30 ? __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false)
+                                           : __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+                g0 = pr[0], g1 = pr[1];
+                const unsigned e = MODE == 30 ? ((r & 1u) ? lane - 16u : lane) : (lane & 31u);
+                const unsigned o = MODE == 30 ? ((r & 1u) ? lane : lane + 16u) : (lane | 32u);
+                w0 = (uint32_t)__shfl((int)__float_as_uint(x), (int)e, 64);
+                w1 = (uint32_t)__shfl((int)__float_as_uint(x), (int)o, 64);
+            } else if (MODE == 32 || MODE == 33) {
+                const uint32_t lo = (uint32_t)bx, hi = (uint32_t)(bx >> 32);
+                const auto l2 = MODE == 32 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                                           : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+                const auto h2 = MODE == 32 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                                           : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+                const double sum = __builtin_bit_cast(double, (uint64_t)l2[0] | ((uint64_t)h2[0] << 32)) +
+                                   __builtin_bit_cast(double, (uint64_t)l2[1] | ((uint64_t)h2[1] << 32));
+                const unsigned q = MODE == 32 ? (lane ^ 16u) : (lane ^ 32u);
+                const uint64_t pb = (uint64_t)(uint32_t)__shfl((int)lo, (int)q, 64) |
+                                    ((uint64_t)(uint32_t)__shfl((int)hi, (int)q, 64) << 32);
+                const double pd = __builtin_bit_cast(double, pb);
+                const bool first = MODE == 32 ? !(r & 1u) : lane < 32u;      /* this lane's value is the even / low one */
+                const double ws = first ? dx + pd : pd + dx;
+                const uint64_t gs = __builtin_bit_cast(uint64_t, sum), wsb = __builtin_bit_cast(uint64_t, ws);
+                g0 = (uint32_t)gs, g1 = (uint32_t)(gs >> 32), w0 = (uint32_t)wsb, w1 = (uint32_t)(wsb >> 32);
+            } else if (MODE == 34 || MODE == 35) {
+                const uint32_t m = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)__float_as_uint(x), MODE == 34 ? 0x140 : 0xB1, 0xf, 0xf, false);
+                const float sum = x + __uint_as_float(m);
+                const unsigned q = MODE == 34 ? ((lane & ~15u) | (15u - (lane & 15u))) : (lane ^ 1u);
+                const float pv = __uint_as_float((uint32_t)__shfl((int)__float_as_uint(x), (int)q, 64));
+                g0 = __float_as_uint(sum), w0 = __float_as_uint(x + pv);
+                g1 = m, w1 = __float_as_uint(pv);
+            } else {                             /* 36: fp64 row_mirror + v_add_f64 */
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)bx, 0x140, 0xf, 0xf, false);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(bx >> 32), 0x140, 0xf, 0xf, false);
+                const double sum = dx + __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+                const unsigned q = (lane & ~15u) | (15u - (lane & 15u));
+                const uint64_t pb = (uint64_t)(uint32_t)__shfl((int)(uint32_t)bx, (int)q, 64) |
+                                    ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(bx >> 32), (int)q, 64) << 32);
+                const double ws = dx + __builtin_bit_cast(double, pb);
+                const uint64_t gs = __builtin_bit_cast(uint64_t, sum), wsb = __builtin_bit_cast(uint64_t, ws);
+                g0 = (uint32_t)gs, g1 = (uint32_t)(gs >> 32), w0 = (uint32_t)wsb, w1 = (uint32_t)(wsb >> 32);
+            }
+            D = f2{__uint_as_float(g0), __uint_as_float(g1)};
+            wx = __uint_as_float(w0), wy = __uint_as_float(w1);
         } else {                                 /* 17: swap src1, both halves of B old (written one iteration early) */
             asm volatile("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(D) : "v"(A), "v"(Bold));
             wx = A.x + Bold.y, wy = A.y + Bold.x;
@@ -197,6 +253,19 @@ int main(int argc, char **argv)
         run<5>(d_bad, blocks, iters);
         run<6>(d_bad, blocks, iters);
         run<7>(d_bad, blocks, iters);
+    } else if (which == 3) {
+        run<30, false>(d_bad, blocks, iters);
+        run<30>(d_bad, blocks, iters);
+        run<31, false>(d_bad, blocks, iters);
+        run<31>(d_bad, blocks, iters);
+        run<32, false>(d_bad, blocks, iters);
+        run<32>(d_bad, blocks, iters);
+        run<33>(d_bad, blocks, iters);
+        run<34, false>(d_bad, blocks, iters);
+        run<34>(d_bad, blocks, iters);
+        run<35>(d_bad, blocks, iters);
+        run<36>(d_bad, blocks, iters);
+        run<1>(d_bad, blocks, iters);
     } else if (which == 2) {
         run<20>(d_bad, blocks, iters);
         run<21>(d_bad, blocks, iters);
