@@ -792,11 +792,11 @@ __device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t,
  * grid-stride layout drifts: instruction arbitration favours older waves,
  * profiles/r03_skeleton_wgrank.txt; the memory skeleton reads 0.72-0.76 non-persistent vs
  * 0.67-0.70 persistent, profiles/r04_*).  What a short wave needs is a cheap start:
- *   - its pixel DMA for all three steps is issued first (step k lives in slot k);
- *   - the B operands (4 KiB, quality-independent; the two Cr sets' operands merged), this quality's scale / limit table with the
- *     hot-path band limits, the zig-zag positions and the exact pass's tables are one pre-laid-out
- *     image (g_mxs_img) that the workgroup's four waves copy into LDS with LDS-DMA (16-byte
- *     pieces), one s_barrier;
+ *   - its B operands (6 KiB, quality-independent, g_mxs_B) come from global memory (L2) into
+ *     registers, then its pixel DMA for all three steps is issued (step k lives in slot k);
+ *   - this quality's scale / limit table with the hot-path band limits, the zig-zag positions and
+ *     the exact pass's tables are one pre-laid-out image (g_mxs_img) that the workgroup's four
+ *     waves copy into LDS with LDS-DMA (16-byte pieces), one s_barrier;
  *   - the exact pass runs inline per step on the stage (no cross-step queue, no side buffer).
  * vmcnt bookkeeping: every step issues exactly two DMA operations up front (padding operations
  * for general / absent steps) and three stores, so step k waits with vmcnt(2 (2 - k) + 3 k).
@@ -809,12 +809,15 @@ struct alignas(16) MxsLds {
     uint16_t task[8];                   /* inline exact batch                           */
 };
 static_assert(sizeof(MxsLds) % 16 == 0, "16-byte aligned LDS regions");
-/* the workgroup image: B operands, scale / limit table, hot-path limits (mx_limc) per lane
- * profile and column kind, zig-zag positions, the exact pass's tables (round 4b: the B operands
- * from global memory instead -- to make room -- gave wrong C rows 12..15 in 10-100 % of launches,
- * profiles/r04b_exact_pass.txt; the room comes from the compact Cr tables of MxsTab) */
+/* the B operands (round 6): read by each wave from global memory (L2) into registers at its start,
+ * [part * 3 + which] = Y|Cb, Cr set 0, Cr set 1 (zero in columns 8..15 / 0..7) -- no zeroing VALU
+ * per step, no reload after an exact pass, and a 4-KiB smaller workgroup image (rounds 4b-5 kept
+ * them in the image: 105.1 vs 106.0 us per launch on one box, profiles/r06_b_operands.txt; round 4b's
+ * wrong C rows 12..15 with B from global memory were the packed-fp32 fault of DESIGN.md 4.3f) */
+/* the workgroup image: scale / limit table, hot-path limits (mx_limc) per lane profile and column
+ * kind, zig-zag positions, the exact pass's tables */
+__device__ mx_u4 g_mxs_B[3 * JX_MX_PARTS][64];
 struct alignas(16) MxsImg {
-    mx_u4 B[2 * JX_MX_PARTS][64];       /* [part * 2 + which]: Y|Cb, the two Cr sets merged */
     MxsTab tab;
     float limc[2][16];
     uint8_t scan_t[8][8];               /* zig-zag position of (v, u) at [u][v] */
@@ -930,6 +933,11 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
     const unsigned lane = threadIdx.x & 63u;
     const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     MxsLds &L = s_lds[wave];
+    mx_u4 B[kParts][3];                          /* older than every DMA of the wave */
+#pragma unroll
+    for (int p = 0; p < kParts; p++)
+#pragma unroll
+        for (int w = 0; w < 3; w++) B[p][w] = g_mxs_B[3 * p + w][lane];
     /* the image into LDS (LDS-DMA: piece p of thread t lands at 16 p) */
     {
         const uint8_t *img = (const uint8_t *)&g_mxs_img[g.force ? 1 : 0][g.quality];
@@ -990,18 +998,6 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
             za[v] = base + 16u * ((z >> 3) ^ hs) + 2u * (z & 7u);
         }
     }
-    /* the B operands; reloaded after an exact pass, so that their registers are free during it */
-    mx_u4 B[kParts][3];
-    const auto load_b = [&](unsigned l) __attribute__((always_inline)) {
-#pragma unroll
-        for (int p = 0; p < kParts; p++) {
-            const mx_u4 bc = s_img.B[2 * p + 1][l], zero = {};
-            B[p][0] = s_img.B[2 * p][l];
-            B[p][1] = (l & 15u) < 8 ? bc : zero;
-            B[p][2] = (l & 15u) < 8 ? zero : bc;
-        }
-    };
-    load_b(lane);
     const float limc0 = s_img.limc[0][j], limc2 = s_img.limc[1][j];
     const MxsTab &tb = s_img.tab;
 
@@ -1098,7 +1094,6 @@ __global__ __launch_bounds__(64 * kMxsWPG, kWPE) void k_mxs(const jx_xform_args 
         if (__builtin_expect(__ballot(fl != 0) != 0, 0)) {
             clamp(fl);
             mx_exact_inline(L, sp, fl, xt);
-            load_b(mx_lane());
         }
         /* stores: always three store instructions (the vmcnt accounting counts on it) */
         if (early) {
@@ -2171,17 +2166,6 @@ int mx_tables_for_current_device()
                 for (int q = 1; q <= JX_MAXQ; q++) {
                     MxsImg &I = img[f * (JX_MAXQ + 1) + q];
                     const jx_mxtab &t = tab[f * (JX_MAXQ + 1) + q];
-                    for (int p = 0; p < JX_MX_PARTS; p++)
-                        for (unsigned l = 0; l < 64; l++) {
-                            /* the Cr sets' operands are zero in opposite column halves (B1 in
-                             * 8..15, B2 in 0..7): lane l keeps set (l & 15) / 8's */
-                            const bool set0 = (l & 15u) < 8;
-                            const uint16_t *keep = ops[3 * p + (set0 ? 1 : 2)][l], *zero = ops[3 * p + (set0 ? 2 : 1)][l];
-                            for (int e = 0; e < 8; e++)
-                                if (zero[e]) rc = JPGX_EARG;
-                            memcpy(&I.B[2 * p][l], ops[3 * p][l], 16);
-                            memcpy(&I.B[2 * p + 1][l], keep, 16);
-                        }
                     mx_ex_tab(I.ex, t);
                     MxTab full;
                     mx_layout_tab(full, t, [](unsigned tt, unsigned jp) { return tt < 2 ? jp : 16u + (jp & 7u); });
@@ -2197,6 +2181,13 @@ int mx_tables_for_current_device()
                     mx_scan_t(I.scan_t);
                 }
             if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs_img), img.data(), img.size() * sizeof(MxsImg)));
+            /* the Cr sets' operands are zero in opposite column halves (B1 in 8..15, B2 in 0..7):
+             * the kernel's Cr sum cr[0] + cr[1] is exact because of it */
+            for (int p = 0; p < JX_MX_PARTS; p++)
+                for (unsigned l = 0; l < 64; l++)
+                    for (int e = 0; e < 8; e++)
+                        if (ops[3 * p + ((l & 15u) < 8 ? 2 : 1)][l][e]) rc = JPGX_EARG;
+            if (!rc) rc = mx_rc(hipMemcpyToSymbol(HIP_SYMBOL(g_mxs_B), ops, sizeof(uint16_t) * 3 * JX_MX_PARTS * 64 * 8));
         }
         g_mx_rc[dev] = rc;
     });
