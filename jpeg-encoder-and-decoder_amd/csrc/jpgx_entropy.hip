@@ -169,7 +169,6 @@ __global__ __launch_bounds__(kAcT, 16 / kAcW) void k_ent_ac(const Chunks c)
     int ch;
     chunk_of(c, blockIdx.x, f, ch, k0);
     const unsigned t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    for (unsigned i = t; i < (unsigned)kBins * 32u; i += kAcT) (&cnt[0][0])[i] = 0;
     const unsigned n = min(c.nb[ch] - k0, (unsigned)kCB);
     const int16_t *z = c.coef + (f * c.fstride + c.off[ch] + k0) * 64;
     static_assert(kLoads == 16, "two halves of 64 blocks per wave");
@@ -184,6 +183,7 @@ __global__ __launch_bounds__(kAcT, 16 / kAcW) void k_ent_ac(const Chunks c)
         const unsigned blk = 8u * kLoads * wave + 64u + 8u * (unsigned)it + (lane >> 3);
         qb[it] = *(const uint4 *)(z + (size_t)(blk < n ? blk : 0u) * 64 + 8u * (lane & 7u));
     }
+    for (unsigned i = t; i < (unsigned)kBins * 32u; i += kAcT) (&cnt[0][0])[i] = 0;   /* under the loads */
     const unsigned ba = 8u * kLoads * wave + lane, bb = ba + 64u;      /* this lane's two blocks */
     uint32_t eob = 0, zcor = 0;
     long long w = 0;
@@ -217,26 +217,33 @@ __global__ __launch_bounds__(kAcT, 16 / kAcW) void k_ent_ac(const Chunks c)
         wez[wave][1] = zcor;
     }
     __syncthreads();
-    if (t <= (unsigned)kSyms) {                       /* symbol t (row 0: EOB), t == 32: ZRL */
-        uint32_t tot = 0;
-        if (t == 0) {
+    {   /* the count rows: symbol r = t / 8 (r 1..31; r 0 stands for bin 47, the ZRL row), eight
+         * threads per row summing four columns each (rotated by the row: distinct banks), then a
+         * three-step shuffle; row 0 is EOB (wez), ZRL = bin 47 minus the trailing-zero groups */
+        static_assert(kAcT == 8 * kSyms, "eight threads per count row");
+        const unsigned r = t >> 3, e = t & 7u, bin = r ? r : 47u;
+        uint32_t sum = 0;
 #pragma unroll
-            for (int i = 0; i < kAcW; i++) tot += wez[i][0];
-        } else {
-            const unsigned bin = t < (unsigned)kSyms ? t : 47u;
+        for (unsigned j = 0; j < 4; j++) sum += cnt[bin][(4u * e + j + r) & 31u];
+        sum += __shfl_xor(sum, 1, 8);
+        sum += __shfl_xor(sum, 2, 8);
+        sum += __shfl_xor(sum, 4, 8);
+        if (e == 0) {
+            if (r == 0) {
+                uint32_t eobs = 0, zc = 0;
 #pragma unroll
-            for (unsigned j = 0; j < 32; j++) tot += cnt[bin][(j + t) & 31u];     /* rotated: distinct banks */
-            if (t == (unsigned)kSyms) {
-#pragma unroll
-                for (int i = 0; i < kAcW; i++) tot -= wez[i][1];
+                for (int i = 0; i < kAcW; i++) eobs += wez[i][0], zc += wez[i][1];
+                c.cnt[blockIdx.x] = eobs;                                        /* row 0: EOB */
+                c.cnt[(size_t)kSyms * c.nchunks + blockIdx.x] = sum - zc;         /* row 32: ZRL */
+            } else {
+                c.cnt[(size_t)r * c.nchunks + blockIdx.x] = sum;
             }
-        }
-        c.cnt[(size_t)t * c.nchunks + blockIdx.x] = tot;
-    } else if (t == (unsigned)kSyms + 1) {
-        long long ws = 0;
+        } else if (t == 1) {
+            long long ws = 0;
 #pragma unroll
-        for (int i = 0; i < kAcW; i++) ws += wsum[i];
-        c.part[blockIdx.x] = ws;
+            for (int i = 0; i < kAcW; i++) ws += wsum[i];
+            c.part[blockIdx.x] = ws;
+        }
     }
 }
 
