@@ -801,7 +801,7 @@ __device__ __forceinline__ void mx_column_t(const mx_f4 (&acc)[4], const MxW &t,
  * vmcnt bookkeeping: every step issues exactly two DMA operations up front (padding operations
  * for general / absent steps) and three stores, so step k waits with vmcnt(2 (2 - k) + 3 k).
  */
-constexpr unsigned kMxsC = 3;           /* steps per wave = LDS input slots */
+constexpr unsigned kMxsC = 3;           /* steps per wave = LDS input slots (4: not faster, round 6) */
 constexpr unsigned kMxsWPG = 4;         /* waves per workgroup (one LDS image) */
 struct alignas(16) MxsLds {
     uint8_t ring[kMxsC][kSlot];         /* pixels, [y][24 jb + k]                       */
