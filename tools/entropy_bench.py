@@ -63,13 +63,16 @@ for r in range(5):
 alg = 3 * nb * (128 + 4)
 print(json.dumps({"us_per_frame": sorted(ts), "bytes_per_frame": alg,
                   "gbs_min": alg / min(ts) / 1e3, "frac_min": alg / min(ts) / 1e3 / 8000.0,
-                  "repeat_equal": same}))
+                  "repeat_equal": same,
+                  "hash": int(hist.to(torch.int64).mul(torch.arange(1, hist.numel() + 1, device=dev).view_as(hist)).sum())
+                          ^ int(dc.to(torch.int64).mul(torch.arange(1, dc.numel() + 1, device=dev).view_as(dc)).sum())}))
 '''
 
 
 def main():
     libs = sys.argv[1:] or ["product"]
     mode = os.environ.get("EB_MODE", "batch")
+    first = None
     for n in libs:
         env = dict(os.environ)
         if n != "product":
@@ -81,8 +84,10 @@ def main():
             print(n, "failed", r.stderr[-2000:])
             sys.exit(r.returncode)
         d = json.loads(r.stdout.strip().splitlines()[-1])
+        first = d["hash"] if first is None else first
         print(f"{n + ' ' + mode:18s} min {d['us_per_frame'][0]:8.1f} us/frame  med {d['us_per_frame'][2]:8.1f}  "
-              f"{d['gbs_min']:7.1f} GB/s  frac(min) {d['frac_min']:.4f}  repeat-equal={d['repeat_equal']}",
+              f"{d['gbs_min']:7.1f} GB/s  frac(min) {d['frac_min']:.4f}  repeat-equal={d['repeat_equal']}  "
+              f"same-as-first={d['hash'] == first}",
               flush=True)
 
 
