@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 import jpgx
+import oracle as O
 from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
@@ -104,6 +105,11 @@ def test_entropy_stats_stitch_across_stripes(frame):
     carry = [int(dca[c * s + s - 1]) for c in range(3)]
     dcb, hb = jpgx.entropy_stats_gpu(b, nb - s, nb - s, carry)
     dc_all = dc_all.cpu().numpy()
+    # the whole frame against the oracle: 4.19 M blocks per channel, so k_ent_dc's loop over more
+    # than 1,024 earlier chunk sums (reached above ~524 K blocks per channel) runs here
+    rdc, rhist = O.entropy_stats(out.cpu().numpy())
+    assert np.array_equal(dc_all, rdc)
+    assert np.array_equal(hist_all.cpu().numpy(), rhist)
     want_b = np.concatenate([dc_all[c * nb + s:(c + 1) * nb] for c in range(3)])
     assert np.array_equal(dcb.cpu().numpy(), want_b)
     tot = ha.cpu().numpy().astype(np.int64) + hb.cpu().numpy()
