@@ -308,6 +308,12 @@ def main():
                     help="roofline.kernel_ms from the span of the K launches / K (queue gaps "
                          "included; default) or from per-launch kernel begin/end events "
                          "(jpgx_blocks_gpu_timed, the interval rocprofv3 reports; slows the loop)")
+    ap.add_argument("--launch", choices=["eager", "graph"], default="eager",
+                    help="the K timed launches as K eager launches (default) or as one HIP graph "
+                         "(captured after the warmup, untimed; the settle and the timed region replay "
+                         "it): within the box's noise of eager (0.677-0.685 vs 0.670-0.682 of 8 TB/s "
+                         "on one box, profiles/r06_launch_gaps.txt), the queue gap being ~1 us of "
+                         "~110; --kernel-timing events implies eager")
     ap.add_argument("--frames-per-gpu", type=int, default=8)
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
@@ -413,12 +419,36 @@ def main():
         e1.record()
         cold.append((e0, e1))
     settle_steps = 0
+    # --launch graph: the K steps' launches captured once into a HIP graph after the
+    # warmup (untimed; the capture executes nothing), the settle loop then replays it, and the timed
+    # region is one more replay -- the same K launches, input sets alternating as before.  (Capture
+    # and instantiation idle the GPU for a while: without the settle after them the timed replay
+    # ran ~30 % slow, the ramp out of idle.)
+    graph, launch_mode = None, "eager"
+    if args.launch == "graph" and args.kernel_timing != "events":
+        try:
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=torch.cuda.Stream(), capture_error_mode="thread_local"):
+                for _ in range(args.steps):
+                    step()
+            launch_mode = "hip-graph"
+        except Exception as e:            # noqa: BLE001 -- fall back to eager launches, say so
+            graph, launch_mode = None, f"eager (graph capture failed: {type(e).__name__})"
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
-    while (time.perf_counter() - t_w) * 1e3 < args.settle_ms:
-        for _ in range(10):
-            step()
-        settle_steps += 10
+    t_s = time.perf_counter()
+    while True:
+        if graph is not None:
+            graph.replay()
+            settle_steps += args.steps
+        else:
+            for _ in range(10):
+                step()
+            settle_steps += 10
         torch.cuda.synchronize()
+        if (time.perf_counter() - t_s) * 1e3 >= args.settle_ms:
+            break
     cold_ms = [a.elapsed_time(b) for a, b in cold]
     # Kernel timing inside the timed region (one launch per step: the exact pass runs inside the
     # kernel).  --kernel-timing span (default): HIP events on the launch stream around the K
@@ -436,8 +466,11 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()
-    for i in range(args.steps):
-        step(kev=kevs[i] if args.kernel_timing == "events" else None)
+    if graph is not None:
+        graph.replay()
+    else:
+        for i in range(args.steps):
+            step(kev=kevs[i] if args.kernel_timing == "events" else None)
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -486,6 +519,7 @@ def main():
                                        f"{backend}: barrier, max-time, output check"),
                        "kernel_timing": ("per-launch kernel begin/end HIP events (hipExtLaunchKernel)"
                                          if launch_ms else "HIP events around the K launches on their stream"),
+                       "launch": launch_mode,
                        "input_sets": args.input_sets},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -21,11 +21,15 @@ def _line(out):
     return json.loads(lines[0])
 
 
-def test_bench_single_gpu_line():
-    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1",
+@pytest.mark.parametrize("launch", ["graph", "eager"])
+def test_bench_single_gpu_line(launch):
+    """The timed K launches as one HIP-graph replay (default) or K eager launches: either way the
+    last timed launch's output is checked against the golden hashes."""
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--launch", launch,
                         "--no-cpu-baseline"], cwd=REPO, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     d = _line(r.stdout)
+    assert d["config"]["launch"] == {"graph": "hip-graph", "eager": "eager"}[launch]
     assert KEYS <= d.keys() and d["n_gpus"] == 1
     assert d["output_check"]["ok"] and d["output_check"]["frames_checked"] == 8
     assert d["output_check"]["repeat_launches"] == 256
